@@ -1,0 +1,86 @@
+"""Build the native libraries in-tree.
+
+* ``lib/libspmm_hip.so``  — every HIP kernel in ``csrc/kernels/*.hip``,
+  compiled for gfx950 only (``hipcc --offload-arch=gfx950``), C ABI launchers.
+* ``lib/libspmm_host.so`` — the C++/OpenMP host runtime in ``csrc/host``:
+  reference-format and Matrix-Market I/O, the CPU backend.
+
+Replaces the reference's Makefile (nvcc ``-arch=sm_35`` + mpicxx, Makefile:1-26).
+Run ``python -m spmm_amd._build`` or call :func:`build`.  Rebuilds only when a
+source or header is newer than the library.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libspmm_hip.so")
+HOST_LIB = os.path.join(LIB_DIR, "libspmm_host.so")
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (need ROCm in /opt/rocm)")
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout)
+        raise RuntimeError("native build failed: " + " ".join(cmd[:4]) + " ...")
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.hpp"))
+    if force or _stale(HIP_LIB, deps):
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = HIP_LIB + ".tmp"
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-fvisibility=hidden", "-munsafe-fp-atomics", "-o", tmp] + srcs
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+        os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    deps = srcs + glob.glob(os.path.join(CSRC, "host", "*.hpp"))
+    if force or _stale(HOST_LIB, deps):
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = HOST_LIB + ".tmp"
+        cxx = os.environ.get("CXX", "g++")
+        cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fvisibility=hidden",
+               "-o", tmp] + srcs
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+        os.replace(tmp, HOST_LIB)
+    return HOST_LIB
+
+
+def build(force: bool = False, verbose: bool = False) -> None:
+    build_host(force, verbose)
+    build_hip(force, verbose)
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

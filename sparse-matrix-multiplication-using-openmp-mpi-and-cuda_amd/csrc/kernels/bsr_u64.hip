@@ -1,0 +1,232 @@
+// Block-sparse (BSR) uint64 tile-pair multiply-accumulate for gfx950.
+//
+// Capability parity: sparse_matrix_mult.cu:44-66 (matrix_multiplyKernel) plus
+// the host staging around it (:181-270).  The reference copies every (A tile,
+// B tile) pair of a round into a host staging buffer, ships it over PCIe and
+// runs one 1024-thread block per output tile with no LDS.  Here the tiles stay
+// resident in HBM and the kernel gathers them by index:
+//
+//   C[t] = (+)_{p in pairs(t), ascending middle index}  (+)_{j<k} A[pa[p]][r][j] (x) B[pb[p]][j][c]
+//
+// with the reference's wrap/collapse arithmetic (common.hpp: ref_mac) and the
+// reference's exact per-element order (pairs ascending, then j ascending), so
+// outputs are bit-identical even for adversarial values near 2^64-1.
+//
+// There is no 64-bit integer MFMA, so the exact path is a VALU kernel: per MAC
+// one v_mad_u64_u32 + two v_mul_lo_u32 + add/compare/select.  The kernel keeps
+// the VALU fed: A/B sub-tiles are staged through LDS (A padded to 33 u64 per
+// row so the 8 rows a wave reads hit distinct banks), each thread owns a
+// 1x4 strip of outputs, and the next pair's tiles are prefetched into
+// registers while the current pair is being multiplied (async-STAGE split).
+#include "common.hpp"
+
+namespace {
+
+constexpr int TS = 32;        // sub-tile edge handled by one workgroup
+constexpr int APAD = TS + 1;  // A row stride in LDS (u64), breaks the 256-B bank period
+constexpr int NT = 256;       // threads per workgroup (4 waves)
+
+// Stage one 32x32 sub-block of a k x k tile into registers.
+// FULL: k == 32, so the sub-block is the whole tile and contiguous (8 KB):
+//       each thread moves 2 x 16 B.
+// !FULL: generic k, bounds-checked element loads, zero padding (a zero term
+//       is the identity of the reference arithmetic, so padding is exact).
+template <bool FULL>
+struct Stage {
+  uint64_t a[4], b[4];
+  __device__ __forceinline__ void load(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
+                                       int k, int ti, int tj, int jc, int tid) {
+    if constexpr (FULL) {
+      const ulonglong2* A2 = reinterpret_cast<const ulonglong2*>(A);
+      const ulonglong2* B2 = reinterpret_cast<const ulonglong2*>(B);
+      ulonglong2 x0 = A2[tid], x1 = A2[tid + NT];
+      ulonglong2 y0 = B2[tid], y1 = B2[tid + NT];
+      a[0] = x0.x; a[1] = x0.y; a[2] = x1.x; a[3] = x1.y;
+      b[0] = y0.x; b[1] = y0.y; b[2] = y1.x; b[3] = y1.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        int e = tid + q * NT;          // element of the 32x32 sub-block
+        int r = e >> 5, c = e & 31;
+        int ar = ti * TS + r, ac = jc * TS + c;   // A sub-block rows ti, cols jc
+        int br = jc * TS + r, bc = tj * TS + c;   // B sub-block rows jc, cols tj
+        a[q] = (ar < k && ac < k) ? A[(int64_t)ar * k + ac] : 0ull;
+        b[q] = (br < k && bc < k) ? B[(int64_t)br * k + bc] : 0ull;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint64_t (*As)[APAD], uint64_t (*Bs)[TS], int tid) {
+    if constexpr (FULL) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int e = 2 * (tid + h * NT);
+        int r = e >> 5, c = e & 31;
+        As[r][c] = a[2 * h];
+        As[r][c + 1] = a[2 * h + 1];
+        *reinterpret_cast<ulonglong2*>(&Bs[r][c]) = make_ulonglong2(b[2 * h], b[2 * h + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        int e = tid + q * NT;
+        int r = e >> 5, c = e & 31;
+        As[r][c] = a[q];
+        Bs[r][c] = b[q];
+      }
+    }
+  }
+};
+
+template <bool FULL>
+__global__ __launch_bounds__(NT) void bsr_u64_numeric_lds(
+    const uint64_t* __restrict__ Avals, const uint64_t* __restrict__ Bvals,
+    const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
+    const int64_t* __restrict__ tile_ptr, uint64_t* __restrict__ Cvals,
+    int32_t* __restrict__ nz_flag, int k, int nsub, int64_t nwg) {
+  __shared__ uint64_t As[TS][APAD];
+  __shared__ __attribute__((aligned(16))) uint64_t Bs[TS][TS];
+
+  const int tid = threadIdx.x;
+  const int64_t wg = spmm::xcd_remap(blockIdx.x, nwg);
+  const int nsub2 = nsub * nsub;
+  const int64_t tile = wg / nsub2;
+  const int sub = (int)(wg % nsub2);
+  const int ti = sub / nsub, tj = sub % nsub;
+  const int64_t kk = (int64_t)k * k;
+
+  const int ty = tid >> 3;         // output row within the sub-tile
+  const int tx = (tid & 7) * 4;    // first of 4 output columns
+
+  uint64_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+
+  const int64_t p0 = tile_ptr[tile], p1 = tile_ptr[tile + 1];
+  Stage<FULL> st;
+  if (p0 < p1) st.load(Avals + (int64_t)pa[p0] * kk, Bvals + (int64_t)pb[p0] * kk, k, ti, tj, 0, tid);
+
+  for (int64_t p = p0; p < p1; ++p) {
+    for (int jc = 0; jc < nsub; ++jc) {
+      __syncthreads();            // previous compute finished reading LDS
+      st.store(As, Bs, tid);
+      __syncthreads();
+      // Prefetch the next (pair, j-chunk) into registers; it lands while we compute.
+      int64_t np = p;
+      int njc = jc + 1;
+      if (njc == nsub) { njc = 0; np = p + 1; }
+      if (np < p1) st.load(Avals + (int64_t)pa[np] * kk, Bvals + (int64_t)pb[np] * kk, k, ti, tj, njc, tid);
+#pragma unroll 8
+      for (int j = 0; j < TS; ++j) {
+        const uint64_t a = As[ty][j];
+        const ulonglong2 b01 = *reinterpret_cast<const ulonglong2*>(&Bs[j][tx]);
+        const ulonglong2 b23 = *reinterpret_cast<const ulonglong2*>(&Bs[j][tx + 2]);
+        acc0 = spmm::ref_mac(acc0, a, b01.x);
+        acc1 = spmm::ref_mac(acc1, a, b01.y);
+        acc2 = spmm::ref_mac(acc2, a, b23.x);
+        acc3 = spmm::ref_mac(acc3, a, b23.y);
+      }
+    }
+  }
+
+  const int orow = ti * TS + ty, ocol = tj * TS + tx;
+  uint64_t* C = Cvals + tile * kk;
+  if (FULL) {
+    ulonglong2* C2 = reinterpret_cast<ulonglong2*>(C + ty * TS + tx);
+    C2[0] = make_ulonglong2(acc0, acc1);
+    C2[1] = make_ulonglong2(acc2, acc3);
+  } else if (orow < k) {
+    if (ocol + 0 < k) C[(int64_t)orow * k + ocol + 0] = acc0;
+    if (ocol + 1 < k) C[(int64_t)orow * k + ocol + 1] = acc1;
+    if (ocol + 2 < k) C[(int64_t)orow * k + ocol + 2] = acc2;
+    if (ocol + 3 < k) C[(int64_t)orow * k + ocol + 3] = acc3;
+  }
+  // Zero-tile detection fused into the epilogue (replaces the host scan at
+  // sparse_matrix_mult.cu:577-592).  Padding lanes hold 0, so they never set it.
+  const int nz = __syncthreads_or((acc0 | acc1 | acc2 | acc3) != 0ull);
+  if (tid == 0 && nz) {
+    if (nsub == 1) nz_flag[tile] = 1;
+    else atomicOr(&nz_flag[tile], 1);
+  }
+}
+
+// Small tiles (k <= 16): k*k threads per output tile, several tiles per
+// 256-thread workgroup; tiles are small enough (<= 2 KB) that they are served
+// from L1/L2 without LDS staging.
+__global__ __launch_bounds__(NT) void bsr_u64_numeric_small(
+    const uint64_t* __restrict__ Avals, const uint64_t* __restrict__ Bvals,
+    const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
+    const int64_t* __restrict__ tile_ptr, uint64_t* __restrict__ Cvals,
+    int32_t* __restrict__ nz_flag, int k, int tiles_per_wg, int64_t ntiles) {
+  const int kk = k * k;
+  const int local = threadIdx.x / kk;
+  const int e = threadIdx.x % kk;
+  const int64_t tile = (int64_t)blockIdx.x * tiles_per_wg + local;
+  if (local >= tiles_per_wg || tile >= ntiles) return;
+  const int r = e / k, c = e % k;
+  uint64_t acc = 0;
+  const int64_t p0 = tile_ptr[tile], p1 = tile_ptr[tile + 1];
+  for (int64_t p = p0; p < p1; ++p) {
+    const uint64_t* A = Avals + (int64_t)pa[p] * kk + r * k;
+    const uint64_t* B = Bvals + (int64_t)pb[p] * kk + c;
+    for (int j = 0; j < k; ++j) acc = spmm::ref_mac(acc, A[j], B[j * k]);
+  }
+  Cvals[tile * kk + e] = acc;
+  if (acc != 0ull) nz_flag[tile] = 1;   // benign race: every writer stores 1
+}
+
+// Zero-tile scan for tiles that did not come out of the numeric kernel
+// (loaded inputs, received partials).  One wave per tile.
+__global__ __launch_bounds__(NT) void bsr_u64_nonzero(const uint64_t* __restrict__ vals, int64_t kk,
+                                                      int64_t ntiles, int32_t* __restrict__ nz_flag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (tile >= ntiles) return;
+  const uint64_t* v = vals + tile * kk;
+  uint64_t any = 0;
+  for (int64_t i = lane; i < kk; i += 64) any |= v[i];
+  const bool nz = __any(any != 0ull);
+  if (lane == 0) nz_flag[tile] = nz ? 1 : 0;
+}
+
+}  // namespace
+
+// C = A (x) B over precomputed pair lists.
+//   Avals/Bvals: [nA][k][k], [nB][k][k] uint64
+//   pa/pb:       [npairs] tile indices into A / B, grouped by output tile,
+//                ascending middle index inside a group
+//   tile_ptr:    [ntiles+1] group offsets (int64)
+//   Cvals:       [ntiles][k][k] output; nz_flag: [ntiles] int32, must be zeroed
+SPMM_EXPORT int spmm_bsr_u64_numeric(const void* Avals, const void* Bvals, const int32_t* pa,
+                                     const int32_t* pb, const int64_t* tile_ptr, void* Cvals,
+                                     int32_t* nz_flag, int k, int64_t ntiles, void* stream) {
+  if (ntiles <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t* A = (const uint64_t*)Avals;
+  const uint64_t* B = (const uint64_t*)Bvals;
+  uint64_t* C = (uint64_t*)Cvals;
+  if (k <= 16) {
+    int tpw = NT / (k * k);
+    int64_t grid = (ntiles + tpw - 1) / tpw;
+    hipLaunchKernelGGL(bsr_u64_numeric_small, dim3((unsigned)grid), dim3(NT), 0, s, A, B, pa, pb,
+                       tile_ptr, C, nz_flag, k, tpw, ntiles);
+  } else {
+    int nsub = (k + TS - 1) / TS;
+    int64_t nwg = ntiles * nsub * nsub;
+    if (k == TS)
+      hipLaunchKernelGGL(bsr_u64_numeric_lds<true>, dim3((unsigned)nwg), dim3(NT), 0, s, A, B, pa, pb,
+                         tile_ptr, C, nz_flag, k, nsub, nwg);
+    else
+      hipLaunchKernelGGL(bsr_u64_numeric_lds<false>, dim3((unsigned)nwg), dim3(NT), 0, s, A, B, pa,
+                         pb, tile_ptr, C, nz_flag, k, nsub, nwg);
+  }
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_bsr_u64_nonzero(const void* vals, int k, int64_t ntiles, int32_t* nz_flag,
+                                     void* stream) {
+  if (ntiles <= 0) return 0;
+  int64_t grid = (ntiles + 3) / 4;
+  hipLaunchKernelGGL(bsr_u64_nonzero, dim3((unsigned)grid), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint64_t*)vals, (int64_t)k * k, ntiles, nz_flag);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
