@@ -1,0 +1,342 @@
+// CSR x CSR SpGEMM (fp32) for gfx950: row-binned hash accumulation.
+//
+// North-star engine (BASELINE.json configs 2, 4, 5).  The reference has no CSR
+// path at all; its tile-level analogue is the host join + per-tile kernel of
+// sparse_matrix_mult.cu:140-253.
+//
+// Gustavson row by row, two phases:
+//   symbolic: |union of B rows selected by A(i,:)| per row -> row pointer
+//   numeric:  accumulate a(i,j) * b(j,c) per distinct c, write sorted columns
+// Rows are binned by their intermediate-product count (symbolic) or their
+// exact output count (numeric); each bin gets a kernel instantiation whose
+// per-row hash table lives in LDS (up to 16K key/value slots = 128 KiB, one
+// 1024-thread workgroup per CU).  Rows too long for LDS (R-MAT hubs) use the
+// same algorithm with the table in an HBM workspace.
+//
+// Sorted output without a sort: the hash is MONOTONE in the column,
+// h(c) = floor(c * S / ncols), with forward linear probing into an overflow
+// tail.  Then the table in slot order is sorted except inside clusters of
+// consecutive occupied slots (a key can only land in a cluster that starts at
+// or after its home slot), so one thread per cluster insertion-sorts it
+// (clusters are a few slots long at the load factors used) and an
+// order-preserving compaction emits the row sorted.  A probe that wraps past
+// the table end sets a per-row flag; the host re-sorts those rows (never
+// observed at the bin thresholds, but correctness must not depend on it).
+#include "common.hpp"
+
+namespace {
+
+constexpr int EMPTY = -1;
+
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    int s = wsum[i];
+    pre += (i < w) ? s : 0;
+    tot += s;
+  }
+  *total = tot;
+  return pre + x - v;
+}
+
+__device__ __forceinline__ uint32_t hash_mult(int64_t S, int ncols) {
+  return (S >= ncols) ? 0u : (uint32_t)(((uint64_t)S << 32) / (uint64_t)ncols);
+}
+__device__ __forceinline__ int hash_home(int c, uint32_t mult) {
+  return mult ? (int)__umulhi((uint32_t)c, mult) : c;
+}
+
+// ---------------------------------------------------------------------------
+// LDS-resident table.  S = hash range, TS = S + NT slots (the overflow tail
+// lets probes run forward without wrapping).
+template <int S, int NT, bool NUMERIC>
+__global__ __launch_bounds__(NT) void spgemm_lds(
+    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
+    const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
+    const int32_t* __restrict__ rows, int ncols, int32_t* __restrict__ row_nnz,
+    const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci, float* __restrict__ Cv,
+    int32_t* __restrict__ unsorted) {
+  constexpr int TS = S + NT;
+  constexpr int PER = TS / NT;
+  constexpr int NW = NT / 64;
+  __shared__ int keys[TS];
+  __shared__ float vals[NUMERIC ? TS : 1];
+  __shared__ int wsum[NW];
+  __shared__ int s_count, s_wrapped;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row = rows[blockIdx.x];
+  for (int s = tid; s < TS; s += NT) {
+    keys[s] = EMPTY;
+    if constexpr (NUMERIC) vals[s] = 0.f;
+  }
+  if (tid == 0) { s_count = 0; s_wrapped = 0; }
+  __syncthreads();
+
+  const uint32_t mult = hash_mult(S, ncols);
+  volatile int* vkeys = keys;
+  int mine = 0;
+  const int64_t a0 = Arp[row], a1 = Arp[row + 1];
+  for (int64_t e = a0 + w; e < a1; e += NW) {
+    const int j = Aci[e];
+    float a = 0.f;
+    if constexpr (NUMERIC) a = Av[e];
+    const int64_t b0 = Brp[j], b1 = Brp[j + 1];
+    for (int64_t f = b0 + lane; f < b1; f += 64) {
+      const int c = Bci[f];
+      float v = 0.f;
+      if constexpr (NUMERIC) v = a * Bv[f];
+      int h = hash_home(c, mult);
+      while (true) {
+        int k = vkeys[h];
+        if (k == c) break;
+        if (k == EMPTY) {
+          int old = atomicCAS(&keys[h], EMPTY, c);
+          if (old == EMPTY) { ++mine; break; }
+          if (old == c) break;
+        }
+        if (++h == TS) { h = 0; s_wrapped = 1; }
+      }
+      if constexpr (NUMERIC) atomicAdd(&vals[h], v);
+    }
+  }
+  if constexpr (!NUMERIC) {
+    if (mine) atomicAdd(&s_count, mine);
+    __syncthreads();
+    if (tid == 0) row_nnz[row] = s_count;
+    return;
+  } else {
+    __syncthreads();
+    // Sort each cluster of consecutive occupied slots (one thread per cluster).
+    for (int s = tid; s < TS; s += NT) {
+      if (keys[s] != EMPTY && (s == 0 || keys[s - 1] == EMPTY)) {
+        int e = s;
+        while (e + 1 < TS && keys[e + 1] != EMPTY) ++e;
+        for (int i = s + 1; i <= e; ++i) {
+          const int kk = keys[i];
+          const float vv = vals[i];
+          int q = i - 1;
+          while (q >= s && keys[q] > kk) { keys[q + 1] = keys[q]; vals[q + 1] = vals[q]; --q; }
+          keys[q + 1] = kk;
+          vals[q + 1] = vv;
+        }
+      }
+    }
+    __syncthreads();
+    // Order-preserving compaction: registers -> scan -> LDS front -> HBM.
+    int kb[PER];
+    float vb[PER];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      kb[q] = keys[tid * PER + q];
+      vb[q] = vals[tid * PER + q];
+      cnt += kb[q] != EMPTY;
+    }
+    int total;
+    int o = block_excl_scan<NT>(cnt, wsum, &total);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      if (kb[q] != EMPTY) { keys[o] = kb[q]; vals[o] = vb[q]; ++o; }
+    }
+    __syncthreads();
+    const int64_t base = Crp[row];
+    for (int i = tid; i < total; i += NT) {
+      Cci[base + i] = keys[i];
+      Cv[base + i] = vals[i];
+    }
+    if (tid == 0 && s_wrapped) unsorted[row] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// HBM-resident table for rows beyond the LDS bins.  One 1024-thread workgroup
+// per row; table (keys + vals, TS slots each) at ws_off[b] in the workspace,
+// pre-filled with EMPTY / 0 by the host.  Every table access is an atomic or
+// an agent-scope relaxed load, so no L1 staleness can creep in.
+constexpr int GNT = 1024;
+
+template <bool NUMERIC>
+__global__ __launch_bounds__(GNT) void spgemm_global(
+    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
+    const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
+    const int32_t* __restrict__ rows, const int64_t* __restrict__ ws_off, const int64_t* __restrict__ ws_size,
+    int32_t* __restrict__ ws_keys, float* __restrict__ ws_vals, int ncols, int32_t* __restrict__ row_nnz,
+    const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci, float* __restrict__ Cv,
+    int32_t* __restrict__ unsorted) {
+  constexpr int NW = GNT / 64;
+  __shared__ int wsum[NW];
+  __shared__ int s_count, s_wrapped;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row = rows[blockIdx.x];
+  const int64_t TS = ws_size[blockIdx.x];
+  const int64_t S = TS - GNT;
+  int32_t* keys = ws_keys + ws_off[blockIdx.x];
+  float* vals = ws_vals + ws_off[blockIdx.x];
+  if (tid == 0) { s_count = 0; s_wrapped = 0; }
+  __syncthreads();
+  const uint32_t mult = hash_mult(S, ncols);
+  int mine = 0;
+  const int64_t a0 = Arp[row], a1 = Arp[row + 1];
+  for (int64_t e = a0 + w; e < a1; e += NW) {
+    const int j = Aci[e];
+    const float a = NUMERIC ? Av[e] : 0.f;
+    for (int64_t f = Brp[j] + lane; f < Brp[j + 1]; f += 64) {
+      const int c = Bci[f];
+      int64_t h = hash_home(c, mult);
+      while (true) {
+        int k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == c) break;
+        if (k == EMPTY) {
+          int old = atomicCAS(&keys[h], EMPTY, c);
+          if (old == EMPTY) { ++mine; break; }
+          if (old == c) break;
+        }
+        if (++h == TS) { h = 0; s_wrapped = 1; }
+      }
+      if (NUMERIC) atomicAdd(&vals[h], a * Bv[f]);
+    }
+  }
+  if (!NUMERIC) {
+    if (mine) atomicAdd(&s_count, mine);
+    __syncthreads();
+    if (tid == 0) row_nnz[row] = s_count;
+    return;
+  }
+  __syncthreads();
+  auto ld = [](const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ldf = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto st = [](int32_t* p, int32_t x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto stf = [](float* p, float x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  for (int64_t s = tid; s < TS; s += GNT) {
+    if (ld(&keys[s]) != EMPTY && (s == 0 || ld(&keys[s - 1]) == EMPTY)) {
+      int64_t e = s;
+      while (e + 1 < TS && ld(&keys[e + 1]) != EMPTY) ++e;
+      for (int64_t i = s + 1; i <= e; ++i) {
+        const int kk = ld(&keys[i]);
+        const float vv = ldf(&vals[i]);
+        int64_t q = i - 1;
+        while (q >= s && ld(&keys[q]) > kk) { st(&keys[q + 1], ld(&keys[q])); stf(&vals[q + 1], ldf(&vals[q])); --q; }
+        st(&keys[q + 1], kk);
+        stf(&vals[q + 1], vv);
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t per = (TS + GNT - 1) / GNT;
+  const int64_t s0 = tid * per, s1 = (s0 + per < TS) ? s0 + per : TS;
+  int cnt = 0;
+  for (int64_t s = s0; s < s1; ++s) cnt += ld(&keys[s]) != EMPTY;
+  int total;
+  int o = block_excl_scan<GNT>(cnt, wsum, &total);
+  const int64_t base = Crp[row] + o;
+  int64_t q = 0;
+  for (int64_t s = s0; s < s1; ++s) {
+    const int k = ld(&keys[s]);
+    if (k != EMPTY) { Cci[base + q] = k; Cv[base + q] = ldf(&vals[s]); ++q; }
+  }
+  if (tid == 0 && s_wrapped) unsorted[row] = 1;
+}
+
+// nprod[i] = sum over A(i,:) of nnz(B(j,:)); one wave per row.
+__global__ __launch_bounds__(256) void spgemm_row_nprod(const int64_t* __restrict__ Arp,
+                                                        const int32_t* __restrict__ Aci,
+                                                        const int64_t* __restrict__ Brp, int64_t m,
+                                                        int64_t* __restrict__ nprod) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= m) return;
+  int64_t s = 0;
+  for (int64_t e = Arp[row] + lane; e < Arp[row + 1]; e += 64) {
+    const int j = Aci[e];
+    s += Brp[j + 1] - Brp[j];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+  if (lane == 0) nprod[row] = s;
+}
+
+template <int S, int NT, bool NUMERIC>
+int launch_lds(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
+               const float* Bv, const int32_t* rows, int64_t nrows, int ncols, int32_t* row_nnz,
+               const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* unsorted, hipStream_t s) {
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL((spgemm_lds<S, NT, NUMERIC>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp, Bci,
+                     Bv, rows, ncols, row_nnz, Crp, Cci, Cv, unsorted);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+// Bin b uses table range S = 128 << b (b = 0..8 symbolic, 0..7 numeric).
+SPMM_EXPORT int spmm_spgemm_lds_max_bin(int numeric) { return numeric ? 7 : 8; }
+
+SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, int64_t m,
+                                      int64_t* nprod, void* stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(spgemm_row_nprod, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Arp, Aci,
+                     Brp, m, nprod);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                                const int64_t* Brp, const int32_t* Bci, const float* Bv, const int32_t* rows,
+                                int64_t nrows, int ncols, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci,
+                                float* Cv, int32_t* unsorted, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define SPMM_BIN(B, S, NT)                                                                                    \
+  case B:                                                                                                      \
+    return numeric ? launch_lds<S, NT, true>(Arp, Aci, Av, Brp, Bci, Bv, rows, nrows, ncols, row_nnz, Crp,     \
+                                             Cci, Cv, unsorted, s)                                             \
+                   : launch_lds<S, NT, false>(Arp, Aci, Av, Brp, Bci, Bv, rows, nrows, ncols, row_nnz, Crp,    \
+                                              Cci, Cv, unsorted, s);
+  switch (bin) {
+    SPMM_BIN(0, 128, 64)
+    SPMM_BIN(1, 256, 64)
+    SPMM_BIN(2, 512, 128)
+    SPMM_BIN(3, 1024, 128)
+    SPMM_BIN(4, 2048, 256)
+    SPMM_BIN(5, 4096, 256)
+    SPMM_BIN(6, 8192, 512)
+    SPMM_BIN(7, 16384, 1024)
+    case 8:
+      if (numeric) return (int)hipErrorInvalidValue;
+      return launch_lds<32768, 1024, false>(Arp, Aci, Av, Brp, Bci, Bv, rows, nrows, ncols, row_nnz, Crp, Cci, Cv,
+                                            unsorted, s);
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef SPMM_BIN
+}
+
+SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                                   const int64_t* Brp, const int32_t* Bci, const float* Bv, const int32_t* rows,
+                                   int64_t nrows, const int64_t* ws_off, const int64_t* ws_size, int32_t* ws_keys,
+                                   float* ws_vals, int ncols, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci,
+                                   float* Cv, int32_t* unsorted, void* stream) {
+  if (nrows <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (numeric)
+    hipLaunchKernelGGL(spgemm_global<true>, dim3((unsigned)nrows), dim3(GNT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
+                       rows, ws_off, ws_size, ws_keys, ws_vals, ncols, row_nnz, Crp, Cci, Cv, unsorted);
+  else
+    hipLaunchKernelGGL(spgemm_global<false>, dim3((unsigned)nrows), dim3(GNT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
+                       rows, ws_off, ws_size, ws_keys, ws_vals, ncols, row_nnz, Crp, Cci, Cv, unsorted);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
