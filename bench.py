@@ -1,0 +1,197 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json metric): whole-node GFLOP/s + wall-clock of
+an n x n CSR SpGEMM at fixed density, 1D row-block over N MI355X GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Config (BASELINE.json config 4): A, B = 1M x 1M (n = 2^20) uniform random CSR
+at 0.01 % density (~105 nnz/row), fp32 values, synthetic data generated on the
+device with a row-chunk-seeded RNG, so every N multiplies the SAME matrices
+(strong scaling).  One step = all-gather of B's row panels over RCCL + local
+symbolic + numeric SpGEMM of this rank's A row panel (C stays distributed).
+FLOPs = 2 x intermediate products (BASELINE.md convention), summed over ranks;
+value = total FLOPs / max-over-ranks step time.
+
+Other workloads (--workload): ``spmm`` (65536^2 CSR x dense 128 cols, bf16,
+config 3), ``spgemm64k`` (65536^2 @ 0.1 %, config 2), ``rmat`` (R-MAT A.A^T,
+config 5), ``chain`` (the reference's block-sparse uint64 chain, report
+Table 1 Medium preset).  BASELINE.json publishes no number for the CSR
+configs, so vs_baseline is null for them; for ``chain`` it is the speed-up
+over the report's P100 kernel throughput (500 GOP/s, report.pdf p.3 §4.2).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GFLOP/s (whole node) + wall-clock, NxN SpGEMM at fixed density, 1/2/4/8 GPU"
+
+
+def _sync_barrier(comm):
+    import torch
+
+    if comm.device.type == "cuda":
+        torch.cuda.synchronize(comm.device)
+    comm.barrier()
+    if comm.device.type == "cuda":
+        torch.cuda.synchronize(comm.device)
+
+
+def _allreduce_sum(comm, x: float) -> float:
+    import torch
+    import torch.distributed as dist
+
+    if not comm.is_dist:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=comm.device if comm.backend == "nccl" else "cpu")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def run_spgemm(comm, args, n: int, density: float, model: str):
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.ops.spgemm import SpgemmInfo
+
+    prob = MS.UniformProblem.build(n, density, comm, seed=args.seed)
+    info = SpgemmInfo()
+    C = MS.rowblock_spgemm(prob.A, prob.B, comm, info)   # first (untimed) run also counts FLOPs
+    flops_local = info.flops
+    nnz_local = info.nnz
+    del C
+    step = lambda: MS.rowblock_spgemm(prob.A, prob.B, comm)  # noqa: E731
+    total_flops = _allreduce_sum(comm, flops_local)
+    total_nnz = _allreduce_sum(comm, nnz_local)
+    extra = dict(nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(total_nnz))
+    return step, total_flops, extra, dict(model=model, n=n, density=density, dtype_values="fp32",
+                                          global_batch=1, seq_len=n, parallelism=f"rowblock{comm.world}")
+
+
+def run_rmat(comm, args):
+    import torch
+
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.ops.spgemm import SpgemmInfo, spgemm
+    from spmm_amd.parallel.partition import row_panels
+    from spmm_amd.utils import gen_csr
+
+    A = gen_csr.rmat_csr(args.scale, args.edge_factor, seed=args.seed, device=comm.device)
+    At = A.transpose()
+    lo, hi = row_panels(A.m, comm.world)[comm.rank]
+    Ap = A.row_slice(lo, hi)
+    del A
+    info = SpgemmInfo()
+    C = spgemm(Ap, At, info)
+    del C
+    step = lambda: spgemm(Ap, At)  # noqa: E731
+    torch.cuda.empty_cache()
+    return step, _allreduce_sum(comm, info.flops), dict(nnz_C=int(_allreduce_sum(comm, info.nnz))), dict(
+        model=f"R-MAT scale-{args.scale} A.A^T", scale=args.scale, edge_factor=args.edge_factor, global_batch=1,
+        seq_len=1 << args.scale, parallelism=f"rowblock{comm.world}")
+
+
+def run_spmm(comm, args):
+    from spmm_amd.models import spmm as MM
+
+    step, flops, extra, cfg = MM.bench_setup(comm, n=args.spmm_n, density=args.spmm_density, cols=128,
+                                             seed=args.seed)
+    return step, flops, extra, cfg
+
+
+def run_chain(comm, args):
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "benches"))
+    from bench_chain import PRESETS, device_random_bsr
+    from spmm_amd.models.chain import ChainStats, chain_product, reduce_tree
+
+    cfg = PRESETS["medium"]
+    g = torch.Generator(device=comm.device)
+    g.manual_seed(args.seed + comm.rank)
+    mats = [device_random_bsr(cfg["blocks"], 32, cfg["density"], g, comm.device) for _ in range(cfg["n"])]
+    st = ChainStats()
+    reduce_tree(mats, 0, None, st)
+    ops = st.tile_pairs * 2 * 32 ** 3
+    step = lambda: chain_product(mats)  # noqa: E731
+    return step, _allreduce_sum(comm, ops), dict(tile_pairs=st.tile_pairs), dict(
+        model="block-sparse uint64 chain, report Medium preset (k=32, ~100k tiles/chain per GPU)", global_batch=comm.world,
+        seq_len=cfg["n"], parallelism=f"dp{comm.world}")
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="spgemm", choices=["spgemm", "spgemm64k", "spmm", "rmat", "chain"])
+    ap.add_argument("--matrix-n", dest="n", type=int, default=1 << 20)
+    ap.add_argument("--matrix-density", dest="density", type=float, default=1e-4)
+    ap.add_argument("--spmm-n", type=int, default=65536)
+    ap.add_argument("--spmm-density", type=float, default=1e-3)
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=1)
+    args = ap.parse_args()
+
+    import torch
+
+    import spmm_amd  # noqa: F401
+    from spmm_amd import _native
+    from spmm_amd.parallel import comm as CM
+
+    comm = CM.init(backend="auto", device="auto")
+    if comm.device.type == "cuda":
+        _native.hip()
+    if args.workload == "spgemm":
+        step, flops, extra, cfg = run_spgemm(comm, args, args.n, args.density,
+                                             "1Mx1M CSR SpGEMM at 0.01% density, 1D row-block via RCCL/xGMI")
+    elif args.workload == "spgemm64k":
+        step, flops, extra, cfg = run_spgemm(comm, args, 65536, 1e-3, "65536x65536 CSR SpGEMM at 0.1% density")
+    elif args.workload == "rmat":
+        step, flops, extra, cfg = run_rmat(comm, args)
+    elif args.workload == "spmm":
+        step, flops, extra, cfg = run_spmm(comm, args)
+    else:
+        step, flops, extra, cfg = run_chain(comm, args)
+
+    for _ in range(args.warmup):
+        out = step()
+        del out
+    _sync_barrier(comm)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = None
+        out = step()
+    del out
+    _sync_barrier(comm)
+    dt = comm.allreduce_max(time.perf_counter() - t0)
+    ms = dt / args.steps * 1e3
+    value = flops * args.steps / dt / 1e9
+    vs = None
+    unit = "GFLOP/s"
+    metric = METRIC
+    if args.workload == "chain":
+        unit = "GOP/s (integer, 2k^3 per tile pair)"
+        metric = "block-sparse uint64 chain product throughput (report.pdf §4.2)"
+        vs = value / (500.0 * comm.world)
+    if comm.rank == 0:
+        rec = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": comm.world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+               "scaling": "strong" if args.workload != "chain" else "weak", "vs_baseline": vs,
+               "dtype": "fp32" if args.workload in ("spgemm", "spgemm64k", "rmat") else (
+                   "bf16" if args.workload == "spmm" else "uint64"),
+               "data": "synthetic (device RNG, random values)", "config": cfg, "flops_per_step": flops,
+               "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu", **extra}
+        print(json.dumps(rec), flush=True)
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()

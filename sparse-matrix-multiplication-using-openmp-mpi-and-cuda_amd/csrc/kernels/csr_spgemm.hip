@@ -15,13 +15,13 @@
 //
 // Sorted output without a sort: the hash is MONOTONE in the column,
 // h(c) = floor(c * S / ncols), with forward linear probing into an overflow
-// tail.  Then the table in slot order is sorted except inside clusters of
-// consecutive occupied slots (a key can only land in a cluster that starts at
-// or after its home slot), so one thread per cluster insertion-sorts it
-// (clusters are a few slots long at the load factors used) and an
-// order-preserving compaction emits the row sorted.  A probe that wraps past
-// the table end sets a per-row flag; the host re-sorts those rows (never
-// observed at the bin thresholds, but correctness must not depend on it).
+// tail.  A key can only land in a cluster (run of occupied slots) that starts
+// at or after its home slot, so every key of an earlier cluster is smaller:
+// a key's output position is (#occupied slots before its cluster) + (#smaller
+// keys inside its cluster), computed independently per slot.  A probe that
+// wraps past the table end sets a per-row flag; the row is then emitted in
+// slot order and re-sorted by the host (not observed at the bin load factors,
+// but correctness does not depend on it).
 #include "common.hpp"
 
 namespace {
@@ -59,8 +59,39 @@ __device__ __forceinline__ int hash_home(int c, uint32_t mult) {
 }
 
 // ---------------------------------------------------------------------------
-// LDS-resident table.  S = hash range, TS = S + NT slots (the overflow tail
-// lets probes run forward without wrapping).
+// LDS-resident table.  S = hash range, TS = S + NT slots (the overflow tail lets
+// probes run forward without wrapping) + 4 EMPTY sentinels so cluster scans can
+// read 4 keys per step unguarded.
+//
+// Product stream: the row's A entries (<= NT per batch) are staged in LDS with
+// their B row start and an exclusive prefix of B row lengths; the row's
+// intermediate products are then split into one contiguous range per wave and
+// walked 64 at a time (lane = product), so every lane is busy whatever the B
+// row lengths, B reads are coalesced, and DEPTH blocks of loads are kept in
+// flight per wave (register ring) to cover HBM latency.
+//
+// Sorted output (numeric): position of the key in slot s = (#occupied slots
+// before its cluster) + (#keys of its cluster that are smaller) — the monotone
+// hash guarantees keys of earlier clusters are smaller.  Every occupied slot
+// computes its rank independently (no serial per-cluster sort).
+
+__device__ __forceinline__ int advance(const int* apre, int nb, int e, int p) {
+  // largest e' >= e with apre[e'] <= p  (apre[nb] > p)
+  if (apre[e + 1] > p) return e;
+  int lo = e + 1, step = 1, hi;
+  while (true) {
+    const int nx = lo + step;
+    if (nx >= nb || apre[nx] > p) { hi = nx < nb ? nx : nb; break; }
+    lo = nx;
+    step <<= 1;
+  }
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (apre[mid] <= p) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 template <int S, int NT, bool NUMERIC>
 __global__ __launch_bounds__(NT) void spgemm_lds(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
@@ -71,86 +102,152 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   constexpr int TS = S + NT;
   constexpr int PER = TS / NT;
   constexpr int NW = NT / 64;
-  __shared__ int keys[TS];
+  constexpr int ACAP = NT;
+  constexpr int DEPTH = 4;
+  __shared__ int keys[TS + 4];
   __shared__ float vals[NUMERIC ? TS : 1];
+  __shared__ int64_t abeg[ACAP];
+  __shared__ int apre[ACAP + 1];
+  __shared__ float aval[NUMERIC ? ACAP : 1];
   __shared__ int wsum[NW];
   __shared__ int s_count, s_wrapped;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int row = rows[blockIdx.x];
-  for (int s = tid; s < TS; s += NT) {
-    keys[s] = EMPTY;
-    if constexpr (NUMERIC) vals[s] = 0.f;
+  for (int s = tid; s < TS + 4; s += NT) keys[s] = EMPTY;
+  if constexpr (NUMERIC) {
+    for (int s = tid; s < TS; s += NT) vals[s] = 0.f;
   }
   if (tid == 0) { s_count = 0; s_wrapped = 0; }
-  __syncthreads();
 
   const uint32_t mult = hash_mult(S, ncols);
   volatile int* vkeys = keys;
   int mine = 0;
-  const int64_t a0 = Arp[row], a1 = Arp[row + 1];
-  for (int64_t e = a0 + w; e < a1; e += NW) {
-    const int j = Aci[e];
-    float a = 0.f;
-    if constexpr (NUMERIC) a = Av[e];
-    const int64_t b0 = Brp[j], b1 = Brp[j + 1];
-    for (int64_t f = b0 + lane; f < b1; f += 64) {
-      const int c = Bci[f];
-      float v = 0.f;
-      if constexpr (NUMERIC) v = a * Bv[f];
-      int h = hash_home(c, mult);
-      while (true) {
-        int k = vkeys[h];
-        if (k == c) break;
-        if (k == EMPTY) {
-          int old = atomicCAS(&keys[h], EMPTY, c);
-          if (old == EMPTY) { ++mine; break; }
-          if (old == c) break;
+  const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
+
+  for (int64_t bat = 0; bat < na; bat += ACAP) {
+    const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
+    __syncthreads();  // init done / previous batch consumed
+    int len = 0;
+    if (tid < nb) {
+      const int j = Aci[a0 + bat + tid];
+      const int64_t b0 = Brp[j];
+      len = (int)(Brp[j + 1] - b0);
+      abeg[tid] = b0;
+      if constexpr (NUMERIC) aval[tid] = Av[a0 + bat + tid];
+    }
+    int tot;
+    const int pre = block_excl_scan<NT>(len, wsum, &tot);
+    if (tid < nb) apre[tid] = pre;
+    if (tid == 0) apre[nb] = tot;
+    __syncthreads();
+
+    const int Q = (((tot + NW - 1) / NW) + 63) & ~63;
+    const int pbeg = w * Q;
+    const int pend = (pbeg + Q < tot) ? pbeg + Q : tot;
+    const int nblk = (pend > pbeg) ? ((pend - pbeg + 63) >> 6) : 0;
+    if (nblk > 0) {
+      int e_is = advance(apre, nb, 0, (pbeg + lane < pend) ? pbeg + lane : pend - 1);
+      int c_r[DEPTH];
+      float b_r[DEPTH], a_r[DEPTH];
+      auto issue = [&](int kk, int& c, float& b, float& a) {
+        int p = pbeg + kk * 64 + lane;
+        p = p < pend ? p : pend - 1;           // clamp: always a valid product, no branch around the load
+        e_is = advance(apre, nb, e_is, p);
+        const int64_t f = abeg[e_is] + (p - apre[e_is]);
+        c = Bci[f];
+        if constexpr (NUMERIC) { b = Bv[f]; a = aval[e_is]; }
+      };
+#pragma unroll
+      for (int u = 0; u < DEPTH; ++u)
+        if (u < nblk) issue(u, c_r[u], b_r[u], a_r[u]);
+      for (int kk = 0; kk < nblk; kk += DEPTH) {
+#pragma unroll
+        for (int u = 0; u < DEPTH; ++u) {
+          const int k = kk + u;
+          if (k < nblk) {
+            const int c = c_r[u];
+            float v = 0.f;
+            if constexpr (NUMERIC) v = a_r[u] * b_r[u];
+            const bool valid = pbeg + k * 64 + lane < pend;
+            if (k + DEPTH < nblk) issue(k + DEPTH, c_r[u], b_r[u], a_r[u]);
+            if (valid) {
+              int h = hash_home(c, mult);
+              while (true) {
+                const int kv = vkeys[h];
+                if (kv == c) break;
+                if (kv == EMPTY) {
+                  const int old = atomicCAS(&keys[h], EMPTY, c);
+                  if (old == EMPTY) { ++mine; break; }
+                  if (old == c) break;
+                }
+                if (++h == TS) { h = 0; s_wrapped = 1; }
+              }
+              if constexpr (NUMERIC) atomicAdd(&vals[h], v);
+            }
+          }
         }
-        if (++h == TS) { h = 0; s_wrapped = 1; }
       }
-      if constexpr (NUMERIC) atomicAdd(&vals[h], v);
     }
   }
+  __syncthreads();
   if constexpr (!NUMERIC) {
     if (mine) atomicAdd(&s_count, mine);
     __syncthreads();
     if (tid == 0) row_nnz[row] = s_count;
-    return;
   } else {
-    __syncthreads();
-    // Sort each cluster of consecutive occupied slots (one thread per cluster).
-    for (int s = tid; s < TS; s += NT) {
-      if (keys[s] != EMPTY && (s == 0 || keys[s - 1] == EMPTY)) {
-        int e = s;
-        while (e + 1 < TS && keys[e + 1] != EMPTY) ++e;
-        for (int i = s + 1; i <= e; ++i) {
-          const int kk = keys[i];
-          const float vv = vals[i];
-          int q = i - 1;
-          while (q >= s && keys[q] > kk) { keys[q + 1] = keys[q]; vals[q + 1] = vals[q]; --q; }
-          keys[q + 1] = kk;
-          vals[q + 1] = vv;
-        }
-      }
-    }
-    __syncthreads();
-    // Order-preserving compaction: registers -> scan -> LDS front -> HBM.
-    int kb[PER];
+    const int s0 = tid * PER;
+    int kb[PER], pos[PER];
     float vb[PER];
     int cnt = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      kb[q] = keys[tid * PER + q];
-      vb[q] = vals[tid * PER + q];
+      kb[q] = keys[s0 + q];
+      vb[q] = vals[s0 + q];
       cnt += kb[q] != EMPTY;
     }
     int total;
-    int o = block_excl_scan<NT>(cnt, wsum, &total);
+    const int P0 = block_excl_scan<NT>(cnt, wsum, &total);
+    const bool wrapped = s_wrapped != 0;
+    if (!wrapped) {
+      int cs = s0, Pcs = P0;
+      if (kb[0] != EMPTY) {
+        while (cs > 0 && keys[cs - 1] != EMPTY) --cs;
+        Pcs = P0 - (s0 - cs);
+      }
+      int lp = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        pos[q] = -1;
+        if (kb[q] != EMPTY) {
+          if (q > 0 && kb[q - 1] == EMPTY) { cs = s0 + q; Pcs = P0 + lp; }
+          const int key = kb[q];
+          int r = 0, i = cs;
+          while (true) {
+            const int k0 = keys[i], k1 = keys[i + 1], k2 = keys[i + 2], k3 = keys[i + 3];
+            if (k0 == EMPTY) break;
+            r += k0 < key;
+            if (k1 == EMPTY) break;
+            r += k1 < key;
+            if (k2 == EMPTY) break;
+            r += k2 < key;
+            if (k3 == EMPTY) break;
+            r += k3 < key;
+            i += 4;
+          }
+          pos[q] = Pcs + r;
+          ++lp;
+        }
+      }
+    } else {  // a probe wrapped: emit slot order, the host re-sorts this row
+      int lp = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) pos[q] = (kb[q] != EMPTY) ? P0 + lp++ : -1;
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      if (kb[q] != EMPTY) { keys[o] = kb[q]; vals[o] = vb[q]; ++o; }
+      if (pos[q] >= 0) { keys[pos[q]] = kb[q]; vals[pos[q]] = vb[q]; }
     }
     __syncthreads();
     const int64_t base = Crp[row];
@@ -158,7 +255,7 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
       Cci[base + i] = keys[i];
       Cv[base + i] = vals[i];
     }
-    if (tid == 0 && s_wrapped) unsorted[row] = 1;
+    if (tid == 0 && wrapped) unsorted[row] = 1;
   }
 }
 

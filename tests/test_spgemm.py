@@ -1,0 +1,156 @@
+"""CSR SpGEMM: CPU (OpenMP) and GPU (gfx950 hash kernels) against a plain
+PyTorch fp32 dense reference; generators; row-block distribution (gloo)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import spmm_amd  # noqa: F401
+from spmm_amd.ops import csr as CS
+from spmm_amd.ops import spgemm as SG
+from spmm_amd.utils import gen_csr
+
+
+def dense_ref(A, B):
+    return A.to_dense().double() @ B.to_dense().double()
+
+
+def check(C, A, B, tol=1e-4):
+    ref = dense_ref(A, B)
+    got = C.to_dense().double()
+    assert C.is_sorted()
+    assert torch.allclose(got, ref, atol=tol, rtol=1e-4), (got - ref).abs().max()
+    # exact structure: C stores exactly the structural non-zeros of A.B
+    pat = (A.to_dense() != 0).double() @ (B.to_dense() != 0).double()
+    assert C.nnz == int((pat != 0).sum())
+
+
+def test_coo_csr_roundtrip():
+    r = torch.tensor([2, 0, 2, 1, 0])
+    c = torch.tensor([1, 3, 1, 0, 0])
+    v = torch.tensor([1.0, 2.0, 3.0, 4.0, 5.0])
+    M = CS.from_coo(r, c, v, 3, 4)
+    assert M.rowptr.tolist() == [0, 2, 3, 4]
+    assert M.col.tolist() == [0, 3, 0, 1]
+    assert M.val.tolist() == [5.0, 2.0, 4.0, 4.0]
+    assert torch.equal(M.transpose().transpose().to_dense(), M.to_dense())
+
+
+def test_uniform_generator_partition_independent():
+    full = gen_csr.uniform_csr(1000, 500, 0.02, seed=5)
+    top = gen_csr.uniform_csr(1000, 500, 0.02, seed=5, rows=(0, 400))
+    bot = gen_csr.uniform_csr(1000, 500, 0.02, seed=5, rows=(400, 1000))
+    assert torch.equal(full.to_dense()[:400], top.to_dense())
+    assert torch.equal(full.to_dense()[400:], bot.to_dense())
+    assert full.is_sorted()
+    d = full.nnz / (1000 * 500)
+    assert 0.015 < d < 0.025
+
+
+def test_rmat_generator():
+    M = gen_csr.rmat_csr(10, 8, seed=1)
+    assert M.m == 1024 and M.is_sorted()
+    deg = (M.rowptr[1:] - M.rowptr[:-1]).float()
+    assert deg.max() > 4 * deg.mean()   # power-law: hubs exist
+
+
+@pytest.mark.parametrize("m,k,n,d", [(1024, 1024, 1024, 0.01), (200, 300, 150, 0.05), (64, 64, 64, 0.3)])
+def test_spgemm_cpu(m, k, n, d):
+    A = gen_csr.uniform_csr(m, k, d, seed=1)
+    B = gen_csr.uniform_csr(k, n, d, seed=2)
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, B, info)
+    check(C, A, B)
+    assert info.flops == 2 * int(SG.row_nprod(A, B).sum())
+
+
+def test_spgemm_cpu_empty_rows():
+    A = gen_csr.uniform_csr(50, 40, 0.0, seed=1)
+    B = gen_csr.uniform_csr(40, 30, 0.2, seed=2)
+    C = SG.spgemm(A, B)
+    assert C.nnz == 0 and C.rowptr.shape[0] == 51
+
+
+def _worker(rank, world, port, n, d, tmp):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.parallel import comm as CM
+
+    comm = CM.init(backend="gloo", device="cpu", timeout_s=120)
+    try:
+        prob = MS.UniformProblem.build(n, d, comm, seed=7)
+        Cp = MS.rowblock_spgemm(prob.A, prob.B, comm)
+        C = MS.gather_rows(Cp, comm)
+        if rank == 0:
+            torch.save({"rp": C.rowptr, "col": C.col, "val": C.val}, os.path.join(tmp, "C.pt"))
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rowblock_spgemm_gloo(tmp_path, world):
+    n, d = 600, 0.02
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_worker, args=(world, port, n, d, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = torch.load(os.path.join(tmp_path, "C.pt"), weights_only=True)
+    A = gen_csr.uniform_csr(n, n, d, seed=7)
+    B = gen_csr.uniform_csr(n, n, d, seed=8)
+    C = CS.CSR(n, n, got["rp"], got["col"], got["val"])
+    check(C, A, B)
+
+
+# ----------------------------------------------------------------- GPU ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n,d", [(1024, 1024, 1024, 0.01), (3000, 2000, 2500, 0.004), (500, 400, 300, 0.1),
+                                     (200, 3000, 5000, 0.03), (64, 64, 64, 0.5)])
+def test_spgemm_gpu_vs_dense(m, k, n, d):
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, k, d, seed=11, device=dev)
+    B = gen_csr.uniform_csr(k, n, d, seed=12, device=dev)
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, B, info)
+    check(C, A, B)
+    assert info.resorted_rows == 0
+
+
+@pytest.mark.gpu
+def test_spgemm_gpu_matches_cpu_structure_all_bins():
+    """Row lengths spread over every LDS bin and the HBM (global) path."""
+    dev = torch.device("cuda")
+    # rows with very different product counts: dense-ish rows hit the global bins
+    m, k, n = 700, 2000, 40000
+    A = gen_csr.uniform_csr(m, k, 0.004, seed=1)
+    # make a few heavy rows
+    heavy = gen_csr.uniform_csr(6, k, 0.9, seed=2)
+    rows = torch.cat([A.row_ids(), heavy.row_ids() + m])
+    cols = torch.cat([A.col, heavy.col]).long()
+    vals = torch.cat([A.val, heavy.val])
+    A = CS.from_coo(rows, cols, vals, m + 6, k)
+    B = gen_csr.uniform_csr(k, n, 0.01, seed=3)
+    Cc = SG.spgemm(A, B)
+    info = SG.SpgemmInfo()
+    Cg = SG.spgemm(A.to(dev), B.to(dev), info)
+    assert SG.SYM_MAX_BIN + 1 in info.rows_per_bin_sym or SG.NUM_MAX_BIN + 1 in info.rows_per_bin_num
+    assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+    assert torch.equal(Cg.col.cpu(), Cc.col)
+    assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_spgemm_gpu_rmat_aat():
+    dev = torch.device("cuda")
+    A = gen_csr.rmat_csr(12, 8, seed=2, device=dev)
+    At = A.transpose()
+    Cg = SG.spgemm(A, At)
+    Cc = SG.spgemm(A.to("cpu"), At.to("cpu"))
+    assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+    assert torch.equal(Cg.col.cpu(), Cc.col)
+    assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
