@@ -67,8 +67,9 @@ __device__ __forceinline__ int hash_home(int c, uint32_t mult) {
 // their B row start and an exclusive prefix of B row lengths; the row's
 // intermediate products are then split into one contiguous range per wave and
 // walked 64 at a time (lane = product), so every lane is busy whatever the B
-// row lengths, B reads are coalesced, and DEPTH blocks of loads are kept in
-// flight per wave (register ring) to cover HBM latency.
+// row lengths, B reads are coalesced, and D products per lane are fetched per
+// batch with the next batch's loads in flight while the current one is
+// inserted (register double buffer) to cover HBM latency.
 //
 // Sorted output (numeric): position of the key in slot s = (#occupied slots
 // before its cluster) + (#keys of its cluster that are smaller) — the monotone
@@ -103,7 +104,9 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   constexpr int PER = TS / NT;
   constexpr int NW = NT / 64;
   constexpr int ACAP = NT;
-  constexpr int DEPTH = 4;
+  // products per lane per fetch batch: deep where LDS already caps occupancy at
+  // one workgroup per CU, shallow (fewer VGPRs, more waves) for small tables
+  constexpr int D = (NT >= 512) ? (NUMERIC ? 6 : 8) : 4;
   __shared__ int keys[TS + 4];
   __shared__ float vals[NUMERIC ? TS : 1];
   __shared__ int64_t abeg[ACAP];
@@ -112,7 +115,8 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   __shared__ int wsum[NW];
   __shared__ int s_count, s_wrapped;
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int row = rows[blockIdx.x];
   for (int s = tid; s < TS + 4; s += NT) keys[s] = EMPTY;
   if constexpr (NUMERIC) {
@@ -121,7 +125,6 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   if (tid == 0) { s_count = 0; s_wrapped = 0; }
 
   const uint32_t mult = hash_mult(S, ncols);
-  volatile int* vkeys = keys;
   int mine = 0;
   const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
 
@@ -145,48 +148,60 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
     const int Q = (((tot + NW - 1) / NW) + 63) & ~63;
     const int pbeg = w * Q;
     const int pend = (pbeg + Q < tot) ? pbeg + Q : tot;
-    const int nblk = (pend > pbeg) ? ((pend - pbeg + 63) >> 6) : 0;
-    if (nblk > 0) {
-      int e_is = advance(apre, nb, 0, (pbeg + lane < pend) ? pbeg + lane : pend - 1);
-      int c_r[DEPTH];
-      float b_r[DEPTH], a_r[DEPTH];
-      auto issue = [&](int kk, int& c, float& b, float& a) {
-        int p = pbeg + kk * 64 + lane;
-        p = p < pend ? p : pend - 1;           // clamp: always a valid product, no branch around the load
-        e_is = advance(apre, nb, e_is, p);
-        const int64_t f = abeg[e_is] + (p - apre[e_is]);
-        c = Bci[f];
-        if constexpr (NUMERIC) { b = Bv[f]; a = aval[e_is]; }
+    // Batches of D products per lane (lane-strided by 64: coalesced B reads),
+    // double-buffered: the loads of batch t+1 are issued before batch t is
+    // inserted.  All loads are unconditional (addresses clamped to a valid
+    // product) and all branches around them wave-uniform, so the compiler
+    // emits a counted vmcnt instead of draining per load.
+    const int nbat = (pend > pbeg) ? (pend - pbeg + 64 * D - 1) / (64 * D) : 0;
+    if (nbat > 0) {
+      int e_is = 0;
+      int cA[D], cB[D];
+      float bA[D], bB[D], aA[D], aB[D];
+      auto fetch = [&](int bt, int (&c)[D], float (&bv)[D], float (&av)[D]) {
+        int64_t f[D];
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+          int pp = pbeg + (bt * D + u) * 64 + lane;
+          pp = pp < pend ? pp : pend - 1;
+          e_is = advance(apre, nb, e_is, pp);
+          f[u] = abeg[e_is] + (pp - apre[e_is]);
+          if constexpr (NUMERIC) av[u] = aval[e_is];
+        }
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+          c[u] = Bci[f[u]];
+          if constexpr (NUMERIC) bv[u] = Bv[f[u]];
+        }
       };
+      auto consume = [&](int bt, const int (&c)[D], const float (&bv)[D], const float (&av)[D]) {
 #pragma unroll
-      for (int u = 0; u < DEPTH; ++u)
-        if (u < nblk) issue(u, c_r[u], b_r[u], a_r[u]);
-      for (int kk = 0; kk < nblk; kk += DEPTH) {
-#pragma unroll
-        for (int u = 0; u < DEPTH; ++u) {
-          const int k = kk + u;
-          if (k < nblk) {
-            const int c = c_r[u];
-            float v = 0.f;
-            if constexpr (NUMERIC) v = a_r[u] * b_r[u];
-            const bool valid = pbeg + k * 64 + lane < pend;
-            if (k + DEPTH < nblk) issue(k + DEPTH, c_r[u], b_r[u], a_r[u]);
-            if (valid) {
-              int h = hash_home(c, mult);
-              while (true) {
-                const int kv = vkeys[h];
-                if (kv == c) break;
-                if (kv == EMPTY) {
-                  const int old = atomicCAS(&keys[h], EMPTY, c);
-                  if (old == EMPTY) { ++mine; break; }
-                  if (old == c) break;
-                }
-                if (++h == TS) { h = 0; s_wrapped = 1; }
+        for (int u = 0; u < D; ++u) {
+          if (pbeg + (bt * D + u) * 64 + lane < pend) {
+            const int key = c[u];
+            int h = hash_home(key, mult);
+            while (true) {
+              // LDS-typed relaxed load (a volatile generic pointer would become a
+              // flat_load, whose vmcnt(0) drains the prefetched B loads)
+              const int kv = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (kv == key) break;
+              if (kv == EMPTY) {
+                const int old = atomicCAS(&keys[h], EMPTY, key);
+                if (old == EMPTY) { ++mine; break; }
+                if (old == key) break;
               }
-              if constexpr (NUMERIC) atomicAdd(&vals[h], v);
+              if (++h == TS) { h = 0; s_wrapped = 1; }
             }
+            if constexpr (NUMERIC) atomicAdd(&vals[h], av[u] * bv[u]);
           }
         }
+      };
+      fetch(0, cA, bA, aA);
+      for (int bt = 0; bt < nbat; bt += 2) {
+        fetch(bt + 1, cB, bB, aB);
+        consume(bt, cA, bA, aA);
+        fetch(bt + 2, cA, bA, aA);
+        consume(bt + 1, cB, bB, aB);
       }
     }
   }

@@ -1,0 +1,117 @@
+"""Distributed SpMM over RCCL / xGMI: Y = A . X, A sparse (bf16), X dense [n, D].
+
+Two decompositions (north-star: "all-gather of B row panels plus
+reduce-scatter of C"):
+
+* ``rowblock_spmm`` — rank r holds A's row panel r and X's row panel r;
+  X is all-gathered (ring over xGMI), Y's row panel is computed locally.
+  Communication: (P-1)/P * n * D * 2 B per rank.
+* ``innerdim_spmm`` — rank r holds A's COLUMN panel r (all rows) and X's
+  row panel r; each rank computes a full-height fp32 partial Y_r = A[:, r] .
+  X_r, and a reduce-scatter sums the partials into row panels.
+  Communication: (P-1)/P * m * D * 4 B per rank, no X replication — the
+  right choice when X (n x D) is much larger than Y, or X cannot be
+  replicated.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops.csr import CSR, from_coo
+from ..ops.spmm import PanelPlan, plan_panels, spmm
+from ..parallel.comm import Comm
+from ..parallel.partition import row_panels
+from ..utils.gen_csr import uniform_csr
+
+
+def allgather_rows(Xp: torch.Tensor, comm: Comm, counts) -> torch.Tensor:
+    """Concatenate row panels of a dense matrix (uneven panels padded)."""
+    if not comm.is_dist:
+        return Xp
+    mx = max(counts)
+    wd = Xp.device if comm.backend == "nccl" else torch.device("cpu")
+    buf = torch.zeros((mx, Xp.shape[1]), dtype=Xp.dtype, device=wd)
+    buf[:Xp.shape[0]] = Xp.to(wd)
+    if comm.backend == "nccl":
+        out = torch.empty((comm.world * mx, Xp.shape[1]), dtype=Xp.dtype, device=wd)
+        dist.all_gather_into_tensor(out, buf)
+        parts = list(out.view(comm.world, mx, -1))
+    else:
+        parts = [torch.empty_like(buf) for _ in range(comm.world)]
+        dist.all_gather(parts, buf)
+    if all(c == mx for c in counts):
+        return torch.cat(parts).to(Xp.device)
+    return torch.cat([parts[r][:counts[r]] for r in range(comm.world)]).to(Xp.device)
+
+
+def rowblock_spmm(A_panel: CSR, X_panel: torch.Tensor, comm: Comm, counts, plan: Optional[PanelPlan] = None,
+                  method: str = "auto", out_dtype=torch.float32) -> torch.Tensor:
+    X = allgather_rows(X_panel, comm, counts)
+    return spmm(A_panel, X, out_dtype=out_dtype, method=method, plan=plan)
+
+
+def innerdim_spmm(A_colpanel: CSR, X_panel: torch.Tensor, comm: Comm, row_counts, method: str = "auto",
+                  plan: Optional[PanelPlan] = None) -> torch.Tensor:
+    """A_colpanel: all m rows, columns of this rank's panel (re-indexed from 0).
+    Returns this rank's fp32 row panel of Y."""
+    Yp = spmm(A_colpanel, X_panel, out_dtype=torch.float32, method=method, plan=plan)
+    if not comm.is_dist:
+        return Yp
+    mx = max(row_counts)
+    wd = Yp.device if comm.backend == "nccl" else torch.device("cpu")
+    D = Yp.shape[1]
+    full = torch.zeros((comm.world * mx, D), dtype=torch.float32, device=wd)
+    off = 0
+    for r, c in enumerate(row_counts):
+        full[r * mx:r * mx + c] = Yp[off:off + c].to(wd)
+        off += c
+    out = torch.empty((mx, D), dtype=torch.float32, device=wd)
+    if comm.backend == "nccl":
+        dist.reduce_scatter_tensor(out, full)
+    else:
+        _gloo_reduce_scatter(out, full, comm, mx)
+    return out[:row_counts[comm.rank]].to(Yp.device)
+
+
+def _gloo_reduce_scatter(out, full, comm: Comm, mx: int) -> None:
+    # gloo has no reduce_scatter: all_reduce then keep this rank's block
+    dist.all_reduce(full)
+    out.copy_(full[comm.rank * mx:(comm.rank + 1) * mx])
+
+
+def column_panel(A: CSR, lo: int, hi: int) -> CSR:
+    """Columns [lo, hi) of A, re-indexed to start at 0 (all rows kept)."""
+    r = A.row_ids()
+    sel = (A.col >= lo) & (A.col < hi)
+    return from_coo(r[sel], (A.col[sel] - lo).long(), A.val[sel], A.m, hi - lo, sum_duplicates=False,
+                    dtype=A.val.dtype)
+
+
+def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 128, seed: int = 1,
+                method: str = "mfma"):
+    """BASELINE config 3: 65536^2 CSR (bf16) x dense [65536, 128] (bf16).
+    One step = all-gather of X row panels (P > 1) + SpMM of this rank's rows."""
+    panels = row_panels(n, comm.world)
+    lo, hi = panels[comm.rank]
+    A = uniform_csr(n, n, density, seed=seed, device=comm.device, rows=(lo, hi), dtype=torch.bfloat16)
+    g = torch.Generator(device=comm.device)
+    g.manual_seed(seed * 31 + comm.rank)
+    Xp = (torch.rand((hi - lo, cols), generator=g, device=comm.device) * 2 - 1).to(torch.bfloat16)
+    counts = [b - a for a, b in panels]
+    plan = plan_panels(A) if comm.device.type == "cuda" and method == "mfma" else None
+    step = lambda: rowblock_spmm(A, Xp, comm, counts, plan=plan, method=method if plan is not None else "auto")  # noqa: E731
+    flops_local = 2.0 * A.nnz * cols
+    if comm.is_dist:
+        t = torch.tensor([flops_local], dtype=torch.float64,
+                         device=comm.device if comm.backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        flops = float(t.item())
+    else:
+        flops = flops_local
+    extra = dict(nnz_A=int(A.nnz), spmm_method=method, panel_reuse=(plan.reuse if plan is not None else None))
+    cfg = dict(model=f"{n}x{n} CSR SpMM (sparse x dense {cols}-col) at {density * 100:g}% density, bf16 MFMA",
+               n=n, density=density, cols=cols, global_batch=1, seq_len=n, parallelism=f"rowblock{comm.world}")
+    return step, flops, extra, cfg

@@ -1,0 +1,128 @@
+"""CSR x dense SpMM: Y = A . X  (A bf16 CSR, X bf16 [n, D], fp32 accumulate).
+
+Two gfx950 kernels (``csrc/kernels/csr_spmm.hip``):
+
+* ``mfma``    — panel kernel: an inspector (:func:`plan_panels`, run once per
+  matrix) lists each 64-row panel's sorted union of columns in chunks of 64;
+  the kernel gathers each chunk's X rows into LDS once, scatters the chunk's
+  entries into a dense 64x64 A tile and runs v_mfma_f32_16x16x32_bf16.
+  X rows shared by several rows of a panel are fetched once.
+* ``rowwise`` — VALU row-gather kernel, no inspector; one wave per row.
+
+``auto`` picks ``mfma`` when the panel column reuse (nnz / union columns) is
+at least ``MFMA_MIN_REUSE`` — i.e. when the MFMA path moves fewer bytes —
+and ``rowwise`` otherwise.  CPU tensors use the OpenMP kernel.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .. import _native
+from .._native import c_vp
+from .csr import CSR
+
+_native.register_hip("spmm_spmm_panel_mfma", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64,
+                     c_vp, C.c_int64, C.c_int, c_vp)
+_native.register_hip("spmm_spmm_rowwise", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp,
+                     C.c_int64, C.c_int, c_vp)
+
+PANEL = 64
+CHUNK = 64
+MFMA_MIN_REUSE = 1.15
+
+
+@dataclass
+class PanelPlan:
+    m: int
+    n: int
+    panel_chunk_ptr: torch.Tensor   # int64 [npanels + 1]
+    chunk_cols: torch.Tensor        # int32 [nchunks * 64], -1 = padding
+    chunk_ent_ptr: torch.Tensor     # int64 [nchunks + 1]
+    ent_rc: torch.Tensor            # int32 [nnz]: row_in_panel * 64 + slot
+    ent_val: torch.Tensor           # bf16 [nnz]
+    union_cols: int                 # X rows gathered per pass (sum over panels)
+    nnz: int
+
+    @property
+    def reuse(self) -> float:
+        return self.nnz / max(self.union_cols, 1)
+
+
+def plan_panels(A: CSR) -> PanelPlan:
+    """Inspector for the MFMA kernel (device-side torch ops, done once)."""
+    dev = A.device
+    n = A.n
+    npan = (A.m + PANEL - 1) // PANEL
+    r = A.row_ids()
+    p = torch.div(r, PANEL, rounding_mode="floor")
+    key, perm = torch.sort(p * n + A.col.long(), stable=True)
+    r, p = r[perm], p[perm]
+    vals = A.val[perm].to(torch.bfloat16)
+    uniq, inv = torch.unique_consecutive(key, return_inverse=True)
+    up = torch.div(uniq, n, rounding_mode="floor")
+    ucol = uniq - up * n
+    ucount = torch.bincount(up, minlength=npan)
+    ustart = torch.cumsum(ucount, 0) - ucount
+    uidx = torch.arange(uniq.numel(), device=dev) - ustart[up]
+    nch = torch.div(ucount + CHUNK - 1, CHUNK, rounding_mode="floor")
+    chend = torch.cumsum(nch, 0)
+    chstart = chend - nch
+    total_ch = int(chend[-1]) if npan else 0
+    panel_chunk_ptr = torch.zeros(npan + 1, dtype=torch.int64, device=dev)
+    panel_chunk_ptr[1:] = chend
+    chunk_cols = torch.full((total_ch * CHUNK,), -1, dtype=torch.int32, device=dev)
+    chunk_cols[chstart[up] * CHUNK + uidx] = ucol.to(torch.int32)
+    e_upos = uidx[inv]
+    e_chunk = chstart[p] + torch.div(e_upos, CHUNK, rounding_mode="floor")
+    ent_rc = ((r - p * PANEL) * CHUNK + e_upos % CHUNK).to(torch.int32)
+    chunk_ent_ptr = torch.zeros(total_ch + 1, dtype=torch.int64, device=dev)
+    if total_ch:
+        torch.cumsum(torch.bincount(e_chunk, minlength=total_ch), 0, out=chunk_ent_ptr[1:])
+    return PanelPlan(A.m, n, panel_chunk_ptr, chunk_cols, chunk_ent_ptr, ent_rc.contiguous(), vals.contiguous(),
+                     int(uniq.numel()), A.nnz)
+
+
+def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
+         plan: Optional[PanelPlan] = None) -> torch.Tensor:
+    if X.dim() != 2 or X.shape[0] != A.n:
+        raise ValueError(f"X must be [{A.n}, D], got {tuple(X.shape)}")
+    D = X.shape[1]
+    dev = A.device
+    if dev.type != "cuda":
+        Af = A.val.float().contiguous()
+        Xf = X.float().contiguous()
+        Y = torch.empty((A.m, D), dtype=torch.float32)
+        _native.host().spmm_cpu_csr_spmm(A.m, D, _native.ptr(A.rowptr), _native.ptr(A.col), _native.ptr(Af),
+                                         _native.ptr(Xf), _native.ptr(Y), 0)
+        return Y.to(out_dtype)
+    X = X.to(torch.bfloat16).contiguous()
+    Y = torch.empty((A.m, D), dtype=out_dtype, device=dev)
+    out_bf16 = 1 if out_dtype == torch.bfloat16 else 0
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("out_dtype must be float32 or bfloat16")
+    P = _native.ptr
+    lib = _native.hip()
+    stream = _native.stream_ptr(dev)
+    if method == "auto":
+        if D % 128 == 0 and (plan is not None and plan.reuse >= MFMA_MIN_REUSE):
+            method = "mfma"
+        else:
+            method = "rowwise"
+    if method == "mfma":
+        if D % 128 != 0:
+            raise ValueError("MFMA SpMM needs D % 128 == 0")
+        plan = plan if plan is not None else plan_panels(A)
+        _native.check(lib.spmm_spmm_panel_mfma(P(plan.panel_chunk_ptr), P(plan.chunk_cols), P(plan.chunk_ent_ptr),
+                                               P(plan.ent_rc), P(plan.ent_val), P(X), D, A.m, D, P(Y), D, out_bf16,
+                                               stream), "spmm_panel_mfma")
+    elif method == "rowwise":
+        av = A.val.to(torch.bfloat16).contiguous()
+        _native.check(lib.spmm_spmm_rowwise(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, D, P(Y), D, out_bf16,
+                                            stream), "spmm_rowwise")
+    else:
+        raise ValueError(f"unknown method {method!r}")
+    return Y

@@ -1,0 +1,118 @@
+"""SpMM: CPU / GPU (rowwise VALU and MFMA panel kernels) against a plain
+PyTorch fp32 reference on the same bf16-rounded inputs; inspector invariants;
+row-block (all-gather) and inner-dimension (reduce-scatter) decompositions."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import spmm_amd  # noqa: F401
+from spmm_amd.ops import csr as CS
+from spmm_amd.ops import spmm as SM
+from spmm_amd.utils import gen_csr
+
+
+def ref(A, X):
+    return A.to_dense(torch.float32) @ X.float()
+
+
+def test_spmm_cpu():
+    A = gen_csr.uniform_csr(300, 200, 0.05, seed=1, dtype=torch.bfloat16)
+    X = torch.randn(200, 64).to(torch.bfloat16)
+    Y = SM.spmm(A, X)
+    assert torch.allclose(Y, ref(A, X), atol=1e-4, rtol=1e-4)
+
+
+def test_plan_panels_invariants():
+    A = gen_csr.uniform_csr(200, 500, 0.05, seed=2, dtype=torch.bfloat16)
+    P = SM.plan_panels(A)
+    assert P.nnz == A.nnz
+    assert int(P.chunk_ent_ptr[-1]) == A.nnz
+    # reconstruct A from the plan
+    dense = torch.zeros(A.m, A.n)
+    cc = P.chunk_cols
+    npan = P.panel_chunk_ptr.numel() - 1
+    for p in range(npan):
+        for ch in range(int(P.panel_chunk_ptr[p]), int(P.panel_chunk_ptr[p + 1])):
+            for e in range(int(P.chunk_ent_ptr[ch]), int(P.chunk_ent_ptr[ch + 1])):
+                rc = int(P.ent_rc[e])
+                row = p * 64 + rc // 64
+                col = int(cc[ch * 64 + rc % 64])
+                dense[row, col] += float(P.ent_val[e])
+    assert torch.equal(dense, A.to_dense())
+    assert P.union_cols <= A.nnz
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, tmp):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from spmm_amd.models import spmm as MM
+    from spmm_amd.parallel import comm as CM
+    from spmm_amd.parallel.partition import row_panels
+
+    comm = CM.init(backend="gloo", device="cpu", timeout_s=120)
+    try:
+        m, n, D = 150, 130, 16
+        A = gen_csr.uniform_csr(m, n, 0.08, seed=5, dtype=torch.bfloat16)
+        X = (torch.arange(n * D, dtype=torch.float32).view(n, D) % 7 - 3).to(torch.bfloat16)
+        rp = row_panels(m, world)
+        xp = row_panels(n, world)
+        lo, hi = rp[rank]
+        xlo, xhi = xp[rank]
+        Y1 = MM.rowblock_spmm(A.row_slice(lo, hi), X[xlo:xhi], comm, [b - a for a, b in xp])
+        Acol = MM.column_panel(A, xlo, xhi)
+        Y2 = MM.innerdim_spmm(Acol, X[xlo:xhi], comm, [b - a for a, b in rp])
+        torch.save({"y1": Y1, "y2": Y2}, os.path.join(tmp, f"y{rank}.pt"))
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_spmm_gloo(tmp_path, world):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    m, n, D = 150, 130, 16
+    A = gen_csr.uniform_csr(m, n, 0.08, seed=5, dtype=torch.bfloat16)
+    X = (torch.arange(n * D, dtype=torch.float32).view(n, D) % 7 - 3).to(torch.bfloat16)
+    want = ref(A, X)
+    parts = [torch.load(os.path.join(tmp_path, f"y{r}.pt"), weights_only=True) for r in range(world)]
+    assert torch.allclose(torch.cat([p["y1"] for p in parts]), want, atol=1e-4)
+    assert torch.allclose(torch.cat([p["y2"] for p in parts]), want, atol=1e-4)
+
+
+# ----------------------------------------------------------------- GPU ----
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["rowwise", "mfma"])
+@pytest.mark.parametrize("m,n,D,d", [(1000, 800, 128, 0.02), (333, 4096, 256, 0.01), (64, 64, 128, 0.5),
+                                     (4097, 300, 128, 0.05)])
+def test_spmm_gpu(method, m, n, D, d):
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, n, d, seed=3, device=dev, dtype=torch.bfloat16)
+    X = torch.randn(n, D, device=dev).to(torch.bfloat16)
+    Y = SM.spmm(A, X, method=method)
+    R = ref(A, X)
+    assert torch.allclose(Y, R, atol=2e-3, rtol=2e-3), (Y - R).abs().max()
+    Yb = SM.spmm(A, X, method=method, out_dtype=torch.bfloat16)
+    assert torch.allclose(Yb.float(), R, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_spmm_mfma_exact_small_integers():
+    """Exact integer data catches any fragment-layout / transpose mistake."""
+    dev = torch.device("cuda")
+    m, n, D = 130, 200, 128
+    A = gen_csr.uniform_csr(m, n, 0.1, seed=9, device=dev, values="small_int", dtype=torch.bfloat16)
+    X = (torch.arange(n * D, device=dev).view(n, D) % 11 - 5).to(torch.bfloat16)
+    Y = SM.spmm(A, X, method="mfma")
+    assert torch.equal(Y, ref(A, X))
