@@ -28,6 +28,20 @@ namespace {
 
 constexpr int EMPTY = -1;
 
+// Diagnostic phase stamps (off unless the host sets g_stamp_on): thread 0 of
+// every workgroup adds the shader-clock cycles of each phase, measured between
+// the workgroup barriers that delimit it.  Read with spmm_spgemm_stamps().
+__device__ int g_stamp_on = 0;
+__device__ unsigned long long g_stamps[8];
+#define SPMM_STAMP(i)                                                              \
+  do {                                                                             \
+    if (stamp_on && threadIdx.x == 0) {                                            \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
+      atomicAdd(&g_stamps[i], _t - t_prev);                                        \
+      t_prev = _t;                                                                 \
+    }                                                                              \
+  } while (0)
+
 template <int NT>
 __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* total) {
   constexpr int NW = NT / 64;
@@ -93,21 +107,22 @@ __device__ __forceinline__ int advance(const int* apre, int nb, int e, int p) {
   return lo;
 }
 
-template <int S, int NT, bool NUMERIC>
+template <int S, int NT, bool NUMERIC, int NP>
 __global__ __launch_bounds__(NT) void spgemm_lds(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
     const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
-    const int32_t* __restrict__ rows, int ncols, int32_t* __restrict__ row_nnz,
-    const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci, float* __restrict__ Cv,
-    int32_t* __restrict__ unsorted) {
-  constexpr int TS = S + NT;
+    const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols,
+    int32_t* __restrict__ row_nnz, const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci,
+    float* __restrict__ Cv, int32_t* __restrict__ flags) {
+  constexpr int TS = S + NT;            // multiple of 4 (S, NT powers of two >= 64)
   constexpr int PER = TS / NT;
   constexpr int NW = NT / 64;
   constexpr int ACAP = NT;
+  constexpr int QSTEP = 4 / NP;         // quarters per column slice
   // products per lane per fetch batch: deep where LDS already caps occupancy at
   // one workgroup per CU, shallow (fewer VGPRs, more waves) for small tables
-  constexpr int D = (NT >= 512) ? (NUMERIC ? 6 : 8) : 4;
-  __shared__ int keys[TS + 4];
+  constexpr int D = NUMERIC ? 4 : ((NT >= 512) ? 8 : 4);
+  __shared__ __attribute__((aligned(16))) int keys[TS + 4];
   __shared__ float vals[NUMERIC ? TS : 1];
   __shared__ int64_t abeg[ACAP];
   __shared__ int apre[ACAP + 1];
@@ -118,159 +133,274 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int row = rows[blockIdx.x];
-  for (int s = tid; s < TS + 4; s += NT) keys[s] = EMPTY;
-  if constexpr (NUMERIC) {
-    for (int s = tid; s < TS; s += NT) vals[s] = 0.f;
-  }
-  if (tid == 0) { s_count = 0; s_wrapped = 0; }
-
-  const uint32_t mult = hash_mult(S, ncols);
-  int mine = 0;
   const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
+  const int stamp_on = g_stamp_on;
+  unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;
+  int written = 0;      // numeric: entries of earlier slices already stored
+  int row_count = 0;    // symbolic: distinct columns over all slices
 
-  for (int64_t bat = 0; bat < na; bat += ACAP) {
-    const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
-    __syncthreads();  // init done / previous batch consumed
-    int len = 0;
-    if (tid < nb) {
-      const int j = Aci[a0 + bat + tid];
-      const int64_t b0 = Brp[j];
-      len = (int)(Brp[j + 1] - b0);
-      abeg[tid] = b0;
-      if constexpr (NUMERIC) aval[tid] = Av[a0 + bat + tid];
+  for (int sl = 0; sl < NP; ++sl) {
+    // column slice [clo, chi) and its monotone hash
+    const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
+    const int clo = (int)(((int64_t)q0 * ncols) >> 2), chi = (int)(((int64_t)q1 * ncols) >> 2);
+    const uint32_t mult = hash_mult(S, chi - clo);
+    for (int i = tid; i < (TS + 4) / 4; i += NT) reinterpret_cast<int4*>(keys)[i] = make_int4(EMPTY, EMPTY, EMPTY, EMPTY);
+    if constexpr (NUMERIC) {
+      for (int i = tid; i < TS; i += NT) vals[i] = 0.f;
     }
-    int tot;
-    const int pre = block_excl_scan<NT>(len, wsum, &tot);
-    if (tid < nb) apre[tid] = pre;
-    if (tid == 0) apre[nb] = tot;
-    __syncthreads();
+    if (tid == 0) { s_count = 0; s_wrapped = 0; }
+    int mine = 0;
+    int64_t slice_products = 0;
+    bool overflow = false;
 
-    const int Q = (((tot + NW - 1) / NW) + 63) & ~63;
-    const int pbeg = w * Q;
-    const int pend = (pbeg + Q < tot) ? pbeg + Q : tot;
-    // Batches of D products per lane (lane-strided by 64: coalesced B reads),
-    // double-buffered: the loads of batch t+1 are issued before batch t is
-    // inserted.  All loads are unconditional (addresses clamped to a valid
-    // product) and all branches around them wave-uniform, so the compiler
-    // emits a counted vmcnt instead of draining per load.
-    const int nbat = (pend > pbeg) ? (pend - pbeg + 64 * D - 1) / (64 * D) : 0;
-    if (nbat > 0) {
-      int e_is = 0;
-      int cA[D], cB[D];
-      float bA[D], bB[D], aA[D], aB[D];
-      auto fetch = [&](int bt, int (&c)[D], float (&bv)[D], float (&av)[D]) {
-        int64_t f[D];
-#pragma unroll
-        for (int u = 0; u < D; ++u) {
-          int pp = pbeg + (bt * D + u) * 64 + lane;
-          pp = pp < pend ? pp : pend - 1;
-          e_is = advance(apre, nb, e_is, pp);
-          f[u] = abeg[e_is] + (pp - apre[e_is]);
-          if constexpr (NUMERIC) av[u] = aval[e_is];
-        }
-#pragma unroll
-        for (int u = 0; u < D; ++u) {
-          c[u] = Bci[f[u]];
-          if constexpr (NUMERIC) bv[u] = Bv[f[u]];
-        }
-      };
-      auto consume = [&](int bt, const int (&c)[D], const float (&bv)[D], const float (&av)[D]) {
-#pragma unroll
-        for (int u = 0; u < D; ++u) {
-          if (pbeg + (bt * D + u) * 64 + lane < pend) {
-            const int key = c[u];
-            int h = hash_home(key, mult);
-            while (true) {
-              // LDS-typed relaxed load (a volatile generic pointer would become a
-              // flat_load, whose vmcnt(0) drains the prefetched B loads)
-              const int kv = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (kv == key) break;
-              if (kv == EMPTY) {
-                const int old = atomicCAS(&keys[h], EMPTY, key);
-                if (old == EMPTY) { ++mine; break; }
-                if (old == key) break;
-              }
-              if (++h == TS) { h = 0; s_wrapped = 1; }
-            }
-            if constexpr (NUMERIC) atomicAdd(&vals[h], av[u] * bv[u]);
-          }
-        }
-      };
-      fetch(0, cA, bA, aA);
-      for (int bt = 0; bt < nbat; bt += 2) {
-        fetch(bt + 1, cB, bB, aB);
-        consume(bt, cA, bA, aA);
-        fetch(bt + 2, cA, bA, aA);
-        consume(bt + 1, cB, bB, aB);
+    for (int64_t bat = 0; bat < na; bat += ACAP) {
+      const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
+      __syncthreads();  // init done / previous batch consumed
+      int len = 0;
+      if (tid < nb) {
+        const int j = Aci[a0 + bat + tid];
+        const int64_t rb = Brp[j], re = Brp[j + 1];
+        const int64_t b0 = (NP == 1 || q0 == 0) ? rb : bsplit[(int64_t)j * 3 + q0 - 1];
+        const int64_t b1 = (NP == 1 || q1 == 4) ? re : bsplit[(int64_t)j * 3 + q1 - 1];
+        len = (int)(b1 - b0);
+        abeg[tid] = b0;
+        if constexpr (NUMERIC) aval[tid] = Av[a0 + bat + tid];
       }
+      int tot;
+      const int pre = block_excl_scan<NT>(len, wsum, &tot);
+      if (tid < nb) apre[tid] = pre;
+      if (tid == 0) apre[nb] = tot;
+      __syncthreads();
+      SPMM_STAMP(0);
+      // Distinct keys <= products: a slice whose products could exceed the
+      // table is handed to the HBM path instead (a full table would never
+      // terminate a probe).
+      slice_products += tot;
+      if (slice_products > TS - 8) { overflow = true; break; }
+
+      // This wave's contiguous share of the products; lane takes D consecutive
+      // products per batch with its current A entry cached in registers.
+      int nlog = 0;
+      while ((1 << nlog) < nb) ++nlog;   // binary-search depth over nb entries (uniform)
+      const int Q = (tot + NW - 1) / NW;
+      const int pbeg = w * Q;
+      const int pend = (pbeg + Q < tot) ? pbeg + Q : tot;
+      const int nbat = (pend > pbeg) ? (pend - pbeg + 64 * D - 1) / (64 * D) : 0;
+      if (nbat > 0) {
+        int cA[D], cB[D];
+        float bA[D], bB[D], aA[D], aB[D];
+        auto fetch = [&](int bt, int (&c)[D], float (&bv)[D], float (&av)[D]) {
+          // entry of each product: D independent binary searches over apre with a
+          // wave-uniform trip count (no divergent per-lane advance loops)
+          int64_t f[D];
+          int lo[D], hi[D], pp[D];
+          const int p0 = pbeg + (bt * 64 + lane) * D;
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            pp[u] = (p0 + u < pend) ? p0 + u : pend - 1;   // clamp: always a valid product
+            lo[u] = 0;
+            hi[u] = nb;
+          }
+          for (int it = 0; it < nlog; ++it) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+              const int mid = (lo[u] + hi[u]) >> 1;
+              if (apre[mid] <= pp[u]) lo[u] = mid; else hi[u] = mid;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            f[u] = abeg[lo[u]] + (pp[u] - apre[lo[u]]);
+            if constexpr (NUMERIC) av[u] = aval[lo[u]];
+          }
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            c[u] = Bci[f[u]];
+            if constexpr (NUMERIC) bv[u] = Bv[f[u]];
+          }
+        };
+        auto consume = [&](int bt, const int (&c)[D], const float (&bv)[D], const float (&av)[D]) {
+          const int p0 = pbeg + (bt * 64 + lane) * D;
+          // round 1: read every key's home group (D ds_read_b128 in flight)
+          int h[D], slot[D], cmpv[D], st[D];
+          int4 g4[D];
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            const int hk = c[u] - clo;
+            h[u] = mult ? (int)__umulhi((uint32_t)hk, mult) : hk;
+            g4[u] = *reinterpret_cast<const int4*>(&keys[h[u] & ~3]);
+          }
+          // first slot >= home in the group holding the key or EMPTY
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            const int gb = h[u] & ~3;
+            const int k4[4] = {g4[u].x, g4[u].y, g4[u].z, g4[u].w};
+            int sel = -1;
+            bool hit = false;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if (sel < 0 && gb + i >= h[u] && (k4[i] == c[u] || k4[i] == EMPTY)) { sel = gb + i; hit = k4[i] == c[u]; }
+            }
+            const bool valid = p0 + u < pend;
+            // st: 0 skip/done, 1 try CAS, 2 keep probing
+            st[u] = !valid ? 0 : (hit ? 0 : (sel >= 0 ? 1 : 2));
+            slot[u] = sel >= 0 ? sel : TS + 3;
+            cmpv[u] = (st[u] == 1) ? EMPTY : -2;   // -2 never matches: a no-op CAS
+          }
+          // round 2: D CAS in flight, unconditional (no branch around the LDS ops)
+          int old[D];
+#pragma unroll
+          for (int u = 0; u < D; ++u) old[u] = atomicCAS(&keys[slot[u]], cmpv[u], c[u]);
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            if (st[u] == 1) {
+              if (old[u] == EMPTY) { ++mine; st[u] = 0; }
+              else if (old[u] == c[u]) st[u] = 0;
+              else { st[u] = 2; h[u] = slot[u] + 1; }
+            } else if (st[u] == 2) {
+              h[u] = (h[u] | 3) + 1;
+            }
+          }
+          // slow path (long clusters, lost races): plain linear probing
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            if (st[u] == 2) {
+              int hh = h[u];
+              const int key = c[u];
+              while (true) {
+                if (hh >= TS) { hh = 0; s_wrapped = 1; }
+                const int kv = __hip_atomic_load(&keys[hh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (kv == key) break;
+                if (kv == EMPTY) {
+                  const int o = atomicCAS(&keys[hh], EMPTY, key);
+                  if (o == EMPTY) { ++mine; break; }
+                  if (o == key) break;
+                }
+                ++hh;
+              }
+              slot[u] = hh;
+            }
+          }
+          if constexpr (NUMERIC) {
+#pragma unroll
+            for (int u = 0; u < D; ++u)
+              if (p0 + u < pend) atomicAdd(&vals[slot[u]], av[u] * bv[u]);
+          }
+        };
+        fetch(0, cA, bA, aA);
+        for (int bt = 0; bt < nbat; bt += 2) {
+          fetch(bt + 1, cB, bB, aB);
+          consume(bt, cA, bA, aA);
+          fetch(bt + 2, cA, bA, aA);
+          consume(bt + 1, cB, bB, aB);
+        }
+      }
+    }
+    if (overflow) {
+      if (tid == 0) flags[row] |= 2;
+      return;   // uniform: every thread saw the same slice_products
+    }
+    __syncthreads();
+    SPMM_STAMP(1);
+    if (mine) atomicAdd(&s_count, mine);
+    if constexpr (!NUMERIC) {
+      __syncthreads();
+      row_count += s_count;
+      continue;
+    } else {
+      // Sorted positions.  Windows of 64 slots (one wave-instruction each):
+      // occupancy ballots give per-window counts (scanned into apre, free now)
+      // and each key's cluster start without walking; the rank inside the
+      // cluster is a scan of the cluster (lanes of one cluster read the same
+      // addresses: LDS broadcast).
+      constexpr int NWIN = TS / 64;
+      for (int W = w; W < NWIN; W += NW) {
+        const unsigned long long M = __ballot(keys[W * 64 + lane] != EMPTY);
+        if (lane == 0) apre[W] = __popcll(M);
+      }
+      __syncthreads();
+      int total;
+      {
+        const int cw = (tid < NWIN) ? apre[tid] : 0;
+        const int bw = block_excl_scan<NT>(cw, wsum, &total);
+        __syncthreads();
+        if (tid < NWIN) apre[tid] = bw;
+      }
+      __syncthreads();
+      const bool wrapped = s_wrapped != 0;
+      const int64_t base = Crp[row] + written;
+      // positions of neighbouring slots are nearly consecutive, so the direct
+      // stores below coalesce well within the row's output range
+      for (int W = w; W < NWIN; W += NW) {
+        const int sidx = W * 64 + lane;
+        const int key = keys[sidx];
+        const unsigned long long M = __ballot(key != EMPTY);
+        if (key != EMPTY) {
+          const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+          int pos;
+          if (wrapped) {
+            pos = apre[W] + __popcll(M & below);
+          } else {
+            const unsigned long long zb = ~M & below;
+            int cs, Pcs;
+            if (zb) {
+              const int ci = 64 - __builtin_clzll(zb);
+              cs = W * 64 + ci;
+              Pcs = apre[W] + __popcll(M & (~0ull >> (64 - ci)));
+            } else {
+              cs = W * 64;
+              while (cs > 0 && keys[cs - 1] != EMPTY) --cs;
+              Pcs = apre[W] - (W * 64 - cs);
+            }
+            int r = 0, x = cs;
+            while (true) {
+              const int k0 = keys[x], k1 = keys[x + 1], k2 = keys[x + 2], k3 = keys[x + 3];
+              if (k0 == EMPTY) break;
+              r += k0 < key;
+              if (k1 == EMPTY) break;
+              r += k1 < key;
+              if (k2 == EMPTY) break;
+              r += k2 < key;
+              if (k3 == EMPTY) break;
+              r += k3 < key;
+              x += 4;
+            }
+            pos = Pcs + r;
+          }
+          Cci[base + pos] = key;
+          Cv[base + pos] = vals[sidx];
+        }
+      }
+      SPMM_STAMP(2);
+      written += total;
+      if (tid == 0 && wrapped) flags[row] |= 1;
+      SPMM_STAMP(3);
+      __syncthreads();   // copy-out done before the next slice re-initialises the table
     }
   }
-  __syncthreads();
+  if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
   if constexpr (!NUMERIC) {
-    if (mine) atomicAdd(&s_count, mine);
-    __syncthreads();
-    if (tid == 0) row_nnz[row] = s_count;
-  } else {
-    const int s0 = tid * PER;
-    int kb[PER], pos[PER];
-    float vb[PER];
-    int cnt = 0;
+    if (tid == 0) row_nnz[row] = row_count;
+  }
+}
+
+// Quarter split points of every B row (rows column-sorted): bsplit[j*3 + q-1] =
+// first index of row j whose column >= floor(q * ncols / 4), q = 1..3.
+__global__ __launch_bounds__(256) void spgemm_row_splits(const int64_t* __restrict__ Brp,
+                                                         const int32_t* __restrict__ Bci, int64_t mb, int ncols,
+                                                         int64_t* __restrict__ bsplit) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= mb) return;
+  const int64_t lo0 = Brp[j], hi0 = Brp[j + 1];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      kb[q] = keys[s0 + q];
-      vb[q] = vals[s0 + q];
-      cnt += kb[q] != EMPTY;
+  for (int q = 1; q <= 3; ++q) {
+    const int bound = (int)(((int64_t)q * ncols) >> 2);
+    int64_t lo = lo0, hi = hi0;   // first index with col >= bound
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (Bci[mid] < bound) lo = mid + 1; else hi = mid;
     }
-    int total;
-    const int P0 = block_excl_scan<NT>(cnt, wsum, &total);
-    const bool wrapped = s_wrapped != 0;
-    if (!wrapped) {
-      int cs = s0, Pcs = P0;
-      if (kb[0] != EMPTY) {
-        while (cs > 0 && keys[cs - 1] != EMPTY) --cs;
-        Pcs = P0 - (s0 - cs);
-      }
-      int lp = 0;
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        pos[q] = -1;
-        if (kb[q] != EMPTY) {
-          if (q > 0 && kb[q - 1] == EMPTY) { cs = s0 + q; Pcs = P0 + lp; }
-          const int key = kb[q];
-          int r = 0, i = cs;
-          while (true) {
-            const int k0 = keys[i], k1 = keys[i + 1], k2 = keys[i + 2], k3 = keys[i + 3];
-            if (k0 == EMPTY) break;
-            r += k0 < key;
-            if (k1 == EMPTY) break;
-            r += k1 < key;
-            if (k2 == EMPTY) break;
-            r += k2 < key;
-            if (k3 == EMPTY) break;
-            r += k3 < key;
-            i += 4;
-          }
-          pos[q] = Pcs + r;
-          ++lp;
-        }
-      }
-    } else {  // a probe wrapped: emit slot order, the host re-sorts this row
-      int lp = 0;
-#pragma unroll
-      for (int q = 0; q < PER; ++q) pos[q] = (kb[q] != EMPTY) ? P0 + lp++ : -1;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      if (pos[q] >= 0) { keys[pos[q]] = kb[q]; vals[pos[q]] = vb[q]; }
-    }
-    __syncthreads();
-    const int64_t base = Crp[row];
-    for (int i = tid; i < total; i += NT) {
-      Cci[base + i] = keys[i];
-      Cv[base + i] = vals[i];
-    }
-    if (tid == 0 && wrapped) unsorted[row] = 1;
+    bsplit[j * 3 + q - 1] = lo;
   }
 }
 
@@ -381,21 +511,18 @@ __global__ __launch_bounds__(256) void spgemm_row_nprod(const int64_t* __restric
   if (lane == 0) nprod[row] = s;
 }
 
-template <int S, int NT, bool NUMERIC>
+template <int S, int NT, bool NUMERIC, int NP>
 int launch_lds(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
-               const float* Bv, const int32_t* rows, int64_t nrows, int ncols, int32_t* row_nnz,
-               const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* unsorted, hipStream_t s) {
+               const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows, int ncols,
+               int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags, hipStream_t s) {
   if (nrows <= 0) return 0;
-  hipLaunchKernelGGL((spgemm_lds<S, NT, NUMERIC>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp, Bci,
-                     Bv, rows, ncols, row_nnz, Crp, Cci, Cv, unsorted);
+  hipLaunchKernelGGL((spgemm_lds<S, NT, NUMERIC, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp,
+                     Bci, Bv, bsplit, rows, ncols, row_nnz, Crp, Cci, Cv, flags);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
 
 }  // namespace
-
-// Bin b uses table range S = 128 << b (b = 0..8 symbolic, 0..7 numeric).
-SPMM_EXPORT int spmm_spgemm_lds_max_bin(int numeric) { return numeric ? 7 : 8; }
 
 SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, int64_t m,
                                       int64_t* nprod, void* stream) {
@@ -406,17 +533,29 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
   return 0;
 }
 
+SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int ncols,
+                                       int64_t* bsplit, void* stream) {
+  if (mb <= 0) return 0;
+  hipLaunchKernelGGL(spgemm_row_splits, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Brp,
+                     Bci, mb, ncols, bsplit);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Symbolic bins 0..8: table range 128 << b keys, one pass; 9 / 10: 32768 keys,
+// 2 / 4 column slices.  Numeric bins 0..7: 128 << b key/value slots, one
+// pass; 8 / 9: 16384 slots, 2 / 4 column slices.
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
-                                const int64_t* Brp, const int32_t* Bci, const float* Bv, const int32_t* rows,
-                                int64_t nrows, int ncols, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci,
-                                float* Cv, int32_t* unsorted, void* stream) {
+                                const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
+                                const int32_t* rows, int64_t nrows, int ncols, int32_t* row_nnz, const int64_t* Crp,
+                                int32_t* Cci, float* Cv, int32_t* flags, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-#define SPMM_BIN(B, S, NT)                                                                                    \
-  case B:                                                                                                      \
-    return numeric ? launch_lds<S, NT, true>(Arp, Aci, Av, Brp, Bci, Bv, rows, nrows, ncols, row_nnz, Crp,     \
-                                             Cci, Cv, unsorted, s)                                             \
-                   : launch_lds<S, NT, false>(Arp, Aci, Av, Brp, Bci, Bv, rows, nrows, ncols, row_nnz, Crp,    \
-                                              Cci, Cv, unsorted, s);
+#define SPMM_ARGS Arp, Aci, Av, Brp, Bci, Bv, bsplit, rows, nrows, ncols, row_nnz, Crp, Cci, Cv, flags, s
+#define SPMM_BIN(B, S, NT)                                                                   \
+  case B:                                                                                     \
+    return numeric ? launch_lds<S, NT, true, 1>(SPMM_ARGS) : launch_lds<S, NT, false, 1>(SPMM_ARGS);
+  if (numeric && bin == 8) return launch_lds<16384, 1024, true, 2>(SPMM_ARGS);
+  if (numeric && bin == 9) return launch_lds<16384, 1024, true, 4>(SPMM_ARGS);
   switch (bin) {
     SPMM_BIN(0, 128, 64)
     SPMM_BIN(1, 256, 64)
@@ -427,13 +566,16 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
     SPMM_BIN(6, 8192, 512)
     SPMM_BIN(7, 16384, 1024)
     case 8:
-      if (numeric) return (int)hipErrorInvalidValue;
-      return launch_lds<32768, 1024, false>(Arp, Aci, Av, Brp, Bci, Bv, rows, nrows, ncols, row_nnz, Crp, Cci, Cv,
-                                            unsorted, s);
+      return launch_lds<32768, 1024, false, 1>(SPMM_ARGS);
+    case 9:
+      return launch_lds<32768, 1024, false, 2>(SPMM_ARGS);
+    case 10:
+      return launch_lds<32768, 1024, false, 4>(SPMM_ARGS);
     default:
       return (int)hipErrorInvalidValue;
   }
 #undef SPMM_BIN
+#undef SPMM_ARGS
 }
 
 SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
@@ -451,4 +593,19 @@ SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_
                        rows, ws_off, ws_size, ws_keys, ws_vals, ncols, row_nnz, Crp, Cci, Cv, unsorted);
   SPMM_LAUNCH_CHECK();
   return 0;
+}
+
+// Diagnostics: enable/reset (on >= 0) or read the phase-cycle accumulators of
+// spgemm_lds: [0] init+A staging, [1] product inserts, [2] rank computation,
+// [3] output writes, [7] rows.
+SPMM_EXPORT int spmm_spgemm_stamps(int on, unsigned long long* out8) {
+  if (on >= 0) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_on), &on, sizeof on);
+    return (int)e;
+  }
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), 8 * sizeof(unsigned long long));
+  return (int)e;
 }

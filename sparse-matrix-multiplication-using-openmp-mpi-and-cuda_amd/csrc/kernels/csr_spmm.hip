@@ -33,6 +33,7 @@
 namespace {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -116,12 +117,10 @@ __global__ __launch_bounds__(NT) void spmm_panel_mfma(
         const unsigned char* p1 = Xt + r1 * 256 + ((t ^ xswz(r1)) << 5) + p * 8;
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p0));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p1));
-        v8bf b;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          b[j] = __builtin_bit_cast(__bf16, lo[j]);
-          b[j + 4] = __builtin_bit_cast(__bf16, hi[j]);
-        }
+        // whole-vector shuffle + bitcast: per-element short->__bf16 inserts are
+        // miscompiled by hipcc (ROCm 7.2) into duplicated lanes
+        const v8s bs = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const v8bf b = __builtin_bit_cast(v8bf, bs);
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[t], 0, 0, 0);
       }
     }

@@ -23,6 +23,7 @@ import torch
 
 from .. import _native
 from .._native import c_vp
+from ..utils.config import CONFIG
 from .csr import CSR, sort_rows
 import ctypes as C
 
@@ -30,16 +31,22 @@ C_I64 = C.c_int64
 C_INT = C.c_int
 
 _native.register_hip("spmm_spgemm_row_nprod", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
+_native.register_hip("spmm_spgemm_row_splits", c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_global", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp,
                      c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 
-SYM_MAX_BIN = 8      # table range 128 << 8 = 32768 keys (128 KiB)
-NUM_MAX_BIN = 7      # 16384 key/value slots (128 KiB)
-LOAD = 0.75
-TOP_LOAD = 0.85
-GLOBAL_WS_BYTES = 8 << 30   # HBM budget for one batch of global-table rows
+# LDS bins: table range 128 << b.  Symbolic: b = 0..8 single pass (up to 32768
+# keys), 9 / 10 = 32768 keys over 2 / 4 column slices.  Numeric: b = 0..7 single
+# pass (up to 16384 key/value slots), 8 / 9 = 16384 slots over 2 / 4 slices.
+SYM_TOP, SYM_SLICED = 8, (9, 10)
+NUM_TOP, NUM_SLICED = 7, (8, 9)
+SYM_GLOBAL = 11
+NUM_GLOBAL = 10
+LOAD = CONFIG.spgemm_load              # max load factor of an LDS table (per slice)
+GLOBAL_WS_BYTES = int(CONFIG.spgemm_global_ws_gb * (1 << 30))   # HBM budget per batch of global-table rows
 
 
 @dataclass
@@ -51,19 +58,21 @@ class SpgemmInfo:
     resorted_rows: int = 0
 
 
-def _bins(counts: torch.Tensor, max_bin: int) -> torch.Tensor:
-    caps = [LOAD * (128 << b) for b in range(max_bin + 1)]
-    caps[-1] = TOP_LOAD * (128 << max_bin)
-    b = torch.bucketize(counts, torch.tensor([int(c) for c in caps], device=counts.device, dtype=counts.dtype))
+def _bins(counts: torch.Tensor, top: int) -> torch.Tensor:
+    """Bin per row: smallest single-pass table with counts <= LOAD * S, then the
+    2- and 4-slice passes of the top table, then the HBM path; -1 for empty rows."""
+    caps = [int(LOAD * (128 << b)) for b in range(top + 1)]
+    caps += [2 * caps[-1], 4 * caps[-1]]
+    b = torch.bucketize(counts, torch.tensor(caps, device=counts.device, dtype=counts.dtype))
     return torch.where(counts == 0, torch.full_like(b, -1), b)
 
 
-def _group(bins: torch.Tensor, max_bin: int):
-    """rows ordered by bin + host list of (bin, offset, count); bin max_bin+1 = global."""
+def _group(bins: torch.Tensor, nbins: int):
+    """rows ordered by bin + host list of (bin, offset, count) for bins 0..nbins-1."""
     order = torch.argsort(bins, stable=True).to(torch.int32)
-    hist = torch.bincount(bins + 1, minlength=max_bin + 3).tolist()
+    hist = torch.bincount(bins + 1, minlength=nbins + 1).tolist()
     groups, off = [], hist[0]
-    for b in range(max_bin + 2):
+    for b in range(nbins):
         cnt = hist[b + 1]
         if cnt:
             groups.append((b, off, cnt))
@@ -123,55 +132,80 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
         return _spgemm_cpu(A, B, info)
     A = A if A.val.dtype == torch.float32 else A.with_values(A.val.float())
     B = B if B.val.dtype == torch.float32 else B.with_values(B.val.float())
+    nprod = row_nprod(A, B)
+    info.flops = 2 * int(nprod.sum())
+    row_nnz = symbolic(A, B, nprod, info)
+    return numeric(A, B, row_nnz, info)
+
+
+def _dummies(dev):
+    return (torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),
+            torch.zeros(1, dtype=torch.float32, device=dev))
+
+
+def _splits(B: CSR) -> torch.Tensor:
+    sp = torch.empty(B.m * 3, dtype=torch.int64, device=B.device)
+    _native.check(_native.hip().spmm_spgemm_row_splits(_native.ptr(B.rowptr), _native.ptr(B.col), B.m, B.n,
+                                                        _native.ptr(sp), _native.stream_ptr(B.device)),
+                  "spgemm_row_splits")
+    return sp
+
+
+def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins):
     dev = A.device
     lib = _native.hip()
     P = _native.ptr
     stream = _native.stream_ptr(dev)
-    m = A.m
-
-    nprod = row_nprod(A, B)
-    info.flops = 2 * int(nprod.sum())
-
-    # symbolic
-    row_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
-    sbins = _bins(nprod, SYM_MAX_BIN)
-    order, groups = _group(sbins, SYM_MAX_BIN)
-    dummy_i64 = torch.zeros(1, dtype=torch.int64, device=dev)
-    dummy_i32 = torch.zeros(1, dtype=torch.int32, device=dev)
-    dummy_f = torch.zeros(1, dtype=torch.float32, device=dev)
+    top, sliced, glob = (NUM_TOP, NUM_SLICED, NUM_GLOBAL) if numeric else (SYM_TOP, SYM_SLICED, SYM_GLOBAL)
+    order, groups = _group(_bins(counts, top), glob + 1)
+    splits = None
+    global_rows = []
     for b, off, cnt in groups:
-        info.rows_per_bin_sym[b] = cnt
+        info_bins[b] = cnt
         rows = order[off:off + cnt]
-        if b <= SYM_MAX_BIN:
-            _native.check(lib.spmm_spgemm_lds(b, 0, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
-                                              P(B.val), P(rows), cnt, B.n, P(row_nnz), P(dummy_i64), P(dummy_i32),
-                                              P(dummy_f), P(dummy_i32), stream), "spgemm_lds(symbolic)")
-        else:
-            _global_rows(0, A, B, rows, nprod[rows.long()], row_nnz, dummy_i64, dummy_i32, dummy_f, dummy_i32,
-                         stream)
+        if b == glob:
+            global_rows.append(rows)
+            continue
+        if b in sliced and splits is None:
+            splits = _splits(B)
+        _native.check(lib.spmm_spgemm_lds(b, numeric, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
+                                          P(B.val), P(splits) if splits is not None else None, P(rows), cnt, B.n,
+                                          P(row_nnz), P(Crp), P(Cci), P(Cv), P(flags), stream),
+                      "spgemm_lds(numeric)" if numeric else "spgemm_lds(symbolic)")
+    # rows whose column slice could overflow an LDS table were skipped by the kernel
+    spill = ((flags & 2) != 0).nonzero().flatten().to(torch.int32)
+    if spill.numel():
+        info_bins["lds_overflow"] = int(spill.numel())
+        global_rows.append(spill)
+    if global_rows:
+        rows = torch.cat(global_rows)
+        _global_rows(numeric, A, B, rows, counts[rows.long()], row_nnz, Crp, Cci, Cv, flags, stream)
 
+
+def symbolic(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> torch.Tensor:
+    """Exact nnz per output row (int32, device)."""
+    dev = A.device
+    row_nnz = torch.zeros(A.m, dtype=torch.int32, device=dev)
+    flags = torch.zeros(A.m, dtype=torch.int32, device=dev)
+    d64, d32, df = _dummies(dev)
+    _run_bins(0, A, B, nprod, row_nnz, d64, d32, df, flags, info.rows_per_bin_sym)
+    return row_nnz
+
+
+def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo) -> CSR:
+    """Values of C (column-sorted rows) into the layout fixed by ``row_nnz``."""
+    dev = A.device
+    m = A.m
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     torch.cumsum(row_nnz, 0, out=rowptr[1:])
     nnz = int(rowptr[-1])
     info.nnz = nnz
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
-    unsorted = torch.zeros(m, dtype=torch.int32, device=dev)
-
-    # numeric
-    nbins = _bins(row_nnz, NUM_MAX_BIN)
-    order, groups = _group(nbins, NUM_MAX_BIN)
-    for b, off, cnt in groups:
-        info.rows_per_bin_num[b] = cnt
-        rows = order[off:off + cnt]
-        if b <= NUM_MAX_BIN:
-            _native.check(lib.spmm_spgemm_lds(b, 1, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
-                                              P(B.val), P(rows), cnt, B.n, P(row_nnz), P(rowptr), P(Cci), P(Cv),
-                                              P(unsorted), stream), "spgemm_lds(numeric)")
-        else:
-            _global_rows(1, A, B, rows, row_nnz[rows.long()], row_nnz, rowptr, Cci, Cv, unsorted, stream)
+    flags = torch.zeros(m, dtype=torch.int32, device=dev)
+    _run_bins(1, A, B, row_nnz, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num)
     C_ = CSR(m, B.n, rowptr, Cci, Cv)
-    bad = unsorted.nonzero().flatten()
+    bad = ((flags & 1) != 0).nonzero().flatten()
     if bad.numel():
         info.resorted_rows = int(bad.numel())
         C_ = sort_rows(C_, bad)

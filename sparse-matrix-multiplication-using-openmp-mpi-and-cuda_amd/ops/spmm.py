@@ -23,6 +23,7 @@ import torch
 
 from .. import _native
 from .._native import c_vp
+from ..utils.config import CONFIG
 from .csr import CSR
 
 _native.register_hip("spmm_spmm_panel_mfma", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64,
@@ -32,7 +33,7 @@ _native.register_hip("spmm_spmm_rowwise", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c
 
 PANEL = 64
 CHUNK = 64
-MFMA_MIN_REUSE = 1.15
+MFMA_MIN_REUSE = CONFIG.spmm_mfma_min_reuse
 
 
 @dataclass

@@ -1,0 +1,36 @@
+"""Runtime configuration (replaces the reference's compile-time globals).
+
+Reference constants (sparse_matrix_mult.cu): ``BIG_SIZE = 1e9`` staging
+elements (:22), ``small_size = 500`` output tiles per GPU round (:23),
+``num_threads(16)`` parser threads (:334), ``CHUNK_KEYS = 262144`` /
+``CHUNK_VALS = 4194304`` MPI message chunks (:467-468).  None of those is
+needed here (tiles stay in HBM, RCCL chunks internally); what remains
+tunable is read from the environment (``SPMM_*``) with these defaults.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field, fields
+
+
+def _env(name: str, default, cast):
+    v = os.environ.get(name)
+    return default if v in (None, "") else cast(v)
+
+
+@dataclass
+class Config:
+    threads: int = field(default_factory=lambda: _env("SPMM_THREADS", 0, int))          # 0 = all host threads
+    device: str = field(default_factory=lambda: _env("SPMM_DEVICE", "auto", str))
+    comm: str = field(default_factory=lambda: _env("SPMM_COMM", "auto", str))
+    streams: int = field(default_factory=lambda: _env("SPMM_STREAMS", 4, int))           # chain-level concurrency
+    spgemm_load: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD", 0.5, float))   # per LDS table slice
+    spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
+    spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
+    comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))
+
+    def as_dict(self) -> dict:
+        return {f.name: getattr(self, f.name) for f in fields(self)}
+
+
+CONFIG = Config()

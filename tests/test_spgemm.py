@@ -138,7 +138,7 @@ def test_spgemm_gpu_matches_cpu_structure_all_bins():
     Cc = SG.spgemm(A, B)
     info = SG.SpgemmInfo()
     Cg = SG.spgemm(A.to(dev), B.to(dev), info)
-    assert SG.SYM_MAX_BIN + 1 in info.rows_per_bin_sym or SG.NUM_MAX_BIN + 1 in info.rows_per_bin_num
+    assert SG.SYM_GLOBAL in info.rows_per_bin_sym or SG.NUM_GLOBAL in info.rows_per_bin_num
     assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
     assert torch.equal(Cg.col.cpu(), Cc.col)
     assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
@@ -151,6 +151,23 @@ def test_spgemm_gpu_rmat_aat():
     At = A.transpose()
     Cg = SG.spgemm(A, At)
     Cc = SG.spgemm(A.to("cpu"), At.to("cpu"))
+    assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+    assert torch.equal(Cg.col.cpu(), Cc.col)
+    assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("brow,bcols", [(60, 200000), (100, 200000), (100, 40000)])
+def test_spgemm_gpu_column_sliced_bins(brow, bcols):
+    """Rows long enough for the 2- and 4-slice LDS passes (and the overflow
+    hand-off to the HBM path) must match the CPU result exactly in structure."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(300, 2000, 0.1, seed=5)
+    B = gen_csr.uniform_csr(2000, bcols, brow / bcols, seed=6)
+    Cc = SG.spgemm(A, B)
+    info = SG.SpgemmInfo()
+    Cg = SG.spgemm(A.to(dev), B.to(dev), info)
+    assert any(b in info.rows_per_bin_sym for b in SG.SYM_SLICED) or any(b in info.rows_per_bin_num for b in SG.NUM_SLICED)
     assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
     assert torch.equal(Cg.col.cpu(), Cc.col)
     assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
