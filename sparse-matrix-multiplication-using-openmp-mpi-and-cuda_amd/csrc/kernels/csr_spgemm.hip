@@ -32,6 +32,7 @@ constexpr int EMPTY = -1;
 // every workgroup adds the shader-clock cycles of each phase, measured between
 // the workgroup barriers that delimit it.  Read with spmm_spgemm_stamps().
 __device__ int g_stamp_on = 0;
+__device__ int g_diag_mode = 0;   // diagnostics only: 1 = skip inserts, 2 = synthetic keys (no B loads)
 __device__ unsigned long long g_stamps[8];
 #define SPMM_STAMP(i)                                                              \
   do {                                                                             \
@@ -118,12 +119,12 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   constexpr int PER = TS / NT;
   constexpr int NW = NT / 64;
   constexpr int ACAP = NT;
-  constexpr int QSTEP = 4 / NP;         // quarters per column slice
+  constexpr int QSTEP = 8 / NP;         // eighths of the column space per slice
   // products per lane per fetch batch: deep where LDS already caps occupancy at
   // one workgroup per CU, shallow (fewer VGPRs, more waves) for small tables
   constexpr int D = NUMERIC ? 4 : ((NT >= 512) ? 8 : 4);
   __shared__ __attribute__((aligned(16))) int keys[TS + 4];
-  __shared__ float vals[NUMERIC ? TS : 1];
+  __shared__ __attribute__((aligned(16))) float vals[NUMERIC ? TS : 4];
   __shared__ int64_t abeg[ACAP];
   __shared__ int apre[ACAP + 1];
   __shared__ float aval[NUMERIC ? ACAP : 1];
@@ -135,6 +136,7 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   const int row = rows[blockIdx.x];
   const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
   const int stamp_on = g_stamp_on;
+  const int diag = g_diag_mode;
   unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;
   int written = 0;      // numeric: entries of earlier slices already stored
   int row_count = 0;    // symbolic: distinct columns over all slices
@@ -142,11 +144,11 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   for (int sl = 0; sl < NP; ++sl) {
     // column slice [clo, chi) and its monotone hash
     const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
-    const int clo = (int)(((int64_t)q0 * ncols) >> 2), chi = (int)(((int64_t)q1 * ncols) >> 2);
+    const int clo = (int)(((int64_t)q0 * ncols) >> 3), chi = (int)(((int64_t)q1 * ncols) >> 3);
     const uint32_t mult = hash_mult(S, chi - clo);
     for (int i = tid; i < (TS + 4) / 4; i += NT) reinterpret_cast<int4*>(keys)[i] = make_int4(EMPTY, EMPTY, EMPTY, EMPTY);
     if constexpr (NUMERIC) {
-      for (int i = tid; i < TS; i += NT) vals[i] = 0.f;
+      for (int i = tid; i < TS / 4; i += NT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (tid == 0) { s_count = 0; s_wrapped = 0; }
     int mine = 0;
@@ -160,8 +162,8 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
       if (tid < nb) {
         const int j = Aci[a0 + bat + tid];
         const int64_t rb = Brp[j], re = Brp[j + 1];
-        const int64_t b0 = (NP == 1 || q0 == 0) ? rb : bsplit[(int64_t)j * 3 + q0 - 1];
-        const int64_t b1 = (NP == 1 || q1 == 4) ? re : bsplit[(int64_t)j * 3 + q1 - 1];
+        const int64_t b0 = (NP == 1 || q0 == 0) ? rb : bsplit[(int64_t)j * 7 + q0 - 1];
+        const int64_t b1 = (NP == 1 || q1 == 8) ? re : bsplit[(int64_t)j * 7 + q1 - 1];
         len = (int)(b1 - b0);
         abeg[tid] = b0;
         if constexpr (NUMERIC) aval[tid] = Av[a0 + bat + tid];
@@ -213,6 +215,14 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
             f[u] = abeg[lo[u]] + (pp[u] - apre[lo[u]]);
             if constexpr (NUMERIC) av[u] = aval[lo[u]];
           }
+          if (diag == 2) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+              c[u] = clo + (int)__umulhi((uint32_t)(f[u] * 2654435761ull), (uint32_t)(chi - clo));
+              if constexpr (NUMERIC) bv[u] = 1.f;
+            }
+            return;
+          }
 #pragma unroll
           for (int u = 0; u < D; ++u) {
             c[u] = Bci[f[u]];
@@ -221,70 +231,63 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
         };
         auto consume = [&](int bt, const int (&c)[D], const float (&bv)[D], const float (&av)[D]) {
           const int p0 = pbeg + (bt * 64 + lane) * D;
-          // round 1: read every key's home group (D ds_read_b128 in flight)
-          int h[D], slot[D], cmpv[D], st[D];
-          int4 g4[D];
+          if (diag == 1) {   // keep the loaded values live, skip the table
+#pragma unroll
+            for (int u = 0; u < D; ++u) mine ^= (p0 + u < pend) ? (c[u] & 1) : 0;
+            return;
+          }
+          // CAS-only linear probing in rounds over the lane's D keys: a CAS of
+          // EMPTY -> key both claims a free slot and reports the occupant
+          // (one LDS op per probe step; ds_cmpst costs ~11 cycles per
+          // wave-instruction on gfx950, a read + CAS pair ~17).  A key u is
+          // only touched while some lane still has it pending.
+          int h[D], st[D];
 #pragma unroll
           for (int u = 0; u < D; ++u) {
             const int hk = c[u] - clo;
             h[u] = mult ? (int)__umulhi((uint32_t)hk, mult) : hk;
-            g4[u] = *reinterpret_cast<const int4*>(&keys[h[u] & ~3]);
+            st[u] = (p0 + u < pend) ? 1 : 0;   // 1 = pending
           }
-          // first slot >= home in the group holding the key or EMPTY
+          while (true) {
+            bool more = false;
 #pragma unroll
-          for (int u = 0; u < D; ++u) {
-            const int gb = h[u] & ~3;
-            const int k4[4] = {g4[u].x, g4[u].y, g4[u].z, g4[u].w};
-            int sel = -1;
-            bool hit = false;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              if (sel < 0 && gb + i >= h[u] && (k4[i] == c[u] || k4[i] == EMPTY)) { sel = gb + i; hit = k4[i] == c[u]; }
-            }
-            const bool valid = p0 + u < pend;
-            // st: 0 skip/done, 1 try CAS, 2 keep probing
-            st[u] = !valid ? 0 : (hit ? 0 : (sel >= 0 ? 1 : 2));
-            slot[u] = sel >= 0 ? sel : TS + 3;
-            cmpv[u] = (st[u] == 1) ? EMPTY : -2;   // -2 never matches: a no-op CAS
-          }
-          // round 2: D CAS in flight, unconditional (no branch around the LDS ops)
-          int old[D];
-#pragma unroll
-          for (int u = 0; u < D; ++u) old[u] = atomicCAS(&keys[slot[u]], cmpv[u], c[u]);
-#pragma unroll
-          for (int u = 0; u < D; ++u) {
-            if (st[u] == 1) {
-              if (old[u] == EMPTY) { ++mine; st[u] = 0; }
-              else if (old[u] == c[u]) st[u] = 0;
-              else { st[u] = 2; h[u] = slot[u] + 1; }
-            } else if (st[u] == 2) {
-              h[u] = (h[u] | 3) + 1;
-            }
-          }
-          // slow path (long clusters, lost races): plain linear probing
-#pragma unroll
-          for (int u = 0; u < D; ++u) {
-            if (st[u] == 2) {
-              int hh = h[u];
-              const int key = c[u];
-              while (true) {
-                if (hh >= TS) { hh = 0; s_wrapped = 1; }
-                const int kv = __hip_atomic_load(&keys[hh], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (kv == key) break;
-                if (kv == EMPTY) {
-                  const int o = atomicCAS(&keys[hh], EMPTY, key);
-                  if (o == EMPTY) { ++mine; break; }
-                  if (o == key) break;
+            for (int u = 0; u < D; ++u) {
+              if (__any(st[u] != 0)) {
+                if (st[u]) {
+                  const int old = atomicCAS(&keys[h[u]], EMPTY, c[u]);
+                  if (old == EMPTY) { ++mine; st[u] = 0; }
+                  else if (old == c[u]) st[u] = 0;
+                  else if (++h[u] >= TS) { h[u] = 0; s_wrapped = 1; }
                 }
-                ++hh;
+                more |= st[u] != 0;
               }
-              slot[u] = hh;
             }
+            if (!__any(more)) break;
           }
           if constexpr (NUMERIC) {
+            // float accumulate by read + CAS (ds_add_f32 serialises lanes: ~192
+            // cycles per wave-instruction measured on gfx950)
+            int ob[D];
+            bool pendv[D];
 #pragma unroll
-            for (int u = 0; u < D; ++u)
-              if (p0 + u < pend) atomicAdd(&vals[slot[u]], av[u] * bv[u]);
+            for (int u = 0; u < D; ++u) {
+              pendv[u] = p0 + u < pend;
+              ob[u] = pendv[u] ? __hip_atomic_load(reinterpret_cast<int*>(&vals[h[u]]), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+            }
+            while (true) {
+              bool again = false;
+#pragma unroll
+              for (int u = 0; u < D; ++u) {
+                if (pendv[u]) {
+                  const int nv = __float_as_int(__int_as_float(ob[u]) + av[u] * bv[u]);
+                  const int o = atomicCAS(reinterpret_cast<int*>(&vals[h[u]]), ob[u], nv);
+                  if (o == ob[u]) pendv[u] = false;
+                  else { ob[u] = o; again = true; }
+                }
+              }
+              if (!__any(again)) break;
+            }
           }
         };
         fetch(0, cA, bA, aA);
@@ -314,9 +317,20 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
       // cluster is a scan of the cluster (lanes of one cluster read the same
       // addresses: LDS broadcast).
       constexpr int NWIN = TS / 64;
-      for (int W = w; W < NWIN; W += NW) {
-        const unsigned long long M = __ballot(keys[W * 64 + lane] != EMPTY);
-        if (lane == 0) apre[W] = __popcll(M);
+      constexpr int WPW = (NWIN + NW - 1) / NW;   // windows per wave, kept in registers
+      int kq[WPW];
+      float vq[WPW];
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) {
+        const int W = w + j * NW;
+        kq[j] = (W < NWIN) ? keys[W * 64 + lane] : EMPTY;
+        vq[j] = (W < NWIN) ? vals[W * 64 + lane] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) {
+        const int W = w + j * NW;
+        const unsigned long long M = __ballot(kq[j] != EMPTY);
+        if (lane == 0 && W < NWIN) apre[W] = __popcll(M);
       }
       __syncthreads();
       int total;
@@ -329,46 +343,75 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
       __syncthreads();
       const bool wrapped = s_wrapped != 0;
       const int64_t base = Crp[row] + written;
-      // positions of neighbouring slots are nearly consecutive, so the direct
-      // stores below coalesce well within the row's output range
-      for (int W = w; W < NWIN; W += NW) {
-        const int sidx = W * 64 + lane;
-        const int key = keys[sidx];
-        const unsigned long long M = __ballot(key != EMPTY);
-        if (key != EMPTY) {
-          const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-          int pos;
-          if (wrapped) {
-            pos = apre[W] + __popcll(M & below);
-          } else {
-            const unsigned long long zb = ~M & below;
-            int cs, Pcs;
-            if (zb) {
-              const int ci = 64 - __builtin_clzll(zb);
-              cs = W * 64 + ci;
-              Pcs = apre[W] + __popcll(M & (~0ull >> (64 - ci)));
+      // symbolic fixed the row's size; never store past it whatever happened here
+      const int room = row_nnz[row] - written;
+      const int lim = total < room ? total : room;
+      if (tid == 0 && total > room) flags[row] |= 4;
+      const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      const int rlo = lane & ~15;   // first lane of this lane's 16-lane DPP row
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) {
+        const int W = w + j * NW;
+        if (W < NWIN) {
+          const int key = kq[j];
+          const unsigned long long M = __ballot(key != EMPTY);
+          // neighbours inside the 16-lane row (DPP row shifts, no LDS traffic)
+          const int m1 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x111, 0xF, 0xF, false);
+          const int m2 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x112, 0xF, 0xF, false);
+          const int m3 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x113, 0xF, 0xF, false);
+          const int p1 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x101, 0xF, 0xF, false);
+          const int p2 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x102, 0xF, 0xF, false);
+          const int p3 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x103, 0xF, 0xF, false);
+          if (key != EMPTY) {
+            int pos;
+            if (wrapped) {
+              pos = apre[W] + __popcll(M & below);
             } else {
-              cs = W * 64;
-              while (cs > 0 && keys[cs - 1] != EMPTY) --cs;
-              Pcs = apre[W] - (W * 64 - cs);
+              const unsigned long long zb = ~M & below;                       // empty slots below me
+              const unsigned long long za = ~M & ~(below | (1ull << lane));   // empty slots above me
+              const int ci = zb ? 64 - __builtin_clzll(zb) : -1;              // cluster start lane (-1: before window)
+              const int ce = za ? __builtin_ctzll(za) : 64;                   // cluster end lane (64: past window)
+              int Pcs, cs;
+              if (ci >= 0) {
+                cs = W * 64 + ci;
+                Pcs = apre[W] + __popcll(M & (ci ? (~0ull >> (64 - ci)) : 0ull));
+              } else {
+                cs = W * 64;
+                while (cs > 0 && keys[cs - 1] != EMPTY) --cs;
+                Pcs = apre[W] - (W * 64 - cs);
+              }
+              int r = 0;
+              if (ci >= rlo && ce < 64 && ce <= rlo + 16 && ce - ci <= 4) {   // whole cluster within 3 lanes, same row
+                r += (lane - 1 >= ci) & (m1 < key);
+                r += (lane - 2 >= ci) & (m2 < key);
+                r += (lane - 3 >= ci) & (m3 < key);
+                r += (lane + 1 < ce) & (p1 < key);
+                r += (lane + 2 < ce) & (p2 < key);
+                r += (lane + 3 < ce) & (p3 < key);
+              } else {   // long or boundary-crossing cluster: scan it in LDS
+                int x = cs;
+                while (true) {
+                  const int k0 = keys[x], k1 = keys[x + 1], k2 = keys[x + 2], k3 = keys[x + 3];
+                  if (k0 == EMPTY) break;
+                  r += k0 < key;
+                  if (k1 == EMPTY) break;
+                  r += k1 < key;
+                  if (k2 == EMPTY) break;
+                  r += k2 < key;
+                  if (k3 == EMPTY) break;
+                  r += k3 < key;
+                  x += 4;
+                }
+              }
+              pos = Pcs + r;
             }
-            int r = 0, x = cs;
-            while (true) {
-              const int k0 = keys[x], k1 = keys[x + 1], k2 = keys[x + 2], k3 = keys[x + 3];
-              if (k0 == EMPTY) break;
-              r += k0 < key;
-              if (k1 == EMPTY) break;
-              r += k1 < key;
-              if (k2 == EMPTY) break;
-              r += k2 < key;
-              if (k3 == EMPTY) break;
-              r += k3 < key;
-              x += 4;
+            if (pos >= 0 && pos < lim) {
+              Cci[base + pos] = key;
+              Cv[base + pos] = vq[j];
+            } else {
+              flags[row] |= 4;   // internal error: never write outside the row
             }
-            pos = Pcs + r;
           }
-          Cci[base + pos] = key;
-          Cv[base + pos] = vals[sidx];
         }
       }
       SPMM_STAMP(2);
@@ -384,23 +427,24 @@ __global__ __launch_bounds__(NT) void spgemm_lds(
   }
 }
 
-// Quarter split points of every B row (rows column-sorted): bsplit[j*3 + q-1] =
-// first index of row j whose column >= floor(q * ncols / 4), q = 1..3.
+// Eighth split points of every B row (rows column-sorted): bsplit[j*7 + q-1] =
+// first index of row j whose column >= floor(q * ncols / 8), q = 1..7.
 __global__ __launch_bounds__(256) void spgemm_row_splits(const int64_t* __restrict__ Brp,
                                                          const int32_t* __restrict__ Bci, int64_t mb, int ncols,
                                                          int64_t* __restrict__ bsplit) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= mb) return;
   const int64_t lo0 = Brp[j], hi0 = Brp[j + 1];
+  int64_t lo = lo0;
 #pragma unroll
-  for (int q = 1; q <= 3; ++q) {
-    const int bound = (int)(((int64_t)q * ncols) >> 2);
-    int64_t lo = lo0, hi = hi0;   // first index with col >= bound
+  for (int q = 1; q <= 7; ++q) {
+    const int bound = (int)(((int64_t)q * ncols) >> 3);
+    int64_t hi = hi0;   // first index with col >= bound (search starts at the previous split)
     while (lo < hi) {
       const int64_t mid = (lo + hi) >> 1;
       if (Bci[mid] < bound) lo = mid + 1; else hi = mid;
     }
-    bsplit[j * 3 + q - 1] = lo;
+    bsplit[j * 7 + q - 1] = lo;
   }
 }
 
@@ -542,9 +586,13 @@ SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, i
   return 0;
 }
 
-// Symbolic bins 0..8: table range 128 << b keys, one pass; 9 / 10: 32768 keys,
-// 2 / 4 column slices.  Numeric bins 0..7: 128 << b key/value slots, one
-// pass; 8 / 9: 16384 slots, 2 / 4 column slices.
+// LDS bins.  Every table is sized so that at least two workgroups fit a CU
+// (<= 80 KB of LDS): a workgroup's phases (staging, inserts, ranking) are
+// separated by barriers and their latencies only overlap with ANOTHER
+// workgroup's work.  Long rows are cut into 2 / 4 / 8 column slices instead of
+// using bigger tables.
+//   symbolic bins 0..6: 128 << b keys, one pass; 7..10: 16384 keys x 1/2/4/8 slices
+//   numeric  bins 0..6: 128 << b key/value slots, one pass; 7..9: 8192 slots x 2/4/8 slices
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
                                 const int32_t* rows, int64_t nrows, int ncols, int32_t* row_nnz, const int64_t* Crp,
@@ -554,8 +602,16 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
 #define SPMM_BIN(B, S, NT)                                                                   \
   case B:                                                                                     \
     return numeric ? launch_lds<S, NT, true, 1>(SPMM_ARGS) : launch_lds<S, NT, false, 1>(SPMM_ARGS);
-  if (numeric && bin == 8) return launch_lds<16384, 1024, true, 2>(SPMM_ARGS);
-  if (numeric && bin == 9) return launch_lds<16384, 1024, true, 4>(SPMM_ARGS);
+  if (numeric) {
+    if (bin == 7) return launch_lds<8192, 512, true, 2>(SPMM_ARGS);
+    if (bin == 8) return launch_lds<8192, 512, true, 4>(SPMM_ARGS);
+    if (bin == 9) return launch_lds<8192, 512, true, 8>(SPMM_ARGS);
+  } else {
+    if (bin == 7) return launch_lds<16384, 512, false, 1>(SPMM_ARGS);
+    if (bin == 8) return launch_lds<16384, 512, false, 2>(SPMM_ARGS);
+    if (bin == 9) return launch_lds<16384, 512, false, 4>(SPMM_ARGS);
+    if (bin == 10) return launch_lds<16384, 512, false, 8>(SPMM_ARGS);
+  }
   switch (bin) {
     SPMM_BIN(0, 128, 64)
     SPMM_BIN(1, 256, 64)
@@ -564,13 +620,6 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
     SPMM_BIN(4, 2048, 256)
     SPMM_BIN(5, 4096, 256)
     SPMM_BIN(6, 8192, 512)
-    SPMM_BIN(7, 16384, 1024)
-    case 8:
-      return launch_lds<32768, 1024, false, 1>(SPMM_ARGS);
-    case 9:
-      return launch_lds<32768, 1024, false, 2>(SPMM_ARGS);
-    case 10:
-      return launch_lds<32768, 1024, false, 4>(SPMM_ARGS);
     default:
       return (int)hipErrorInvalidValue;
   }
@@ -601,8 +650,10 @@ SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_
 SPMM_EXPORT int spmm_spgemm_stamps(int on, unsigned long long* out8) {
   if (on >= 0) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int st = on & 1, mode = on >> 1;
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_on), &on, sizeof on);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_on), &st, sizeof st);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_diag_mode), &mode, sizeof mode);
     return (int)e;
   }
   hipError_t e = hipDeviceSynchronize();

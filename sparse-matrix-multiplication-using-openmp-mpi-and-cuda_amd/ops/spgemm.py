@@ -38,11 +38,14 @@ _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_global", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp,
                      c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 
-# LDS bins: table range 128 << b.  Symbolic: b = 0..8 single pass (up to 32768
-# keys), 9 / 10 = 32768 keys over 2 / 4 column slices.  Numeric: b = 0..7 single
-# pass (up to 16384 key/value slots), 8 / 9 = 16384 slots over 2 / 4 slices.
-SYM_TOP, SYM_SLICED = 8, (9, 10)
-NUM_TOP, NUM_SLICED = 7, (8, 9)
+# LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
+# Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
+# 1 / 2 / 4 / 8 column slices.  Numeric: b = 0..6 single pass (128 << b key/value
+# slots), 7..9 = 8192 slots over 2 / 4 / 8 slices.  Then the HBM path.
+SYM_SINGLE_TOP = 6
+NUM_SINGLE_TOP = 6
+SYM_SLICED = (7, 8, 9, 10)
+NUM_SLICED = (7, 8, 9)
 SYM_GLOBAL = 11
 NUM_GLOBAL = 10
 LOAD = CONFIG.spgemm_load              # max load factor of an LDS table (per slice)
@@ -58,11 +61,15 @@ class SpgemmInfo:
     resorted_rows: int = 0
 
 
-def _bins(counts: torch.Tensor, top: int) -> torch.Tensor:
-    """Bin per row: smallest single-pass table with counts <= LOAD * S, then the
-    2- and 4-slice passes of the top table, then the HBM path; -1 for empty rows."""
-    caps = [int(LOAD * (128 << b)) for b in range(top + 1)]
-    caps += [2 * caps[-1], 4 * caps[-1]]
+def _bins(counts: torch.Tensor, numeric: int) -> torch.Tensor:
+    """Bin per row: the smallest single-pass table with counts <= LOAD * S, then
+    the sliced passes (slice capacity LOAD * S_top * slices), then the HBM path;
+    -1 for empty rows."""
+    caps = [int(LOAD * (128 << b)) for b in range(7)]
+    if numeric:
+        caps += [int(LOAD * 8192) * k for k in (2, 4, 8)]
+    else:
+        caps += [int(LOAD * 16384) * k for k in (1, 2, 4, 8)]
     b = torch.bucketize(counts, torch.tensor(caps, device=counts.device, dtype=counts.dtype))
     return torch.where(counts == 0, torch.full_like(b, -1), b)
 
@@ -144,7 +151,7 @@ def _dummies(dev):
 
 
 def _splits(B: CSR) -> torch.Tensor:
-    sp = torch.empty(B.m * 3, dtype=torch.int64, device=B.device)
+    sp = torch.empty(B.m * 7, dtype=torch.int64, device=B.device)
     _native.check(_native.hip().spmm_spgemm_row_splits(_native.ptr(B.rowptr), _native.ptr(B.col), B.m, B.n,
                                                         _native.ptr(sp), _native.stream_ptr(B.device)),
                   "spgemm_row_splits")
@@ -156,8 +163,8 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
     lib = _native.hip()
     P = _native.ptr
     stream = _native.stream_ptr(dev)
-    top, sliced, glob = (NUM_TOP, NUM_SLICED, NUM_GLOBAL) if numeric else (SYM_TOP, SYM_SLICED, SYM_GLOBAL)
-    order, groups = _group(_bins(counts, top), glob + 1)
+    sliced, glob = (NUM_SLICED, NUM_GLOBAL) if numeric else (SYM_SLICED, SYM_GLOBAL)
+    order, groups = _group(_bins(counts, numeric), glob + 1)
     splits = None
     global_rows = []
     for b, off, cnt in groups:
@@ -166,7 +173,8 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
         if b == glob:
             global_rows.append(rows)
             continue
-        if b in sliced and splits is None:
+        multi_slice = b in NUM_SLICED if numeric else b in SYM_SLICED[1:]
+        if multi_slice and splits is None:
             splits = _splits(B)
         _native.check(lib.spmm_spgemm_lds(b, numeric, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
                                           P(B.val), P(splits) if splits is not None else None, P(rows), cnt, B.n,
@@ -205,6 +213,8 @@ def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo) -> CSR:
     flags = torch.zeros(m, dtype=torch.int32, device=dev)
     _run_bins(1, A, B, row_nnz, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num)
     C_ = CSR(m, B.n, rowptr, Cci, Cv)
+    if bool(((flags & 4) != 0).any()):
+        raise RuntimeError("spgemm numeric: output position out of range (kernel invariant violated)")
     bad = ((flags & 1) != 0).nonzero().flatten()
     if bad.numel():
         info.resorted_rows = int(bad.numel())

@@ -1,6 +1,8 @@
 """SpGEMM phase diagnostics on the GPU: per-phase shader cycles per row for the
-symbolic and numeric LDS kernels (diagnostic stamps, csr_spgemm.hip), plus
-wall-clock of each phase.  usage: python tools/spgemm_diag.py [n] [density]"""
+symbolic and numeric LDS kernels (diagnostic stamps in csr_spgemm.hip), with
+diagnostic modes 0 = normal, 1 = loads only (inserts skipped), 2 = inserts of
+synthetic keys (no B loads).  Outputs of modes 1/2 are garbage by design.
+usage: python tools/spgemm_diag.py [n] [density] [modes]"""
 import ctypes as C
 import os
 import sys
@@ -16,6 +18,7 @@ from spmm_amd.utils import gen_csr  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 d = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-4
+modes = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 2]
 dev = torch.device("cuda")
 A = gen_csr.uniform_csr(n, n, d, seed=1, device=dev)
 B = gen_csr.uniform_csr(n, n, d, seed=2, device=dev)
@@ -26,22 +29,25 @@ C_ = SG.spgemm(A, B, info)  # warm
 del C_
 torch.cuda.synchronize()
 nprod = SG.row_nprod(A, B)
-for phase in ("symbolic", "numeric"):
-    lib.spmm_spgemm_stamps(1, None)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if phase == "symbolic":
-        row_nnz = SG.symbolic(A, B, nprod, SG.SpgemmInfo())
-    else:
-        Cm = SG.numeric(A, B, row_nnz, SG.SpgemmInfo())
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    lib.spmm_spgemm_stamps(-1, buf)
-    rows = max(buf[7], 1)
-    names = ["init+staging", "inserts", "rank", "write"]
-    per = {names[i]: buf[i] / rows for i in range(4)}
-    tot = sum(per.values())
-    print(f"{phase}: wall {dt * 1e3:.1f} ms, LDS-kernel rows {buf[7]}, cycles/row " +
-          ", ".join(f"{k} {v:.0f} ({v / max(tot, 1) * 100:.0f}%)" for k, v in per.items()))
+row_nnz = SG.symbolic(A, B, nprod, SG.SpgemmInfo())
+for mode in modes:
+    for phase in ("symbolic", "numeric"):
+        lib.spmm_spgemm_stamps(1 | (mode << 1), None)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if phase == "symbolic":
+            SG.symbolic(A, B, nprod, SG.SpgemmInfo())
+        else:
+            Cm = SG.numeric(A, B, row_nnz, SG.SpgemmInfo())
+            del Cm
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        lib.spmm_spgemm_stamps(-1, buf)
+        rows = max(buf[7], 1)
+        names = ["init+staging", "inserts", "rank", "write"]
+        per = {names[i]: buf[i] / rows for i in range(4)}
+        tot = sum(per.values())
+        print(f"mode {mode} {phase}: wall {dt * 1e3:.1f} ms, rows {buf[7]}, cycles/row " +
+              ", ".join(f"{k} {v:.0f} ({v / max(tot, 1) * 100:.0f}%)" for k, v in per.items()), flush=True)
 lib.spmm_spgemm_stamps(0, None)
 print("bins sym", info.rows_per_bin_sym, "num", info.rows_per_bin_num, "flops", info.flops, "nnz", info.nnz)
