@@ -27,12 +27,12 @@
 namespace {
 
 constexpr int EMPTY = -1;
+constexpr int NOKEY = -2;   // never in a table: a CAS comparing against it only reads
 
 // Diagnostic phase stamps (off unless the host sets g_stamp_on): thread 0 of
 // every workgroup adds the shader-clock cycles of each phase, measured between
 // the workgroup barriers that delimit it.  Read with spmm_spgemm_stamps().
 __device__ int g_stamp_on = 0;
-__device__ int g_diag_mode = 0;   // diagnostics only: 1 = skip inserts, 2 = synthetic keys (no B loads)
 __device__ unsigned long long g_stamps[8];
 #define SPMM_STAMP(i)                                                              \
   do {                                                                             \
@@ -43,22 +43,24 @@ __device__ unsigned long long g_stamps[8];
     }                                                                              \
   } while (0)
 
-template <int NT>
-__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* total) {
+// Block-wide exclusive scan (+ total); ends with the block synchronised and
+// wsum still live: a second scan needs a barrier before it reuses wsum.
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* wsum, T* total) {
   constexpr int NW = NT / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
+  T x = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl_up(x, d);
+    T y = __shfl_up(x, d);
     if (lane >= d) x += y;
   }
   if (lane == 63) wsum[w] = x;
   __syncthreads();
-  int pre = 0, tot = 0;
+  T pre = 0, tot = 0;
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
-    int s = wsum[i];
+    T s = wsum[i];
     pre += (i < w) ? s : 0;
     tot += s;
   }
@@ -74,357 +76,412 @@ __device__ __forceinline__ int hash_home(int c, uint32_t mult) {
 }
 
 // ---------------------------------------------------------------------------
-// LDS-resident table.  S = hash range, TS = S + NT slots (the overflow tail lets
-// probes run forward without wrapping) + 4 EMPTY sentinels so cluster scans can
-// read 4 keys per step unguarded.
+// LDS-resident tables.  S = hash range, TS = S + NT slots (the overflow tail
+// lets probes run forward without wrapping).
 //
-// Product stream: the row's A entries (<= NT per batch) are staged in LDS with
-// their B row start and an exclusive prefix of B row lengths; the row's
-// intermediate products are then split into one contiguous range per wave and
-// walked 64 at a time (lane = product), so every lane is busy whatever the B
-// row lengths, B reads are coalesced, and D products per lane are fetched per
-// batch with the next batch's loads in flight while the current one is
-// inserted (register double buffer) to cover HBM latency.
+// Product stream (both phases): the row's A entries (<= NT per batch) are
+// staged in LDS (B-row segment start, A value) and cut into chunks of
+// G = 1 << lg products (16, 32 or 64, chosen by the host from the mean B-row
+// segment length).  A block scan lays the chunk descriptors (entry, chunk
+// index, valid lanes) out in LDS; lanes form groups of G and group g takes
+// chunks g, g + #groups, ... so a lane's product is b0 + G*k + lane: no
+// per-product search, coalesced B reads, a wave-uniform trip count.  D chunks
+// per lane are fetched per batch and the next batch's loads are in flight
+// while the current one is inserted (register double buffer; loads are never
+// predicated off, so the compiler keeps counted vmcnt waits).
 //
-// Sorted output (numeric): position of the key in slot s = (#occupied slots
-// before its cluster) + (#keys of its cluster that are smaller) — the monotone
-// hash guarantees keys of earlier clusters are smaller.  Every occupied slot
-// computes its rank independently (no serial per-cluster sort).
+// Symbolic: 32-bit keys, CAS-only linear probing in rounds (a CAS of
+// EMPTY -> key both claims a free slot and reports the occupant); every lane
+// issues all of its CASes of a round before looking at any result.
+//
+// Numeric: ORDERED linear probing over 64-bit slots (key | value bits).  An
+// insert walks forward from its home slot; at an occupant with a larger key it
+// swaps itself in (one 64-bit CAS) and carries the displaced pair onward, at
+// an equal key it adds its value (CAS), at a smaller key it moves on.  With
+// the monotone hash every cluster stays sorted and clusters are ordered, so
+// the table read in slot order IS the sorted row: the output position is just
+// the number of occupied slots before the slot (ballot + mbcnt + one block
+// scan over 64-slot windows).  A cheap adjacency check (DPP) flags any row
+// whose slots are not increasing (only possible after a wrap-around), and the
+// host re-sorts those rows.
 
-__device__ __forceinline__ int advance(const int* apre, int nb, int e, int p) {
-  // largest e' >= e with apre[e'] <= p  (apre[nb] > p)
-  if (apre[e + 1] > p) return e;
-  int lo = e + 1, step = 1, hi;
-  while (true) {
-    const int nx = lo + step;
-    if (nx >= nb || apre[nx] > p) { hi = nx < nb ? nx : nb; break; }
-    lo = nx;
-    step <<= 1;
-  }
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (apre[mid] <= p) lo = mid; else hi = mid;
-  }
-  return lo;
+// Smallest lg >= 4 whose worst-case chunk count fits the descriptor buffer
+// (chunks <= products / G + entries and products <= TS are both enforced).
+constexpr int lds_lg_min(int TS, int NT, int CCAP) {
+  int lg = 4;
+  while (lg < 6 && ((TS + (1 << lg) - 1) >> lg) + NT > CCAP) ++lg;
+  return lg;
 }
 
-template <int S, int NT, bool NUMERIC, int NP>
-__global__ __launch_bounds__(NT) void spgemm_lds(
-    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
-    const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
-    const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols,
-    int32_t* __restrict__ row_nnz, const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci,
-    float* __restrict__ Cv, int32_t* __restrict__ flags) {
-  constexpr int TS = S + NT;            // multiple of 4 (S, NT powers of two >= 64)
-  constexpr int PER = TS / NT;
-  constexpr int NW = NT / 64;
-  constexpr int ACAP = NT;
-  constexpr int QSTEP = 8 / NP;         // eighths of the column space per slice
-  // products per lane per fetch batch: deep where LDS already caps occupancy at
-  // one workgroup per CU, shallow (fewer VGPRs, more waves) for small tables
-  constexpr int D = NUMERIC ? 4 : ((NT >= 512) ? 8 : 4);
-  __shared__ __attribute__((aligned(16))) int keys[TS + 4];
-  __shared__ __attribute__((aligned(16))) float vals[NUMERIC ? TS : 4];
+template <int S, int NT>
+struct LdsGeom {
+  static constexpr int TS = S + NT;        // multiple of 64
+  static constexpr int NW = NT / 64;
+  static constexpr int ACAP = NT;          // A entries per batch
+  static constexpr int CCAP = (S / NT >= 32) ? 3 * NT : 2 * NT;   // chunk descriptors per batch
+  static constexpr int LG_MIN = lds_lg_min(TS, NT, CCAP);
+  static constexpr int NWIN = TS / 64;
+  static_assert(((TS + 63) >> 6) + NT <= CCAP, "descriptor buffer too small even for 64-lane chunks");
+  static_assert(NWIN <= CCAP, "window counts reuse the descriptor buffer");
+  static_assert(NT <= 512, "entry index is 9 bits in a chunk descriptor");
+};
+
+// Stage one batch of A entries of a row slice: B-row segment starts (abeg) and
+// A values (aval) in LDS, one block scan for the chunk offsets and the product
+// total.  Ends synchronised.  The caller checks the capacities, then calls
+// write_chunks().
+template <int NT, int NP, bool VALUES>
+__device__ __forceinline__ void stage_batch(const int32_t* __restrict__ Aci, const float* __restrict__ Av,
+                                            const int64_t* __restrict__ Brp, const int64_t* __restrict__ bsplit,
+                                            int64_t abase, int nb, int q0, int q1, int lgE, int64_t* abeg,
+                                            float* aval, int64_t* wsum, int& len, int& nch, int& pre, int& TC,
+                                            int64_t& tot) {
+  const int tid = threadIdx.x;
+  len = 0;
+  if (tid < nb) {
+    const int j = Aci[abase + tid];
+    const int64_t rb = Brp[j], re = Brp[j + 1];
+    const int64_t b0 = (NP == 1 || q0 == 0) ? rb : bsplit[(int64_t)j * 7 + q0 - 1];
+    const int64_t b1 = (NP == 1 || q1 == 8) ? re : bsplit[(int64_t)j * 7 + q1 - 1];
+    len = (int)(b1 - b0);
+    abeg[tid] = b0;
+    if constexpr (VALUES) aval[tid] = Av[abase + tid];
+  }
+  nch = (len + (1 << lgE) - 1) >> lgE;
+  // one scan: chunk offsets (low word) and the product total (high word)
+  int64_t both;
+  const int64_t pk = block_excl_scan<NT, int64_t>(((int64_t)len << 32) | nch, wsum, &both);
+  pre = (int)(pk & 0xffffffff);
+  TC = (int)(both & 0xffffffff);
+  tot = (int64_t)((uint64_t)both >> 32);
+}
+
+__device__ __forceinline__ void write_chunks(int* clist, int len, int nch, int pre, int lgE) {
+  const int G = 1 << lgE;
+  for (int k = 0; k < nch; ++k) {
+    const int lim = (len - (k << lgE)) < G ? (len - (k << lgE)) : G;
+    clist[pre + k] = threadIdx.x | (lim << 9) | (k << 16);
+  }
+}
+
+// Chunk round i of a lane group = descriptor gid + i * ngrp.  Fills D products
+// per lane: column, B value, A value, valid flag.
+template <int D, bool VALUES>
+__device__ __forceinline__ void fetch_chunks(int i0, int gid, int ngrp, int gl, int lgE, int TC, const int* clist,
+                                             const int64_t* abeg, const float* aval, const int32_t* __restrict__ Bci,
+                                             const float* __restrict__ Bv, int (&c)[D], float (&bv)[D],
+                                             float (&av)[D], bool (&v)[D]) {
+  int d[D], t[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    t[u] = gid + (i0 + u) * ngrp;
+    d[u] = clist[t[u] < TC ? t[u] : TC - 1];   // clamped: every LDS read issues, one wait
+  }
+  int64_t eb[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    eb[u] = abeg[d[u] & 511];
+    if constexpr (VALUES) av[u] = aval[d[u] & 511];
+  }
+  int64_t f[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    const int lim = (d[u] >> 9) & 127, k = d[u] >> 16;
+    v[u] = (t[u] < TC) & (gl < lim);
+    f[u] = v[u] ? eb[u] + (k << lgE) + gl : 0;   // 0: a valid B index (TC > 0); loads never predicated off
+  }
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    c[u] = Bci[f[u]];
+    if constexpr (VALUES) bv[u] = Bv[f[u]];
+  }
+}
+
+// ------------------------------------------------------------- symbolic ----
+template <int S, int NT, int NP>
+__global__ __launch_bounds__(NT, 4) void spgemm_lds_sym(
+    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const int64_t* __restrict__ Brp,
+    const int32_t* __restrict__ Bci, const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows,
+    int ncols, int lg, int32_t* __restrict__ row_nnz, int32_t* __restrict__ flags) {
+  using Gm = LdsGeom<S, NT>;
+  constexpr int TS = Gm::TS, NW = Gm::NW, ACAP = Gm::ACAP, CCAP = Gm::CCAP;
+  constexpr int QSTEP = 8 / NP;
+  constexpr int D = (S >= 16384) ? 8 : 4;   // deeper where LDS caps occupancy anyway
+  __shared__ __attribute__((aligned(16))) int keys[TS];
   __shared__ int64_t abeg[ACAP];
-  __shared__ int apre[ACAP + 1];
-  __shared__ float aval[NUMERIC ? ACAP : 1];
-  __shared__ int wsum[NW];
-  __shared__ int s_count, s_wrapped;
+  __shared__ int clist[CCAP];
+  __shared__ int64_t wsum[NW];
+  __shared__ int s_count;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform
   const int row = rows[blockIdx.x];
   const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
+  const int lgE = lg > Gm::LG_MIN ? lg : Gm::LG_MIN;
+  const int ngrp = NW << (6 - lgE);                         // lane groups in the workgroup
+  const int gid = (w << (6 - lgE)) + (lane >> lgE);
+  const int gl = lane & ((1 << lgE) - 1);
   const int stamp_on = g_stamp_on;
-  const int diag = g_diag_mode;
   unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;
-  int written = 0;      // numeric: entries of earlier slices already stored
-  int row_count = 0;    // symbolic: distinct columns over all slices
+  int row_count = 0;
 
   for (int sl = 0; sl < NP; ++sl) {
-    // column slice [clo, chi) and its monotone hash
     const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
     const int clo = (int)(((int64_t)q0 * ncols) >> 3), chi = (int)(((int64_t)q1 * ncols) >> 3);
     const uint32_t mult = hash_mult(S, chi - clo);
-    for (int i = tid; i < (TS + 4) / 4; i += NT) reinterpret_cast<int4*>(keys)[i] = make_int4(EMPTY, EMPTY, EMPTY, EMPTY);
-    if constexpr (NUMERIC) {
-      for (int i = tid; i < TS / 4; i += NT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (tid == 0) { s_count = 0; s_wrapped = 0; }
+    for (int i = tid; i < TS / 4; i += NT) reinterpret_cast<int4*>(keys)[i] = make_int4(EMPTY, EMPTY, EMPTY, EMPTY);
+    if (tid == 0) s_count = 0;
     int mine = 0;
     int64_t slice_products = 0;
     bool overflow = false;
-
     for (int64_t bat = 0; bat < na; bat += ACAP) {
       const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
       __syncthreads();  // init done / previous batch consumed
-      int len = 0;
-      if (tid < nb) {
-        const int j = Aci[a0 + bat + tid];
-        const int64_t rb = Brp[j], re = Brp[j + 1];
-        const int64_t b0 = (NP == 1 || q0 == 0) ? rb : bsplit[(int64_t)j * 7 + q0 - 1];
-        const int64_t b1 = (NP == 1 || q1 == 8) ? re : bsplit[(int64_t)j * 7 + q1 - 1];
-        len = (int)(b1 - b0);
-        abeg[tid] = b0;
-        if constexpr (NUMERIC) aval[tid] = Av[a0 + bat + tid];
-      }
-      int tot;
-      const int pre = block_excl_scan<NT>(len, wsum, &tot);
-      if (tid < nb) apre[tid] = pre;
-      if (tid == 0) apre[nb] = tot;
-      __syncthreads();
+      int len, nch, pre, TC;
+      int64_t tot;
+      stage_batch<NT, NP, false>(Aci, nullptr, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, nullptr, wsum, len,
+                                 nch, pre, TC, tot);
       SPMM_STAMP(0);
-      // Distinct keys <= products: a slice whose products could exceed the
-      // table is handed to the HBM path instead (a full table would never
-      // terminate a probe).
+      // distinct keys <= products: a slice that could overfill the table goes to the HBM path
       slice_products += tot;
-      if (slice_products > TS - 8) { overflow = true; break; }
+      if (slice_products > TS - 8 || TC > CCAP) { overflow = true; break; }
+      if (TC == 0) continue;
+      write_chunks(clist, len, nch, pre, lgE);
+      __syncthreads();
 
-      // This wave's contiguous share of the products; lane takes D consecutive
-      // products per batch with its current A entry cached in registers.
-      int nlog = 0;
-      while ((1 << nlog) < nb) ++nlog;   // binary-search depth over nb entries (uniform)
-      const int Q = (tot + NW - 1) / NW;
-      const int pbeg = w * Q;
-      const int pend = (pbeg + Q < tot) ? pbeg + Q : tot;
-      const int nbat = (pend > pbeg) ? (pend - pbeg + 64 * D - 1) / (64 * D) : 0;
-      if (nbat > 0) {
-        int cA[D], cB[D];
-        float bA[D], bB[D], aA[D], aB[D];
-        auto fetch = [&](int bt, int (&c)[D], float (&bv)[D], float (&av)[D]) {
-          // entry of each product: D independent binary searches over apre with a
-          // wave-uniform trip count (no divergent per-lane advance loops)
-          int64_t f[D];
-          int lo[D], hi[D], pp[D];
-          const int p0 = pbeg + (bt * 64 + lane) * D;
+      int cA[D], cB[D];
+      float dummy[D];
+      bool vA[D], vB[D];
+      auto consume = [&](const int (&c)[D], const bool (&v)[D]) {
+        // every lane issues its CAS each round; finished / invalid lanes compare
+        // against NOKEY (never stored), i.e. a read: no exec-mask branches
+        int h[D];
+        bool st[D];
 #pragma unroll
-          for (int u = 0; u < D; ++u) {
-            pp[u] = (p0 + u < pend) ? p0 + u : pend - 1;   // clamp: always a valid product
-            lo[u] = 0;
-            hi[u] = nb;
-          }
-          for (int it = 0; it < nlog; ++it) {
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-              const int mid = (lo[u] + hi[u]) >> 1;
-              if (apre[mid] <= pp[u]) lo[u] = mid; else hi[u] = mid;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < D; ++u) {
-            f[u] = abeg[lo[u]] + (pp[u] - apre[lo[u]]);
-            if constexpr (NUMERIC) av[u] = aval[lo[u]];
-          }
-          if (diag == 2) {
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-              c[u] = clo + (int)__umulhi((uint32_t)(f[u] * 2654435761ull), (uint32_t)(chi - clo));
-              if constexpr (NUMERIC) bv[u] = 1.f;
-            }
-            return;
-          }
-#pragma unroll
-          for (int u = 0; u < D; ++u) {
-            c[u] = Bci[f[u]];
-            if constexpr (NUMERIC) bv[u] = Bv[f[u]];
-          }
-        };
-        auto consume = [&](int bt, const int (&c)[D], const float (&bv)[D], const float (&av)[D]) {
-          const int p0 = pbeg + (bt * 64 + lane) * D;
-          if (diag == 1) {   // keep the loaded values live, skip the table
-#pragma unroll
-            for (int u = 0; u < D; ++u) mine ^= (p0 + u < pend) ? (c[u] & 1) : 0;
-            return;
-          }
-          // CAS-only linear probing in rounds over the lane's D keys: a CAS of
-          // EMPTY -> key both claims a free slot and reports the occupant
-          // (one LDS op per probe step; ds_cmpst costs ~11 cycles per
-          // wave-instruction on gfx950, a read + CAS pair ~17).  A key u is
-          // only touched while some lane still has it pending.
-          int h[D], st[D];
-#pragma unroll
-          for (int u = 0; u < D; ++u) {
-            const int hk = c[u] - clo;
-            h[u] = mult ? (int)__umulhi((uint32_t)hk, mult) : hk;
-            st[u] = (p0 + u < pend) ? 1 : 0;   // 1 = pending
-          }
-          while (true) {
-            bool more = false;
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-              if (__any(st[u] != 0)) {
-                if (st[u]) {
-                  const int old = atomicCAS(&keys[h[u]], EMPTY, c[u]);
-                  if (old == EMPTY) { ++mine; st[u] = 0; }
-                  else if (old == c[u]) st[u] = 0;
-                  else if (++h[u] >= TS) { h[u] = 0; s_wrapped = 1; }
-                }
-                more |= st[u] != 0;
-              }
-            }
-            if (!__any(more)) break;
-          }
-          if constexpr (NUMERIC) {
-            // float accumulate by read + CAS (ds_add_f32 serialises lanes: ~192
-            // cycles per wave-instruction measured on gfx950)
-            int ob[D];
-            bool pendv[D];
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-              pendv[u] = p0 + u < pend;
-              ob[u] = pendv[u] ? __hip_atomic_load(reinterpret_cast<int*>(&vals[h[u]]), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
-            }
-            while (true) {
-              bool again = false;
-#pragma unroll
-              for (int u = 0; u < D; ++u) {
-                if (pendv[u]) {
-                  const int nv = __float_as_int(__int_as_float(ob[u]) + av[u] * bv[u]);
-                  const int o = atomicCAS(reinterpret_cast<int*>(&vals[h[u]]), ob[u], nv);
-                  if (o == ob[u]) pendv[u] = false;
-                  else { ob[u] = o; again = true; }
-                }
-              }
-              if (!__any(again)) break;
-            }
-          }
-        };
-        fetch(0, cA, bA, aA);
-        for (int bt = 0; bt < nbat; bt += 2) {
-          fetch(bt + 1, cB, bB, aB);
-          consume(bt, cA, bA, aA);
-          fetch(bt + 2, cA, bA, aA);
-          consume(bt + 1, cB, bB, aB);
+        for (int u = 0; u < D; ++u) {
+          h[u] = v[u] ? hash_home(c[u] - clo, mult) : 0;
+          st[u] = v[u];
         }
+        while (true) {
+          int old[D];
+#pragma unroll
+          for (int u = 0; u < D; ++u) old[u] = atomicCAS(&keys[h[u]], st[u] ? EMPTY : NOKEY, c[u]);
+          bool more = false;
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            mine += (st[u] & (old[u] == EMPTY)) ? 1 : 0;
+            const bool again = st[u] & (old[u] != EMPTY) & (old[u] != c[u]);
+            h[u] += again ? 1 : 0;
+            h[u] = (h[u] >= TS) ? 0 : h[u];   // wrap: only counts matter here
+            st[u] = again;
+            more |= again;
+          }
+          if (!__any(more)) break;
+        }
+      };
+      const int nit = (TC + ngrp - 1) / ngrp;   // chunk rounds of the busiest group (wave-uniform)
+      fetch_chunks<D, false>(0, gid, ngrp, gl, lgE, TC, clist, abeg, nullptr, Bci, nullptr, cA, dummy, dummy, vA);
+      for (int i = 0; i < nit; i += 2 * D) {
+        fetch_chunks<D, false>(i + D, gid, ngrp, gl, lgE, TC, clist, abeg, nullptr, Bci, nullptr, cB, dummy, dummy,
+                               vB);
+        consume(cA, vA);
+        fetch_chunks<D, false>(i + 2 * D, gid, ngrp, gl, lgE, TC, clist, abeg, nullptr, Bci, nullptr, cA, dummy,
+                               dummy, vA);
+        consume(cB, vB);
       }
     }
     if (overflow) {
       if (tid == 0) flags[row] |= 2;
-      return;   // uniform: every thread saw the same slice_products
+      return;   // uniform: every thread saw the same totals
+    }
+    SPMM_STAMP(1);
+    if (mine) atomicAdd(&s_count, mine);
+    __syncthreads();
+    row_count += s_count;
+    __syncthreads();   // s_count read before the next slice resets it
+  }
+  if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
+  if (tid == 0) row_nnz[row] = row_count;
+}
+
+// -------------------------------------------------------------- numeric ----
+constexpr unsigned long long EMPTY64 = 0x00000000FFFFFFFFull;   // key EMPTY, value +0
+constexpr unsigned long long NOKEY64 = 0xFFFFFFFEFFFFFFFEull;   // never in a table: CAS against it is a read
+
+template <int S, int NT, int NP>
+__global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
+    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
+    const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
+    const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols, int lg,
+    const int32_t* __restrict__ row_nnz, const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci,
+    float* __restrict__ Cv, int32_t* __restrict__ flags) {
+  using Gm = LdsGeom<S, NT>;
+  constexpr int TS = Gm::TS, NW = Gm::NW, ACAP = Gm::ACAP, CCAP = Gm::CCAP, NWIN = Gm::NWIN;
+  constexpr int QSTEP = 8 / NP;
+  constexpr int D = 4;
+  __shared__ __attribute__((aligned(16))) unsigned long long tab[TS + 2];   // key (low word) | value bits (high)
+  __shared__ int64_t abeg[ACAP];
+  __shared__ int clist[CCAP];           // chunk descriptors; later the per-window counts
+  __shared__ float aval[ACAP];
+  __shared__ int64_t wsum[NW];
+  __shared__ int s_wrapped;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = rows[blockIdx.x];
+  const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
+  const int lgE = lg > Gm::LG_MIN ? lg : Gm::LG_MIN;
+  const int ngrp = NW << (6 - lgE);
+  const int gid = (w << (6 - lgE)) + (lane >> lgE);
+  const int gl = lane & ((1 << lgE) - 1);
+  const int stamp_on = g_stamp_on;
+  unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;
+  int written = 0;   // entries of earlier slices already stored
+  bool unsorted = false;
+
+  for (int sl = 0; sl < NP; ++sl) {
+    const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
+    const int clo = (int)(((int64_t)q0 * ncols) >> 3), chi = (int)(((int64_t)q1 * ncols) >> 3);
+    const uint32_t mult = hash_mult(S, chi - clo);
+    for (int i = tid; i < (TS + 2) / 2; i += NT)
+      reinterpret_cast<ulonglong2*>(tab)[i] = make_ulonglong2(EMPTY64, EMPTY64);
+    if (tid == 0) s_wrapped = 0;
+    int64_t slice_products = 0;
+    bool overflow = false;
+    for (int64_t bat = 0; bat < na; bat += ACAP) {
+      const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
+      __syncthreads();
+      int len, nch, pre, TC;
+      int64_t tot;
+      stage_batch<NT, NP, true>(Aci, Av, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, aval, wsum, len, nch, pre,
+                                TC, tot);
+      SPMM_STAMP(0);
+      slice_products += tot;
+      if (slice_products > TS - 8 || TC > CCAP) { overflow = true; break; }
+      if (TC == 0) continue;
+      write_chunks(clist, len, nch, pre, lgE);
+      __syncthreads();
+
+      int cA[D], cB[D];
+      float bA[D], bB[D], aA[D], aB[D];
+      bool vA[D], vB[D];
+      auto consume = [&](const int (&c)[D], const float (&bv)[D], const float (&av)[D], const bool (&v)[D]) {
+        int h[D];
+        uint32_t ck[D];
+        float cv[D];
+        unsigned long long cur[D];
+        bool st[D];
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+          h[u] = v[u] ? hash_home(c[u] - clo, mult) : 0;
+          ck[u] = (uint32_t)c[u];
+          cv[u] = av[u] * bv[u];
+          cur[u] = EMPTY64;   // belief about tab[h]
+          st[u] = v[u];
+        }
+        while (true) {
+          // every lane issues its CAS each round; finished / invalid lanes
+          // compare against NOKEY64 (never stored), i.e. a read
+          unsigned long long old[D];
+#pragma unroll
+          for (int u = 0; u < D; ++u) {
+            const uint32_t k = (uint32_t)cur[u];
+            const float nv = (k == ck[u]) ? __uint_as_float((uint32_t)(cur[u] >> 32)) + cv[u] : cv[u];
+            const unsigned long long want = ((unsigned long long)__float_as_uint(nv) << 32) | ck[u];
+            old[u] = atomicCAS(&tab[h[u]], st[u] ? cur[u] : NOKEY64, want);
+          }
+          bool more = false, wrap = false;
+#pragma unroll
+          for (int u = 0; u < D; ++u) {   // branch-free state update (selects only)
+            const uint32_t k = (uint32_t)cur[u];
+            const bool landed = st[u] & (old[u] == cur[u]);
+            const bool done = landed & ((k == (uint32_t)EMPTY) | (k == ck[u]));   // placed / merged
+            const bool disp = landed & !done;                                    // displaced a larger key
+            const bool adv = st[u] & !landed & ((uint32_t)old[u] < ck[u]);      // smaller key (EMPTY is largest)
+            const bool step = disp | adv;
+            ck[u] = disp ? k : ck[u];
+            cv[u] = disp ? __uint_as_float((uint32_t)(cur[u] >> 32)) : cv[u];
+            cur[u] = step ? EMPTY64 : old[u];
+            h[u] += step ? 1 : 0;
+            wrap |= h[u] >= TS;
+            h[u] = (h[u] >= TS) ? 0 : h[u];
+            st[u] = st[u] & !done;
+            more |= st[u];
+          }
+          if (__any(wrap)) s_wrapped = 1;
+          if (!__any(more)) break;
+        }
+      };
+      const int nit = (TC + ngrp - 1) / ngrp;
+      fetch_chunks<D, true>(0, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cA, bA, aA, vA);
+      for (int i = 0; i < nit; i += 2 * D) {
+        fetch_chunks<D, true>(i + D, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cB, bB, aB, vB);
+        consume(cA, bA, aA, vA);
+        fetch_chunks<D, true>(i + 2 * D, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cA, bA, aA, vA);
+        consume(cB, bB, aB, vB);
+      }
+    }
+    if (overflow) {
+      if (tid == 0) flags[row] |= 2;
+      return;
     }
     __syncthreads();
     SPMM_STAMP(1);
-    if (mine) atomicAdd(&s_count, mine);
-    if constexpr (!NUMERIC) {
-      __syncthreads();
-      row_count += s_count;
-      continue;
-    } else {
-      // Sorted positions.  Windows of 64 slots (one wave-instruction each):
-      // occupancy ballots give per-window counts (scanned into apre, free now)
-      // and each key's cluster start without walking; the rank inside the
-      // cluster is a scan of the cluster (lanes of one cluster read the same
-      // addresses: LDS broadcast).
-      constexpr int NWIN = TS / 64;
-      constexpr int WPW = (NWIN + NW - 1) / NW;   // windows per wave, kept in registers
-      int kq[WPW];
-      float vq[WPW];
+    // Output = the table in slot order: position = occupied slots before it.
+    constexpr int WPW = (NWIN + NW - 1) / NW;
+    unsigned long long q[WPW];
 #pragma unroll
-      for (int j = 0; j < WPW; ++j) {
-        const int W = w + j * NW;
-        kq[j] = (W < NWIN) ? keys[W * 64 + lane] : EMPTY;
-        vq[j] = (W < NWIN) ? vals[W * 64 + lane] : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < WPW; ++j) {
-        const int W = w + j * NW;
-        const unsigned long long M = __ballot(kq[j] != EMPTY);
-        if (lane == 0 && W < NWIN) apre[W] = __popcll(M);
-      }
+    for (int j = 0; j < WPW; ++j) {
+      const int W = w + j * NW;
+      q[j] = (W < NWIN) ? tab[W * 64 + lane] : EMPTY64;
+      const unsigned long long M = __ballot((uint32_t)q[j] != (uint32_t)EMPTY);
+      if (lane == 0 && W < NWIN) clist[W] = __popcll(M);
+    }
+    __syncthreads();
+    int total;
+    {
+      const int cw = (tid < NWIN) ? clist[tid] : 0;
+      const int bw = block_excl_scan<NT, int>(cw, reinterpret_cast<int*>(wsum), &total);
       __syncthreads();
-      int total;
-      {
-        const int cw = (tid < NWIN) ? apre[tid] : 0;
-        const int bw = block_excl_scan<NT>(cw, wsum, &total);
-        __syncthreads();
-        if (tid < NWIN) apre[tid] = bw;
-      }
-      __syncthreads();
-      const bool wrapped = s_wrapped != 0;
-      const int64_t base = Crp[row] + written;
-      // symbolic fixed the row's size; never store past it whatever happened here
-      const int room = row_nnz[row] - written;
-      const int lim = total < room ? total : room;
-      if (tid == 0 && total > room) flags[row] |= 4;
-      const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-      const int rlo = lane & ~15;   // first lane of this lane's 16-lane DPP row
+      if (tid < NWIN) clist[tid] = bw;
+    }
+    __syncthreads();
+    const int64_t base = Crp[row] + written;
+    // symbolic fixed the row's size; never store past it whatever happened here
+    const int room = row_nnz[row] - written;
+    const int lim = total < room ? total : room;
+    if (tid == 0 && total > room) atomicOr(&flags[row], 4);
+    bool bad = false;
 #pragma unroll
-      for (int j = 0; j < WPW; ++j) {
-        const int W = w + j * NW;
-        if (W < NWIN) {
-          const int key = kq[j];
-          const unsigned long long M = __ballot(key != EMPTY);
-          // neighbours inside the 16-lane row (DPP row shifts, no LDS traffic)
-          const int m1 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x111, 0xF, 0xF, false);
-          const int m2 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x112, 0xF, 0xF, false);
-          const int m3 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x113, 0xF, 0xF, false);
-          const int p1 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x101, 0xF, 0xF, false);
-          const int p2 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x102, 0xF, 0xF, false);
-          const int p3 = __builtin_amdgcn_update_dpp(EMPTY, key, 0x103, 0xF, 0xF, false);
-          if (key != EMPTY) {
-            int pos;
-            if (wrapped) {
-              pos = apre[W] + __popcll(M & below);
-            } else {
-              const unsigned long long zb = ~M & below;                       // empty slots below me
-              const unsigned long long za = ~M & ~(below | (1ull << lane));   // empty slots above me
-              const int ci = zb ? 64 - __builtin_clzll(zb) : -1;              // cluster start lane (-1: before window)
-              const int ce = za ? __builtin_ctzll(za) : 64;                   // cluster end lane (64: past window)
-              int Pcs, cs;
-              if (ci >= 0) {
-                cs = W * 64 + ci;
-                Pcs = apre[W] + __popcll(M & (ci ? (~0ull >> (64 - ci)) : 0ull));
-              } else {
-                cs = W * 64;
-                while (cs > 0 && keys[cs - 1] != EMPTY) --cs;
-                Pcs = apre[W] - (W * 64 - cs);
-              }
-              int r = 0;
-              if (ci >= rlo && ce < 64 && ce <= rlo + 16 && ce - ci <= 4) {   // whole cluster within 3 lanes, same row
-                r += (lane - 1 >= ci) & (m1 < key);
-                r += (lane - 2 >= ci) & (m2 < key);
-                r += (lane - 3 >= ci) & (m3 < key);
-                r += (lane + 1 < ce) & (p1 < key);
-                r += (lane + 2 < ce) & (p2 < key);
-                r += (lane + 3 < ce) & (p3 < key);
-              } else {   // long or boundary-crossing cluster: scan it in LDS
-                int x = cs;
-                while (true) {
-                  const int k0 = keys[x], k1 = keys[x + 1], k2 = keys[x + 2], k3 = keys[x + 3];
-                  if (k0 == EMPTY) break;
-                  r += k0 < key;
-                  if (k1 == EMPTY) break;
-                  r += k1 < key;
-                  if (k2 == EMPTY) break;
-                  r += k2 < key;
-                  if (k3 == EMPTY) break;
-                  r += k3 < key;
-                  x += 4;
-                }
-              }
-              pos = Pcs + r;
-            }
-            if (pos >= 0 && pos < lim) {
-              Cci[base + pos] = key;
-              Cv[base + pos] = vq[j];
-            } else {
-              flags[row] |= 4;   // internal error: never write outside the row
-            }
+    for (int j = 0; j < WPW; ++j) {
+      const int W = w + j * NW;
+      if (W < NWIN) {
+        const uint32_t key = (uint32_t)q[j];
+        const bool occ = key != (uint32_t)EMPTY;
+        const unsigned long long M = __ballot(occ);
+        // adjacency check: the next slot's key must be larger (EMPTY is the largest)
+        uint32_t nk = (uint32_t)__builtin_amdgcn_update_dpp((int)EMPTY, (int)key, 0x130, 0xF, 0xF, false);   // wave_shl:1
+        if (lane == 63) nk = (W * 64 + 64 < TS) ? (uint32_t)tab[W * 64 + 64] : (uint32_t)EMPTY;
+        bad |= occ & (nk <= key);
+        if (occ) {
+          const int pos = clist[W] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+          if (pos < lim) {
+            Cci[base + pos] = (int)key;
+            Cv[base + pos] = __uint_as_float((uint32_t)(q[j] >> 32));
+          } else {
+            atomicOr(&flags[row], 4);   // internal error: never write outside the row
           }
         }
       }
-      SPMM_STAMP(2);
-      written += total;
-      if (tid == 0 && wrapped) flags[row] |= 1;
-      SPMM_STAMP(3);
-      __syncthreads();   // copy-out done before the next slice re-initialises the table
     }
+    unsorted |= bad | (s_wrapped != 0);
+    SPMM_STAMP(2);
+    written += total;
+    __syncthreads();   // slice done before the next slice re-initialises the table
   }
+  if (__any(unsorted) && lane == 0) atomicOr(&flags[row], 1);
   if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
-  if constexpr (!NUMERIC) {
-    if (tid == 0) row_nnz[row] = row_count;
-  }
 }
 
 // Eighth split points of every B row (rows column-sorted): bsplit[j*7 + q-1] =
@@ -527,7 +584,7 @@ __global__ __launch_bounds__(GNT) void spgemm_global(
   int cnt = 0;
   for (int64_t s = s0; s < s1; ++s) cnt += ld(&keys[s]) != EMPTY;
   int total;
-  int o = block_excl_scan<GNT>(cnt, wsum, &total);
+  int o = block_excl_scan<GNT, int>(cnt, wsum, &total);
   const int64_t base = Crp[row] + o;
   int64_t q = 0;
   for (int64_t s = s0; s < s1; ++s) {
@@ -555,13 +612,24 @@ __global__ __launch_bounds__(256) void spgemm_row_nprod(const int64_t* __restric
   if (lane == 0) nprod[row] = s;
 }
 
-template <int S, int NT, bool NUMERIC, int NP>
-int launch_lds(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
-               const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows, int ncols,
-               int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags, hipStream_t s) {
+template <int S, int NT, int NP>
+int launch_sym(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, const int32_t* Bci, const int64_t* bsplit,
+               const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz, int32_t* flags,
+               hipStream_t s) {
   if (nrows <= 0) return 0;
-  hipLaunchKernelGGL((spgemm_lds<S, NT, NUMERIC, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp,
-                     Bci, Bv, bsplit, rows, ncols, row_nnz, Crp, Cci, Cv, flags);
+  hipLaunchKernelGGL((spgemm_lds_sym<S, NT, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Brp, Bci, bsplit,
+                     rows, ncols, lg, row_nnz, flags);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int S, int NT, int NP>
+int launch_num(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
+               const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows, int ncols, int lg,
+               const int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags, hipStream_t s) {
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL((spgemm_lds_num<S, NT, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
+                     bsplit, rows, ncols, lg, row_nnz, Crp, Cci, Cv, flags);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -595,22 +663,24 @@ SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, i
 //   numeric  bins 0..6: 128 << b key/value slots, one pass; 7..9: 8192 slots x 2/4/8 slices
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
-                                const int32_t* rows, int64_t nrows, int ncols, int32_t* row_nnz, const int64_t* Crp,
-                                int32_t* Cci, float* Cv, int32_t* flags, void* stream) {
+                                const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz,
+                                const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-#define SPMM_ARGS Arp, Aci, Av, Brp, Bci, Bv, bsplit, rows, nrows, ncols, row_nnz, Crp, Cci, Cv, flags, s
+  if (lg < 4 || lg > 6) return (int)hipErrorInvalidValue;
+#define SPMM_NARGS Arp, Aci, Av, Brp, Bci, Bv, bsplit, rows, nrows, ncols, lg, row_nnz, Crp, Cci, Cv, flags, s
+#define SPMM_SARGS Arp, Aci, Brp, Bci, bsplit, rows, nrows, ncols, lg, row_nnz, flags, s
 #define SPMM_BIN(B, S, NT)                                                                   \
   case B:                                                                                     \
-    return numeric ? launch_lds<S, NT, true, 1>(SPMM_ARGS) : launch_lds<S, NT, false, 1>(SPMM_ARGS);
+    return numeric ? launch_num<S, NT, 1>(SPMM_NARGS) : launch_sym<S, NT, 1>(SPMM_SARGS);
   if (numeric) {
-    if (bin == 7) return launch_lds<8192, 512, true, 2>(SPMM_ARGS);
-    if (bin == 8) return launch_lds<8192, 512, true, 4>(SPMM_ARGS);
-    if (bin == 9) return launch_lds<8192, 512, true, 8>(SPMM_ARGS);
+    if (bin == 7) return launch_num<8192, 512, 2>(SPMM_NARGS);
+    if (bin == 8) return launch_num<8192, 512, 4>(SPMM_NARGS);
+    if (bin == 9) return launch_num<8192, 512, 8>(SPMM_NARGS);
   } else {
-    if (bin == 7) return launch_lds<16384, 512, false, 1>(SPMM_ARGS);
-    if (bin == 8) return launch_lds<16384, 512, false, 2>(SPMM_ARGS);
-    if (bin == 9) return launch_lds<16384, 512, false, 4>(SPMM_ARGS);
-    if (bin == 10) return launch_lds<16384, 512, false, 8>(SPMM_ARGS);
+    if (bin == 7) return launch_sym<16384, 512, 1>(SPMM_SARGS);
+    if (bin == 8) return launch_sym<16384, 512, 2>(SPMM_SARGS);
+    if (bin == 9) return launch_sym<16384, 512, 4>(SPMM_SARGS);
+    if (bin == 10) return launch_sym<16384, 512, 8>(SPMM_SARGS);
   }
   switch (bin) {
     SPMM_BIN(0, 128, 64)
@@ -624,7 +694,8 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
       return (int)hipErrorInvalidValue;
   }
 #undef SPMM_BIN
-#undef SPMM_ARGS
+#undef SPMM_NARGS
+#undef SPMM_SARGS
 }
 
 SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
@@ -650,10 +721,9 @@ SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_
 SPMM_EXPORT int spmm_spgemm_stamps(int on, unsigned long long* out8) {
   if (on >= 0) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int st = on & 1, mode = on >> 1;
+    const int st = on & 1;
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_on), &st, sizeof st);
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_diag_mode), &mode, sizeof mode);
     return (int)e;
   }
   hipError_t e = hipDeviceSynchronize();

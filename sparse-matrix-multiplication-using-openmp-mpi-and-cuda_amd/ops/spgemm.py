@@ -2,13 +2,15 @@
 
 GPU path (gfx950, ``csrc/kernels/csr_spgemm.hip``):
   1. ``nprod``: intermediate products per row (one wave per row).
-  2. Symbolic: rows binned by nprod into LDS hash kernels with table sizes
-     128 .. 32768 keys (load factor <= 0.75, 0.85 in the top bin); longer rows
-     go to the HBM-workspace kernel.  Output: exact nnz per row.
+  2. Symbolic: rows binned by nprod into LDS hash kernels (128 .. 8192 keys
+     single pass at load <= LOAD, 16384 keys over 1/2/4/8 column slices at load
+     <= LOAD_SLICED); longer rows go to the HBM-workspace kernel.  Output:
+     exact nnz per row.
   3. Row pointer by a device scan; C allocated once.
-  4. Numeric: rows re-binned by their exact nnz (tables 128 .. 16384 key/value
-     slots, 128 KiB of LDS at the top), monotone hashing + per-cluster sort, so
-     rows come out column-sorted without a sort pass.
+  4. Numeric: rows re-binned by their exact nnz (128 .. 8192 slot tables,
+     8192 slots over 2/4/8 slices for long rows); ordered linear probing with
+     a monotone hash keeps every table sorted, so the output is a compaction
+     of the table, no sort pass.
 CPU path: OpenMP Gustavson (``libspmm_host.so``), identical output layout.
 
 FLOPs are counted as 2 * sum(nprod) (one multiply + one add per intermediate
@@ -33,7 +35,7 @@ C_INT = C.c_int
 _native.register_hip("spmm_spgemm_row_nprod", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_row_splits", c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+                     C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_global", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp,
                      c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
@@ -48,7 +50,8 @@ SYM_SLICED = (7, 8, 9, 10)
 NUM_SLICED = (7, 8, 9)
 SYM_GLOBAL = 11
 NUM_GLOBAL = 10
-LOAD = CONFIG.spgemm_load              # max load factor of an LDS table (per slice)
+LOAD = CONFIG.spgemm_load              # max load factor of a single-pass LDS table
+LOAD_SLICED = CONFIG.spgemm_load_sliced   # ... of the big (column-sliced) tables
 GLOBAL_WS_BYTES = int(CONFIG.spgemm_global_ws_gb * (1 << 30))   # HBM budget per batch of global-table rows
 
 
@@ -59,6 +62,7 @@ class SpgemmInfo:
     rows_per_bin_sym: Dict[int, int] = field(default_factory=dict)
     rows_per_bin_num: Dict[int, int] = field(default_factory=dict)
     resorted_rows: int = 0
+    mean_seg: float = 0.0     # mean B-row length per A entry (products / nnz(A)); picks the LDS lane groups
 
 
 def _bins(counts: torch.Tensor, numeric: int) -> torch.Tensor:
@@ -67,9 +71,9 @@ def _bins(counts: torch.Tensor, numeric: int) -> torch.Tensor:
     -1 for empty rows."""
     caps = [int(LOAD * (128 << b)) for b in range(7)]
     if numeric:
-        caps += [int(LOAD * 8192) * k for k in (2, 4, 8)]
+        caps += [int(LOAD_SLICED * 8192) * k for k in (2, 4, 8)]
     else:
-        caps += [int(LOAD * 16384) * k for k in (1, 2, 4, 8)]
+        caps += [int(LOAD_SLICED * 16384) * k for k in (1, 2, 4, 8)]
     b = torch.bucketize(counts, torch.tensor(caps, device=counts.device, dtype=counts.dtype))
     return torch.where(counts == 0, torch.full_like(b, -1), b)
 
@@ -141,6 +145,7 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
     B = B if B.val.dtype == torch.float32 else B.with_values(B.val.float())
     nprod = row_nprod(A, B)
     info.flops = 2 * int(nprod.sum())
+    info.mean_seg = info.flops / 2 / max(A.nnz, 1)
     row_nnz = symbolic(A, B, nprod, info)
     return numeric(A, B, row_nnz, info)
 
@@ -148,6 +153,23 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
 def _dummies(dev):
     return (torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),
             torch.zeros(1, dtype=torch.float32, device=dev))
+
+
+def _slices(b: int, numeric: int) -> int:
+    """Column slices of LDS bin b."""
+    if numeric:
+        return {7: 2, 8: 4, 9: 8}.get(b, 1)
+    return {8: 2, 9: 4, 10: 8}.get(b, 1)
+
+
+def _group_log2(seg_len: float) -> int:
+    """log2 of the lanes per A-entry group in the LDS kernels: 64 lanes walk a
+    long B-row segment, 32 / 16 share a wave for short ones."""
+    if seg_len >= 40:
+        return 6
+    if seg_len >= 16:
+        return 5
+    return 4
 
 
 def _splits(B: CSR) -> torch.Tensor:
@@ -158,7 +180,8 @@ def _splits(B: CSR) -> torch.Tensor:
     return sp
 
 
-def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins):
+def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins,
+              mean_seg: float = 0.0):
     dev = A.device
     lib = _native.hip()
     P = _native.ptr
@@ -167,6 +190,7 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
     order, groups = _group(_bins(counts, numeric), glob + 1)
     splits = None
     global_rows = []
+    seg = mean_seg if mean_seg > 0 else B.nnz / max(B.m, 1)
     for b, off, cnt in groups:
         info_bins[b] = cnt
         rows = order[off:off + cnt]
@@ -178,7 +202,8 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
             splits = _splits(B)
         _native.check(lib.spmm_spgemm_lds(b, numeric, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
                                           P(B.val), P(splits) if splits is not None else None, P(rows), cnt, B.n,
-                                          P(row_nnz), P(Crp), P(Cci), P(Cv), P(flags), stream),
+                                          _group_log2(seg / _slices(b, numeric)), P(row_nnz), P(Crp), P(Cci),
+                                          P(Cv), P(flags), stream),
                       "spgemm_lds(numeric)" if numeric else "spgemm_lds(symbolic)")
     # rows whose column slice could overflow an LDS table were skipped by the kernel
     spill = ((flags & 2) != 0).nonzero().flatten().to(torch.int32)
@@ -196,7 +221,7 @@ def symbolic(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> torch.Ten
     row_nnz = torch.zeros(A.m, dtype=torch.int32, device=dev)
     flags = torch.zeros(A.m, dtype=torch.int32, device=dev)
     d64, d32, df = _dummies(dev)
-    _run_bins(0, A, B, nprod, row_nnz, d64, d32, df, flags, info.rows_per_bin_sym)
+    _run_bins(0, A, B, nprod, row_nnz, d64, d32, df, flags, info.rows_per_bin_sym, info.mean_seg)
     return row_nnz
 
 
@@ -211,7 +236,7 @@ def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo) -> CSR:
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     flags = torch.zeros(m, dtype=torch.int32, device=dev)
-    _run_bins(1, A, B, row_nnz, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num)
+    _run_bins(1, A, B, row_nnz, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num, info.mean_seg)
     C_ = CSR(m, B.n, rowptr, Cci, Cv)
     if bool(((flags & 4) != 0).any()):
         raise RuntimeError("spgemm numeric: output position out of range (kernel invariant violated)")

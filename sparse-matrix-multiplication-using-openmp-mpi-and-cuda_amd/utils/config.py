@@ -24,7 +24,10 @@ class Config:
     device: str = field(default_factory=lambda: _env("SPMM_DEVICE", "auto", str))
     comm: str = field(default_factory=lambda: _env("SPMM_COMM", "auto", str))
     streams: int = field(default_factory=lambda: _env("SPMM_STREAMS", 4, int))           # chain-level concurrency
-    spgemm_load: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD", 0.5, float))   # per LDS table slice
+    spgemm_load: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD", 0.5, float))   # single-pass LDS tables
+    # 16K-key (symbolic) / 8K-slot (numeric) tables of long rows: a higher load
+    # means fewer column slices, i.e. fewer re-reads of the B rows
+    spgemm_load_sliced: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD_SLICED", 0.7, float))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

@@ -1,8 +1,7 @@
 """SpGEMM phase diagnostics on the GPU: per-phase shader cycles per row for the
-symbolic and numeric LDS kernels (diagnostic stamps in csr_spgemm.hip), with
-diagnostic modes 0 = normal, 1 = loads only (inserts skipped), 2 = inserts of
-synthetic keys (no B loads).  Outputs of modes 1/2 are garbage by design.
-usage: python tools/spgemm_diag.py [n] [density] [modes]"""
+symbolic and numeric LDS kernels (diagnostic stamps in csr_spgemm.hip, taken
+by thread 0 of every workgroup between the barriers that delimit a phase).
+usage: python tools/spgemm_diag.py [n] [density]"""
 import ctypes as C
 import os
 import sys
@@ -18,7 +17,6 @@ from spmm_amd.utils import gen_csr  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 d = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-4
-modes = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 2]
 dev = torch.device("cuda")
 A = gen_csr.uniform_csr(n, n, d, seed=1, device=dev)
 B = gen_csr.uniform_csr(n, n, d, seed=2, device=dev)
@@ -29,16 +27,16 @@ C_ = SG.spgemm(A, B, info)  # warm
 del C_
 torch.cuda.synchronize()
 nprod = SG.row_nprod(A, B)
-row_nnz = SG.symbolic(A, B, nprod, SG.SpgemmInfo())
-for mode in modes:
+row_nnz = SG.symbolic(A, B, nprod, info)
+for mode in (0,):
     for phase in ("symbolic", "numeric"):
-        lib.spmm_spgemm_stamps(1 | (mode << 1), None)
+        lib.spmm_spgemm_stamps(1, None)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if phase == "symbolic":
-            SG.symbolic(A, B, nprod, SG.SpgemmInfo())
+            SG.symbolic(A, B, nprod, info)
         else:
-            Cm = SG.numeric(A, B, row_nnz, SG.SpgemmInfo())
+            Cm = SG.numeric(A, B, row_nnz, info)
             del Cm
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
