@@ -27,7 +27,6 @@
 namespace {
 
 constexpr int EMPTY = -1;
-constexpr int NOKEY = -2;   // never in a table: a CAS comparing against it only reads
 
 // Diagnostic phase stamps (off unless the host sets g_stamp_on): thread 0 of
 // every workgroup adds the shader-clock cycles of each phase, measured between
@@ -253,26 +252,24 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_sym(
       float dummy[D];
       bool vA[D], vB[D];
       auto consume = [&](const int (&c)[D], const bool (&v)[D]) {
-        // every lane issues its CAS each round; finished / invalid lanes compare
-        // against NOKEY (never stored), i.e. a read: no exec-mask branches
         int h[D];
         bool st[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          h[u] = v[u] ? hash_home(c[u] - clo, mult) : 0;
+          h[u] = hash_home(c[u] - clo, mult);
           st[u] = v[u];
         }
         while (true) {
           int old[D];
 #pragma unroll
-          for (int u = 0; u < D; ++u) old[u] = atomicCAS(&keys[h[u]], st[u] ? EMPTY : NOKEY, c[u]);
+          for (int u = 0; u < D; ++u) old[u] = st[u] ? atomicCAS(&keys[h[u]], EMPTY, c[u]) : c[u];
           bool more = false;
 #pragma unroll
           for (int u = 0; u < D; ++u) {
             mine += (st[u] & (old[u] == EMPTY)) ? 1 : 0;
             const bool again = st[u] & (old[u] != EMPTY) & (old[u] != c[u]);
             h[u] += again ? 1 : 0;
-            h[u] = (h[u] >= TS) ? 0 : h[u];   // wrap: only counts matter here
+            if (again && h[u] >= TS) h[u] = 0;   // wrap: only counts matter here
             st[u] = again;
             more |= again;
           }
@@ -306,15 +303,14 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_sym(
 
 // -------------------------------------------------------------- numeric ----
 constexpr unsigned long long EMPTY64 = 0x00000000FFFFFFFFull;   // key EMPTY, value +0
-constexpr unsigned long long NOKEY64 = 0xFFFFFFFEFFFFFFFEull;   // never in a table: CAS against it is a read
 
 template <int S, int NT, int NP>
 __global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
     const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
     const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols, int lg,
-    const int32_t* __restrict__ row_nnz, const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci,
-    float* __restrict__ Cv, int32_t* __restrict__ flags) {
+    const int32_t* __restrict__ row_cap, int32_t* __restrict__ out_nnz, const int64_t* __restrict__ Crp,
+    int32_t* __restrict__ Cci, float* __restrict__ Cv, int32_t* __restrict__ flags) {
   using Gm = LdsGeom<S, NT>;
   constexpr int TS = Gm::TS, NW = Gm::NW, ACAP = Gm::ACAP, CCAP = Gm::CCAP, NWIN = Gm::NWIN;
   constexpr int QSTEP = 8 / NP;
@@ -373,42 +369,45 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
         bool st[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) {
-          h[u] = v[u] ? hash_home(c[u] - clo, mult) : 0;
+          h[u] = hash_home(c[u] - clo, mult);
           ck[u] = (uint32_t)c[u];
           cv[u] = av[u] * bv[u];
           cur[u] = EMPTY64;   // belief about tab[h]
           st[u] = v[u];
         }
         while (true) {
-          // every lane issues its CAS each round; finished / invalid lanes
-          // compare against NOKEY64 (never stored), i.e. a read
           unsigned long long old[D];
 #pragma unroll
           for (int u = 0; u < D; ++u) {
             const uint32_t k = (uint32_t)cur[u];
             const float nv = (k == ck[u]) ? __uint_as_float((uint32_t)(cur[u] >> 32)) + cv[u] : cv[u];
             const unsigned long long want = ((unsigned long long)__float_as_uint(nv) << 32) | ck[u];
-            old[u] = atomicCAS(&tab[h[u]], st[u] ? cur[u] : NOKEY64, want);
+            old[u] = st[u] ? atomicCAS(&tab[h[u]], cur[u], want) : cur[u];
           }
-          bool more = false, wrap = false;
+          bool more = false;
 #pragma unroll
-          for (int u = 0; u < D; ++u) {   // branch-free state update (selects only)
-            const uint32_t k = (uint32_t)cur[u];
-            const bool landed = st[u] & (old[u] == cur[u]);
-            const bool done = landed & ((k == (uint32_t)EMPTY) | (k == ck[u]));   // placed / merged
-            const bool disp = landed & !done;                                    // displaced a larger key
-            const bool adv = st[u] & !landed & ((uint32_t)old[u] < ck[u]);      // smaller key (EMPTY is largest)
-            const bool step = disp | adv;
-            ck[u] = disp ? k : ck[u];
-            cv[u] = disp ? __uint_as_float((uint32_t)(cur[u] >> 32)) : cv[u];
-            cur[u] = step ? EMPTY64 : old[u];
-            h[u] += step ? 1 : 0;
-            wrap |= h[u] >= TS;
-            h[u] = (h[u] >= TS) ? 0 : h[u];
-            st[u] = st[u] & !done;
-            more |= st[u];
+          for (int u = 0; u < D; ++u) {
+            if (st[u]) {
+              const uint32_t k = (uint32_t)cur[u];
+              if (old[u] == cur[u]) {             // our CAS landed
+                if (k == (uint32_t)EMPTY || k == ck[u]) {
+                  st[u] = false;                  // placed / merged
+                } else {                          // displaced a larger key: carry it on
+                  ck[u] = k;
+                  cv[u] = __uint_as_float((uint32_t)(cur[u] >> 32));
+                  ++h[u];
+                  cur[u] = EMPTY64;
+                }
+              } else if ((uint32_t)old[u] < ck[u]) {   // smaller key (EMPTY is the largest): move on
+                ++h[u];
+                cur[u] = EMPTY64;
+              } else {
+                cur[u] = old[u];                  // retry this slot with what is there
+              }
+              if (st[u] && h[u] >= TS) { h[u] = 0; s_wrapped = 1; }
+              more |= st[u];
+            }
           }
-          if (__any(wrap)) s_wrapped = 1;
           if (!__any(more)) break;
         }
       };
@@ -447,8 +446,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
     }
     __syncthreads();
     const int64_t base = Crp[row] + written;
-    // symbolic fixed the row's size; never store past it whatever happened here
-    const int room = row_nnz[row] - written;
+    // the row's space (exact size from symbolic, or the product count in
+    // one-pass mode): never store past it whatever happened here
+    const int room = row_cap[row] - written;
     const int lim = total < room ? total : room;
     if (tid == 0 && total > room) atomicOr(&flags[row], 4);
     bool bad = false;
@@ -481,6 +481,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
     __syncthreads();   // slice done before the next slice re-initialises the table
   }
   if (__any(unsorted) && lane == 0) atomicOr(&flags[row], 1);
+  if (out_nnz != nullptr && tid == 0) out_nnz[row] = written;
   if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
 }
 
@@ -594,6 +595,29 @@ __global__ __launch_bounds__(GNT) void spgemm_global(
   if (tid == 0 && s_wrapped) unsorted[row] = 1;
 }
 
+// One-pass mode: rows were written at their product-count offsets (src_off);
+// copy each row's n[i] entries to the final CSR (dst_off).  One wave per row.
+__global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict__ src_off,
+                                                      const int64_t* __restrict__ dst_off, int64_t m,
+                                                      const int32_t* __restrict__ sci, const float* __restrict__ sv,
+                                                      int32_t* __restrict__ dci, float* __restrict__ dv) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= m) return;
+  const int64_t s0 = src_off[row], d0 = dst_off[row], n = dst_off[row + 1] - d0;
+  int64_t i = lane;
+  for (; i + 192 < n; i += 256) {   // 4 loads in flight per lane
+    const int c0 = sci[s0 + i], c1 = sci[s0 + i + 64], c2 = sci[s0 + i + 128], c3 = sci[s0 + i + 192];
+    const float v0 = sv[s0 + i], v1 = sv[s0 + i + 64], v2 = sv[s0 + i + 128], v3 = sv[s0 + i + 192];
+    dci[d0 + i] = c0; dci[d0 + i + 64] = c1; dci[d0 + i + 128] = c2; dci[d0 + i + 192] = c3;
+    dv[d0 + i] = v0; dv[d0 + i + 64] = v1; dv[d0 + i + 128] = v2; dv[d0 + i + 192] = v3;
+  }
+  for (; i < n; i += 64) {
+    dci[d0 + i] = sci[s0 + i];
+    dv[d0 + i] = sv[s0 + i];
+  }
+}
+
 // nprod[i] = sum over A(i,:) of nnz(B(j,:)); one wave per row.
 __global__ __launch_bounds__(256) void spgemm_row_nprod(const int64_t* __restrict__ Arp,
                                                         const int32_t* __restrict__ Aci,
@@ -626,10 +650,11 @@ int launch_sym(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, const
 template <int S, int NT, int NP>
 int launch_num(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
                const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows, int ncols, int lg,
-               const int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags, hipStream_t s) {
+               const int32_t* row_cap, int32_t* out_nnz, const int64_t* Crp, int32_t* Cci, float* Cv,
+               int32_t* flags, hipStream_t s) {
   if (nrows <= 0) return 0;
   hipLaunchKernelGGL((spgemm_lds_num<S, NT, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
-                     bsplit, rows, ncols, lg, row_nnz, Crp, Cci, Cv, flags);
+                     bsplit, rows, ncols, lg, row_cap, out_nnz, Crp, Cci, Cv, flags);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -641,6 +666,15 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
   if (m <= 0) return 0;
   hipLaunchKernelGGL(spgemm_row_nprod, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Arp, Aci,
                      Brp, m, nprod);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_spgemm_compact(const int64_t* src_off, const int64_t* dst_off, int64_t m, const int32_t* sci,
+                                    const float* sv, int32_t* dci, float* dv, void* stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(spgemm_compact, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, src_off,
+                     dst_off, m, sci, sv, dci, dv);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -664,10 +698,11 @@ SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, i
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
                                 const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz,
-                                const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags, void* stream) {
+                                int32_t* out_nnz, const int64_t* Crp, int32_t* Cci, float* Cv, int32_t* flags,
+                                void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (lg < 4 || lg > 6) return (int)hipErrorInvalidValue;
-#define SPMM_NARGS Arp, Aci, Av, Brp, Bci, Bv, bsplit, rows, nrows, ncols, lg, row_nnz, Crp, Cci, Cv, flags, s
+#define SPMM_NARGS Arp, Aci, Av, Brp, Bci, Bv, bsplit, rows, nrows, ncols, lg, row_nnz, out_nnz, Crp, Cci, Cv, flags, s
 #define SPMM_SARGS Arp, Aci, Brp, Bci, bsplit, rows, nrows, ncols, lg, row_nnz, flags, s
 #define SPMM_BIN(B, S, NT)                                                                   \
   case B:                                                                                     \

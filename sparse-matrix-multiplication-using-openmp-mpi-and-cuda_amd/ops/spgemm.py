@@ -35,7 +35,8 @@ C_INT = C.c_int
 _native.register_hip("spmm_spgemm_row_nprod", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_row_splits", c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+                     C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_compact", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_global", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp,
                      c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
@@ -133,6 +134,18 @@ def _global_rows(numeric: int, A: CSR, B: CSR, rows: torch.Tensor, counts: torch
         i = j
 
 
+def _onepass_fits(total_products: int, dev: torch.device) -> bool:
+    """One-pass mode needs a product-count-sized staging buffer next to C."""
+    mode = CONFIG.spgemm_onepass
+    if mode == "off":
+        return False
+    if mode == "on":
+        return True
+    free, _ = torch.cuda.mem_get_info(dev)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)   # the caching allocator's spare
+    return 2 * total_products * 8 <= 0.8 * free
+
+
 def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
     if A.n != B.m:
         raise ValueError(f"inner dimensions differ: {A.n} vs {B.m}")
@@ -146,8 +159,49 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
     nprod = row_nprod(A, B)
     info.flops = 2 * int(nprod.sum())
     info.mean_seg = info.flops / 2 / max(A.nnz, 1)
+    if _onepass_fits(info.flops // 2, A.device):
+        return onepass(A, B, nprod, info)
     row_nnz = symbolic(A, B, nprod, info)
     return numeric(A, B, row_nnz, info)
+
+
+def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> CSR:
+    """Numeric without a symbolic phase: rows are binned by their product count
+    and written at product-count offsets (an upper bound of their nnz), then
+    compacted into the final CSR by one copy kernel.  Trades one extra pass
+    over C for the whole symbolic phase."""
+    dev = A.device
+    m = A.m
+    ub = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nprod, 0, out=ub[1:])
+    tot = info.flops // 2
+    Uci = torch.empty(tot, dtype=torch.int32, device=dev)
+    Uv = torch.empty(tot, dtype=torch.float32, device=dev)
+    out_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
+    flags = torch.zeros(m, dtype=torch.int32, device=dev)
+    cap = nprod.to(torch.int32)
+    _run_bins(1, A, B, nprod, cap, ub, Uci, Uv, flags, info.rows_per_bin_num, info.mean_seg, out_nnz=out_nnz)
+    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(out_nnz, 0, out=rowptr[1:])
+    nnz = int(rowptr[-1])
+    info.nnz = nnz
+    Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
+    Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
+    P = _native.ptr
+    _native.check(_native.hip().spmm_spgemm_compact(P(ub), P(rowptr), m, P(Uci), P(Uv), P(Cci), P(Cv),
+                                                     _native.stream_ptr(dev)), "spgemm_compact")
+    del Uci, Uv
+    return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
+
+
+def _finish(C_: CSR, flags: torch.Tensor, info: SpgemmInfo) -> CSR:
+    if bool(((flags & 4) != 0).any()):
+        raise RuntimeError("spgemm numeric: output position out of range (kernel invariant violated)")
+    bad = ((flags & 1) != 0).nonzero().flatten()
+    if bad.numel():
+        info.resorted_rows = int(bad.numel())
+        C_ = sort_rows(C_, bad)
+    return C_
 
 
 def _dummies(dev):
@@ -181,7 +235,10 @@ def _splits(B: CSR) -> torch.Tensor:
 
 
 def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins,
-              mean_seg: float = 0.0):
+              mean_seg: float = 0.0, out_nnz: Optional[torch.Tensor] = None):
+    """Run the LDS bins, then the HBM path for the rest.  Numeric: ``row_nnz`` is
+    each row's capacity in the output (exact nnz, or the product count in
+    one-pass mode where ``out_nnz`` receives the real counts)."""
     dev = A.device
     lib = _native.hip()
     P = _native.ptr
@@ -202,8 +259,9 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
             splits = _splits(B)
         _native.check(lib.spmm_spgemm_lds(b, numeric, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
                                           P(B.val), P(splits) if splits is not None else None, P(rows), cnt, B.n,
-                                          _group_log2(seg / _slices(b, numeric)), P(row_nnz), P(Crp), P(Cci),
-                                          P(Cv), P(flags), stream),
+                                          _group_log2(seg / _slices(b, numeric)), P(row_nnz),
+                                          P(out_nnz) if out_nnz is not None else None, P(Crp), P(Cci), P(Cv),
+                                          P(flags), stream),
                       "spgemm_lds(numeric)" if numeric else "spgemm_lds(symbolic)")
     # rows whose column slice could overflow an LDS table were skipped by the kernel
     spill = ((flags & 2) != 0).nonzero().flatten().to(torch.int32)
@@ -212,6 +270,9 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
         global_rows.append(spill)
     if global_rows:
         rows = torch.cat(global_rows)
+        if out_nnz is not None:   # one-pass: exact counts of these rows first
+            d64, d32, df = _dummies(dev)
+            _global_rows(0, A, B, rows, counts[rows.long()], out_nnz, d64, d32, df, flags, stream)
         _global_rows(numeric, A, B, rows, counts[rows.long()], row_nnz, Crp, Cci, Cv, flags, stream)
 
 
@@ -237,14 +298,7 @@ def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo) -> CSR:
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     flags = torch.zeros(m, dtype=torch.int32, device=dev)
     _run_bins(1, A, B, row_nnz, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num, info.mean_seg)
-    C_ = CSR(m, B.n, rowptr, Cci, Cv)
-    if bool(((flags & 4) != 0).any()):
-        raise RuntimeError("spgemm numeric: output position out of range (kernel invariant violated)")
-    bad = ((flags & 1) != 0).nonzero().flatten()
-    if bad.numel():
-        info.resorted_rows = int(bad.numel())
-        C_ = sort_rows(C_, bad)
-    return C_
+    return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
 
 
 def _spgemm_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:

@@ -27,7 +27,10 @@ class Config:
     spgemm_load: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD", 0.5, float))   # single-pass LDS tables
     # 16K-key (symbolic) / 8K-slot (numeric) tables of long rows: a higher load
     # means fewer column slices, i.e. fewer re-reads of the B rows
-    spgemm_load_sliced: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD_SLICED", 0.7, float))
+    spgemm_load_sliced: float = field(default_factory=lambda: _env("SPMM_SPGEMM_LOAD_SLICED", 0.5, float))
+    # SpGEMM without the symbolic phase (product-count staging buffer + compaction):
+    # "auto" = when twice the product count fits in 80% of free memory
+    spgemm_onepass: str = field(default_factory=lambda: _env("SPMM_SPGEMM_ONEPASS", "auto", str))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

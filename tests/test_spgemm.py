@@ -171,3 +171,23 @@ def test_spgemm_gpu_column_sliced_bins(brow, bcols):
     assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
     assert torch.equal(Cg.col.cpu(), Cc.col)
     assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n,d", [(3000, 2000, 2500, 0.004), (300, 2000, 40000, 0.05)])
+def test_spgemm_gpu_onepass_matches_two_phase(monkeypatch, m, k, n, d):
+    """One-pass (product-count staging + compaction) and symbolic+numeric give
+    the same CSR."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, k, d, seed=21, device=dev)
+    B = gen_csr.uniform_csr(k, n, d, seed=22, device=dev)
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", "on")
+    C1 = SG.spgemm(A, B)
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", "off")
+    C2 = SG.spgemm(A, B)
+    assert torch.equal(C1.rowptr, C2.rowptr)
+    assert torch.equal(C1.col, C2.col)
+    assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    check(C1.to("cpu"), A.to("cpu"), B.to("cpu"))

@@ -29,14 +29,17 @@ torch.cuda.synchronize()
 nprod = SG.row_nprod(A, B)
 row_nnz = SG.symbolic(A, B, nprod, info)
 for mode in (0,):
-    for phase in ("symbolic", "numeric"):
+    for phase in ("symbolic", "numeric", "onepass"):
         lib.spmm_spgemm_stamps(1, None)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if phase == "symbolic":
             SG.symbolic(A, B, nprod, info)
-        else:
+        elif phase == "numeric":
             Cm = SG.numeric(A, B, row_nnz, info)
+            del Cm
+        else:
+            Cm = SG.onepass(A, B, nprod, info)
             del Cm
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
