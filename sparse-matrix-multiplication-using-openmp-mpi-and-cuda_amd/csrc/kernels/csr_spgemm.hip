@@ -485,6 +485,293 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
   if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
 }
 
+// ---------------------------------------------------------------- ESC -----
+// Numeric kernel for long rows: bucketed expand-sort-compress in LDS.
+//
+// The CAS-probing tables above spend most of their time in dependent LDS
+// atomic rounds (every probe step is a round trip, and a wave keeps looping
+// until its slowest lane is placed).  Here every product costs a fixed,
+// round-free sequence:
+//   pass H: bucket histogram (ds_add without return: fire and forget)
+//   scan:   bucket offsets (16-bit counters, two per word)
+//   pass S: one ds_add_rtn for the slot + one 8-byte write of (column, a*b)
+//   sort:   one lane per bucket sorts its few items in registers (sorting
+//           network sized by the wave's largest bucket) and folds duplicate
+//           columns into their first occurrence (the rest become holes)
+//   write:  compaction of the non-hole items in slot order (ballot + mbcnt)
+// Buckets are a monotone function of the column, so slot order is column
+// order.  Each product is read from B twice (histogram + scatter); the second
+// read mostly hits L2 / MALL.
+constexpr int ESC_NB = 4096;   // buckets per slice
+
+template <int PCAP, int NT, int NP>
+__global__ __launch_bounds__(NT, 4) void spgemm_esc(
+    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
+    const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
+    const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols, int lg,
+    const int32_t* __restrict__ row_cap, int32_t* __restrict__ out_nnz, const int64_t* __restrict__ Crp,
+    int32_t* __restrict__ Cci, float* __restrict__ Cv, int32_t* __restrict__ flags) {
+  constexpr int NW = NT / 64, ACAP = NT, CCAP = 2 * NT, NB = ESC_NB;
+  constexpr int BPT = NB / NT;                 // buckets per thread in the scan / sort
+  constexpr int QSTEP = 8 / NP;
+  constexpr int D = 4;
+  constexpr int NWIN = PCAP / 64;
+  constexpr int WPW = (NWIN + NW - 1) / NW;
+  constexpr int LG_MIN = lds_lg_min(PCAP, NT, CCAP);
+  static_assert(PCAP % 64 == 0 && PCAP < 65536, "16-bit bucket counters");
+  static_assert(BPT % 2 == 0 && BPT <= 8, "a thread owns whole counter words, at most 8 buckets");
+  static_assert(NWIN <= CCAP, "window counts reuse the descriptor buffer");
+  __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];   // key (low) | value bits (high)
+  __shared__ __attribute__((aligned(16))) uint32_t hist[NB / 2];            // two 16-bit counters per word
+  __shared__ int64_t abeg[ACAP];
+  __shared__ int clist[CCAP];
+  __shared__ float aval[ACAP];
+  __shared__ int64_t wsum[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = rows[blockIdx.x];
+  const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
+  const int lgE = lg > LG_MIN ? lg : LG_MIN;
+  const int ngrp = NW << (6 - lgE);
+  const int gid = (w << (6 - lgE)) + (lane >> lgE);
+  const int gl = lane & ((1 << lgE) - 1);
+  const int stamp_on = g_stamp_on;
+  unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;
+  int written = 0;
+  int tc_keep = 0;   // chunk count of a single-batch row, reused by the second pass
+
+  for (int sl = 0; sl < NP; ++sl) {
+    const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
+    const int clo = (int)(((int64_t)q0 * ncols) >> 3), chi = (int)(((int64_t)q1 * ncols) >> 3);
+    const uint32_t mult = hash_mult(NB, chi - clo);
+    for (int i = tid; i < NB / 8; i += NT) reinterpret_cast<uint4*>(hist)[i] = make_uint4(0, 0, 0, 0);
+    int64_t slice_products = 0;
+    bool overflow = false;
+    for (int pass = 0; pass < 2 && !overflow; ++pass) {
+      for (int64_t bat = 0; bat < na; bat += ACAP) {
+        const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
+        int TC;
+        if (pass == 0 || na > ACAP) {   // single-batch rows keep their staging for the second pass
+          __syncthreads();
+          int len, nch, pre;
+          int64_t tot;
+          stage_batch<NT, NP, true>(Aci, Av, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, aval, wsum, len, nch,
+                                    pre, TC, tot);
+          if (pass == 0) {
+            slice_products += tot;
+            if (slice_products > PCAP || TC > CCAP) { overflow = true; break; }
+          }
+          tc_keep = TC;
+          if (TC == 0) continue;
+          write_chunks(clist, len, nch, pre, lgE);
+          __syncthreads();
+        } else {
+          TC = tc_keep;
+          if (TC == 0) continue;
+        }
+        SPMM_STAMP(0);
+        int cA[D], cB[D];
+        float bA[D], bB[D], aA[D], aB[D];
+        bool vA[D], vB[D];
+        auto bucket = [&](int c) { return hash_home(c - clo, mult); };
+        auto consume = [&](const int (&c)[D], const float (&bv)[D], const float (&av)[D], const bool (&v)[D]) {
+          if (pass == 0) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+              const int b = bucket(c[u]);
+              if (v[u]) atomicAdd(&hist[b >> 1], (b & 1) ? 0x10000u : 1u);
+            }
+          } else {
+            uint32_t old[D];
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+              const int b = bucket(c[u]);
+              old[u] = v[u] ? atomicAdd(&hist[b >> 1], (b & 1) ? 0x10000u : 1u) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+              const int b = bucket(c[u]);
+              const int pos = (b & 1) ? (int)(old[u] >> 16) : (int)(old[u] & 0xffff);
+              if (v[u])
+                items[pos] = ((unsigned long long)__float_as_uint(av[u] * bv[u]) << 32) | (uint32_t)c[u];
+            }
+          }
+        };
+        const int nit = (TC + ngrp - 1) / ngrp;
+        if (pass == 0) {
+          fetch_chunks<D, false>(0, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cA, bA, aA, vA);
+          for (int i = 0; i < nit; i += 2 * D) {
+            fetch_chunks<D, false>(i + D, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cB, bB, aB, vB);
+            consume(cA, bA, aA, vA);
+            fetch_chunks<D, false>(i + 2 * D, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cA, bA, aA, vA);
+            consume(cB, bB, aB, vB);
+          }
+        } else {
+          fetch_chunks<D, true>(0, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cA, bA, aA, vA);
+          for (int i = 0; i < nit; i += 2 * D) {
+            fetch_chunks<D, true>(i + D, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cB, bB, aB, vB);
+            consume(cA, bA, aA, vA);
+            fetch_chunks<D, true>(i + 2 * D, gid, ngrp, gl, lgE, TC, clist, abeg, aval, Bci, Bv, cA, bA, aA, vA);
+            consume(cB, bB, aB, vB);
+          }
+        }
+        SPMM_STAMP(1);
+      }
+      if (overflow) break;
+      __syncthreads();   // all counts (pass 0) / all items (pass 1) in place
+      if (pass == 0) {
+        // exclusive bucket offsets; thread t owns buckets [BPT*t, BPT*t + BPT)
+        uint32_t cw[BPT / 2];
+        int run = 0;
+#pragma unroll
+        for (int i = 0; i < BPT / 2; ++i) {
+          cw[i] = hist[tid * (BPT / 2) + i];
+          run += (int)(cw[i] & 0xffff) + (int)(cw[i] >> 16);
+        }
+        int total;
+        __syncthreads();
+        int off = block_excl_scan<NT, int>(run, reinterpret_cast<int*>(wsum), &total);
+#pragma unroll
+        for (int i = 0; i < BPT / 2; ++i) {
+          const int lo = off, hi = off + (int)(cw[i] & 0xffff);
+          off = hi + (int)(cw[i] >> 16);
+          hist[tid * (BPT / 2) + i] = (uint32_t)lo | ((uint32_t)hi << 16);
+        }
+        __syncthreads();
+      }
+    }
+    if (overflow) {
+      if (tid == 0) atomicOr(&flags[row], 2);
+      return;   // uniform: every thread saw the same totals
+    }
+    // hist[b] now holds the END offset of bucket b.  Sort + fold each bucket.
+    const int P = (int)slice_products;
+    {
+      int e[BPT];
+#pragma unroll
+      for (int i = 0; i < BPT / 2; ++i) {
+        const uint32_t x = hist[tid * (BPT / 2) + i];
+        e[2 * i] = (int)(x & 0xffff);
+        e[2 * i + 1] = (int)(x >> 16);
+      }
+      int s = tid ? (int)(hist[tid * (BPT / 2) - 1] >> 16) : 0;
+#pragma unroll 1
+      for (int i = 0; i < BPT; ++i) {
+        const int k = e[i] - s;
+        int kmax = k;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) kmax = max(kmax, __shfl_xor(kmax, d));
+        if (kmax >= 2) {
+          uint32_t key[8];
+          float val[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned long long x = items[(j < k) ? s + j : min(s, PCAP - 1)];   // clamped: unconditional reads
+            key[j] = (j < k) ? (uint32_t)x : (uint32_t)EMPTY;
+            val[j] = __uint_as_float((uint32_t)(x >> 32));
+          }
+          auto ce = [&](int a, int b) {
+            const bool sw = key[b] < key[a];
+            const uint32_t ka = sw ? key[b] : key[a], kb = sw ? key[a] : key[b];
+            const float va = sw ? val[b] : val[a], vb = sw ? val[a] : val[b];
+            key[a] = ka; key[b] = kb; val[a] = va; val[b] = vb;
+          };
+          if (kmax == 2) {
+            ce(0, 1);
+          } else if (kmax <= 4) {
+            ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+          } else {
+            ce(0, 1); ce(2, 3); ce(4, 5); ce(6, 7);
+            ce(0, 2); ce(1, 3); ce(4, 6); ce(5, 7);
+            ce(1, 2); ce(5, 6);
+            ce(0, 4); ce(1, 5); ce(2, 6); ce(3, 7);
+            ce(2, 4); ce(3, 5);
+            ce(1, 2); ce(3, 4); ce(5, 6);
+          }
+#pragma unroll
+          for (int j = 7; j >= 1; --j) {   // fold equal columns into the first occurrence
+            const bool dup = key[j] != (uint32_t)EMPTY && key[j] == key[j - 1];
+            val[j - 1] += dup ? val[j] : 0.f;
+            key[j] = dup ? (uint32_t)EMPTY : key[j];
+          }
+          if (k <= 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (j < k) items[s + j] = ((unsigned long long)__float_as_uint(val[j]) << 32) | key[j];
+          } else {
+            // rare oversized bucket: insertion sort + fold in LDS by this lane
+            for (int a = s + 1; a < s + k; ++a) {
+              const unsigned long long x = items[a];
+              int b = a - 1;
+              while (b >= s && (uint32_t)items[b] > (uint32_t)x) { items[b + 1] = items[b]; --b; }
+              items[b + 1] = x;
+            }
+            for (int a = s + k - 1; a > s; --a) {
+              const unsigned long long x = items[a], y = items[a - 1];
+              if ((uint32_t)x == (uint32_t)y && (uint32_t)x != (uint32_t)EMPTY) {
+                const float sum = __uint_as_float((uint32_t)(y >> 32)) + __uint_as_float((uint32_t)(x >> 32));
+                items[a - 1] = ((unsigned long long)__float_as_uint(sum) << 32) | (uint32_t)y;
+                items[a] = EMPTY64;
+              }
+            }
+          }
+        }
+        s = e[i];
+      }
+    }
+    __syncthreads();
+    SPMM_STAMP(2);
+    // compaction of the non-hole items [0, P) in slot order
+    unsigned long long q[WPW];
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int W = w + j * NW;
+      const int slot = W * 64 + lane;
+      q[j] = (W < NWIN && slot < P) ? items[slot] : EMPTY64;
+      const unsigned long long M = __ballot((uint32_t)q[j] != (uint32_t)EMPTY);
+      if (lane == 0 && W < NWIN) clist[W] = __popcll(M);
+    }
+    __syncthreads();
+    int total;
+    {
+      const int cw = (tid < NWIN) ? clist[tid] : 0;
+      const int bw = block_excl_scan<NT, int>(cw, reinterpret_cast<int*>(wsum), &total);
+      __syncthreads();
+      if (tid < NWIN) clist[tid] = bw;
+    }
+    __syncthreads();
+    const int64_t base = Crp[row] + written;
+    const int room = row_cap[row] - written;
+    const int lim = total < room ? total : room;
+    if (tid == 0 && total > room) atomicOr(&flags[row], 4);
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int W = w + j * NW;
+      if (W < NWIN) {
+        const uint32_t key = (uint32_t)q[j];
+        const bool occ = key != (uint32_t)EMPTY;
+        const unsigned long long M = __ballot(occ);
+        if (occ) {
+          const int pos = clist[W] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+          if (pos < lim) {
+            Cci[base + pos] = (int)key;
+            Cv[base + pos] = __uint_as_float((uint32_t)(q[j] >> 32));
+          } else {
+            atomicOr(&flags[row], 4);   // internal error: never write outside the row
+          }
+        }
+      }
+    }
+    SPMM_STAMP(3);
+    written += total;
+    __syncthreads();   // slice done before the next slice reuses the buffers
+  }
+  if (out_nnz != nullptr && tid == 0) out_nnz[row] = written;
+  if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
+}
+
 // Eighth split points of every B row (rows column-sorted): bsplit[j*7 + q-1] =
 // first index of row j whose column >= floor(q * ncols / 8), q = 1..7.
 __global__ __launch_bounds__(256) void spgemm_row_splits(const int64_t* __restrict__ Brp,
@@ -647,6 +934,18 @@ int launch_sym(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, const
   return 0;
 }
 
+template <int PCAP, int NT, int NP>
+int launch_esc(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
+               const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows, int ncols, int lg,
+               const int32_t* row_cap, int32_t* out_nnz, const int64_t* Crp, int32_t* Cci, float* Cv,
+               int32_t* flags, hipStream_t s) {
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL((spgemm_esc<PCAP, NT, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
+                     bsplit, rows, ncols, lg, row_cap, out_nnz, Crp, Cci, Cv, flags);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int S, int NT, int NP>
 int launch_num(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
                const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows, int ncols, int lg,
@@ -694,7 +993,8 @@ SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, i
 // workgroup's work.  Long rows are cut into 2 / 4 / 8 column slices instead of
 // using bigger tables.
 //   symbolic bins 0..6: 128 << b keys, one pass; 7..10: 16384 keys x 1/2/4/8 slices
-//   numeric  bins 0..6: 128 << b key/value slots, one pass; 7..9: 8192 slots x 2/4/8 slices
+//   numeric  bins 0..6: 128 << b key/value slots, one pass (ordered hash);
+//            7..10: bucketed ESC, 7680 products per slice x 1/2/4/8 slices
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
                                 const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz,
@@ -708,9 +1008,10 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
   case B:                                                                                     \
     return numeric ? launch_num<S, NT, 1>(SPMM_NARGS) : launch_sym<S, NT, 1>(SPMM_SARGS);
   if (numeric) {
-    if (bin == 7) return launch_num<8192, 512, 2>(SPMM_NARGS);
-    if (bin == 8) return launch_num<8192, 512, 4>(SPMM_NARGS);
-    if (bin == 9) return launch_num<8192, 512, 8>(SPMM_NARGS);
+    if (bin == 7) return launch_esc<7680, 512, 1>(SPMM_NARGS);
+    if (bin == 8) return launch_esc<7680, 512, 2>(SPMM_NARGS);
+    if (bin == 9) return launch_esc<7680, 512, 4>(SPMM_NARGS);
+    if (bin == 10) return launch_esc<7680, 512, 8>(SPMM_NARGS);
   } else {
     if (bin == 7) return launch_sym<16384, 512, 1>(SPMM_SARGS);
     if (bin == 8) return launch_sym<16384, 512, 2>(SPMM_SARGS);

@@ -43,16 +43,22 @@ _native.register_hip("spmm_spgemm_global", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, 
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
-# 1 / 2 / 4 / 8 column slices.  Numeric: b = 0..6 single pass (128 << b key/value
-# slots), 7..9 = 8192 slots over 2 / 4 / 8 slices.  Then the HBM path.
+# 1 / 2 / 4 / 8 column slices.  Numeric: b = 0..6 single pass (128 << b ordered
+# key/value slots) for rows of <= ESC_MIN products, 7..10 = bucketed ESC with
+# ESC_PCAP products per slice over 1 / 2 / 4 / 8 slices.  Then the HBM path.
+# Numeric rows are binned by their PRODUCT count (the ESC capacity is in
+# products, and it bounds the distinct count for the hash bins).
 SYM_SINGLE_TOP = 6
 NUM_SINGLE_TOP = 6
 SYM_SLICED = (7, 8, 9, 10)
-NUM_SLICED = (7, 8, 9)
+NUM_SLICED = (8, 9, 10)
 SYM_GLOBAL = 11
-NUM_GLOBAL = 10
+NUM_GLOBAL = 11
+ESC_PCAP = 7680
 LOAD = CONFIG.spgemm_load              # max load factor of a single-pass LDS table
 LOAD_SLICED = CONFIG.spgemm_load_sliced   # ... of the big (column-sliced) tables
+ESC_MIN = CONFIG.spgemm_esc_min        # numeric rows with more products use the ESC kernel
+ESC_LOAD = 0.9                         # per-slice margin of the multi-slice ESC bins
 GLOBAL_WS_BYTES = int(CONFIG.spgemm_global_ws_gb * (1 << 30))   # HBM budget per batch of global-table rows
 
 
@@ -70,10 +76,11 @@ def _bins(counts: torch.Tensor, numeric: int) -> torch.Tensor:
     """Bin per row: the smallest single-pass table with counts <= LOAD * S, then
     the sliced passes (slice capacity LOAD * S_top * slices), then the HBM path;
     -1 for empty rows."""
-    caps = [int(LOAD * (128 << b)) for b in range(7)]
     if numeric:
-        caps += [int(LOAD_SLICED * 8192) * k for k in (2, 4, 8)]
+        caps = [min(int(LOAD * (128 << b)), ESC_MIN) for b in range(7)]
+        caps += [ESC_PCAP] + [int(ESC_LOAD * ESC_PCAP) * k for k in (2, 4, 8)]
     else:
+        caps = [int(LOAD * (128 << b)) for b in range(7)]
         caps += [int(LOAD_SLICED * 16384) * k for k in (1, 2, 4, 8)]
     b = torch.bucketize(counts, torch.tensor(caps, device=counts.device, dtype=counts.dtype))
     return torch.where(counts == 0, torch.full_like(b, -1), b)
@@ -162,7 +169,7 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
     if _onepass_fits(info.flops // 2, A.device):
         return onepass(A, B, nprod, info)
     row_nnz = symbolic(A, B, nprod, info)
-    return numeric(A, B, row_nnz, info)
+    return numeric(A, B, row_nnz, info, nprod)
 
 
 def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> CSR:
@@ -212,7 +219,7 @@ def _dummies(dev):
 def _slices(b: int, numeric: int) -> int:
     """Column slices of LDS bin b."""
     if numeric:
-        return {7: 2, 8: 4, 9: 8}.get(b, 1)
+        return {8: 2, 9: 4, 10: 8}.get(b, 1)
     return {8: 2, 9: 4, 10: 8}.get(b, 1)
 
 
@@ -286,8 +293,11 @@ def symbolic(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> torch.Ten
     return row_nnz
 
 
-def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo) -> CSR:
+def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo,
+            nprod: Optional[torch.Tensor] = None) -> CSR:
     """Values of C (column-sorted rows) into the layout fixed by ``row_nnz``."""
+    if nprod is None:
+        nprod = row_nprod(A, B)
     dev = A.device
     m = A.m
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
@@ -297,7 +307,7 @@ def numeric(A: CSR, B: CSR, row_nnz: torch.Tensor, info: SpgemmInfo) -> CSR:
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     flags = torch.zeros(m, dtype=torch.int32, device=dev)
-    _run_bins(1, A, B, row_nnz, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num, info.mean_seg)
+    _run_bins(1, A, B, nprod, row_nnz, rowptr, Cci, Cv, flags, info.rows_per_bin_num, info.mean_seg)
     return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
 
 

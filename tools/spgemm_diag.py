@@ -36,7 +36,7 @@ for mode in (0,):
         if phase == "symbolic":
             SG.symbolic(A, B, nprod, info)
         elif phase == "numeric":
-            Cm = SG.numeric(A, B, row_nnz, info)
+            Cm = SG.numeric(A, B, row_nnz, info, nprod)
             del Cm
         else:
             Cm = SG.onepass(A, B, nprod, info)
