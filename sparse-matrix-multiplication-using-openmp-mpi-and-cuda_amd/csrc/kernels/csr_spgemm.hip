@@ -125,6 +125,19 @@ struct LdsGeom {
   static_assert(NT <= 512, "entry index is 9 bits in a chunk descriptor");
 };
 
+// Chunk count of this thread's entry and one block scan giving the chunk
+// offsets (low word) and the product total (high word).
+template <int NT>
+__device__ __forceinline__ void scan_chunks(int len, int lgE, int64_t* wsum, int& nch, int& pre, int& TC,
+                                            int64_t& tot) {
+  nch = (len + (1 << lgE) - 1) >> lgE;
+  int64_t both;
+  const int64_t pk = block_excl_scan<NT, int64_t>(((int64_t)len << 32) | nch, wsum, &both);
+  pre = (int)(pk & 0xffffffff);
+  TC = (int)(both & 0xffffffff);
+  tot = (int64_t)((uint64_t)both >> 32);
+}
+
 // Stage one batch of A entries of a row slice: B-row segment starts (abeg) and
 // A values (aval) in LDS, one block scan for the chunk offsets and the product
 // total.  Ends synchronised.  The caller checks the capacities, then calls
@@ -146,14 +159,9 @@ __device__ __forceinline__ void stage_batch(const int32_t* __restrict__ Aci, con
     abeg[tid] = b0;
     if constexpr (VALUES) aval[tid] = Av[abase + tid];
   }
-  nch = (len + (1 << lgE) - 1) >> lgE;
-  // one scan: chunk offsets (low word) and the product total (high word)
-  int64_t both;
-  const int64_t pk = block_excl_scan<NT, int64_t>(((int64_t)len << 32) | nch, wsum, &both);
-  pre = (int)(pk & 0xffffffff);
-  TC = (int)(both & 0xffffffff);
-  tot = (int64_t)((uint64_t)both >> 32);
+  scan_chunks<NT>(len, lgE, wsum, nch, pre, TC, tot);
 }
+
 
 __device__ __forceinline__ void write_chunks(int* clist, int len, int nch, int pre, int lgE) {
   const int G = 1 << lgE;
@@ -504,6 +512,17 @@ __global__ __launch_bounds__(NT, 4) void spgemm_lds_num(
 // read mostly hits L2 / MALL.
 constexpr int ESC_NB = 4096;   // buckets per slice
 
+// max over the 64 lanes without LDS: DPP within each 16-lane row, then 4 readlanes
+__device__ __forceinline__ int wave_max(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));   // row_half_mirror
+  x = max(x, __builtin_amdgcn_update_dpp(x, x, 0x140, 0xF, 0xF, false));   // row_mirror
+  const int a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
+  const int c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
+  return max(max(a, b), max(c, d));
+}
+
 template <int PCAP, int NT, int NP>
 __global__ __launch_bounds__(NT, 4) void spgemm_esc(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
@@ -540,6 +559,20 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
   unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;
   int written = 0;
   int tc_keep = 0;   // chunk count of a single-batch row, reused by the second pass
+  // Single-batch rows (na <= ACAP, the common case) keep their entry in
+  // registers across slices: the column j, a(i,j), the current segment start
+  // and the NEXT slice boundary, loaded one slice ahead so that only slice 0
+  // waits for global memory during staging.
+  const bool single = na <= ACAP;
+  int ej = 0;
+  float eav = 0.f;
+  int64_t eb0 = 0, eb1 = 0;
+  if (single && tid < na) {
+    ej = Aci[a0 + tid];
+    eav = Av[a0 + tid];
+    eb0 = Brp[ej];
+    eb1 = (NP == 1) ? Brp[ej + 1] : bsplit[(int64_t)ej * 7 + QSTEP - 1];
+  }
 
   for (int sl = 0; sl < NP; ++sl) {
     const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
@@ -552,12 +585,25 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
       for (int64_t bat = 0; bat < na; bat += ACAP) {
         const int nb = (int)((na - bat) < ACAP ? (na - bat) : ACAP);
         int TC;
-        if (pass == 0 || na > ACAP) {   // single-batch rows keep their staging for the second pass
+        if (pass == 0 || !single) {   // single-batch rows keep their staging for the second pass
           __syncthreads();
           int len, nch, pre;
           int64_t tot;
-          stage_batch<NT, NP, true>(Aci, Av, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, aval, wsum, len, nch,
-                                    pre, TC, tot);
+          if (single) {
+            len = 0;
+            if (tid < nb) {
+              len = (int)(eb1 - eb0);
+              abeg[tid] = eb0;
+              aval[tid] = eav;
+              eb0 = eb1;   // next slice starts where this one ends
+              if (sl + 1 < NP)   // prefetch the next slice's end
+                eb1 = (sl + 2 == NP) ? Brp[ej + 1] : bsplit[(int64_t)ej * 7 + (sl + 2) * QSTEP - 1];
+            }
+            scan_chunks<NT>(len, lgE, wsum, nch, pre, TC, tot);
+          } else {
+            stage_batch<NT, NP, true>(Aci, Av, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, aval, wsum, len, nch,
+                                      pre, TC, tot);
+          }
           if (pass == 0) {
             slice_products += tot;
             if (slice_products > PCAP || TC > CCAP) { overflow = true; break; }
@@ -655,69 +701,86 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
         e[2 * i] = (int)(x & 0xffff);
         e[2 * i + 1] = (int)(x >> 16);
       }
-      int s = tid ? (int)(hist[tid * (BPT / 2) - 1] >> 16) : 0;
-#pragma unroll 1
-      for (int i = 0; i < BPT; ++i) {
-        const int k = e[i] - s;
-        int kmax = k;
+      const int s0 = tid ? (int)(hist[tid * (BPT / 2) - 1] >> 16) : 0;
+      auto sb = [&](int i) { return i ? e[i - 1] : s0; };
+      auto kb = [&](int i) { return e[i] - sb(i); };
+      int km[BPT];   // wave-uniform (SGPRs)
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) kmax = max(kmax, __shfl_xor(kmax, d));
-        if (kmax >= 2) {
-          uint32_t key[8];
-          float val[8];
+      for (int i = 0; i < BPT; ++i) km[i] = wave_max(kb(i));   // DPP + readlane: no LDS round trips
+      // software pipeline: bucket i+1's items are read while bucket i sorts
+      auto load = [&](int i, uint32_t (&key)[8], float (&val)[8]) {
+        const int s = sb(i), k = kb(i);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const unsigned long long x = items[(j < k) ? s + j : min(s, PCAP - 1)];   // clamped: unconditional reads
+        for (int j = 0; j < 8; ++j) {
+          key[j] = (uint32_t)EMPTY;
+          val[j] = 0.f;
+          if (j < km[i] && km[i] >= 2) {   // wave-uniform
+            const unsigned long long x = items[(j < k) ? s + j : min(s, PCAP - 1)];   // clamped, unpredicated
             key[j] = (j < k) ? (uint32_t)x : (uint32_t)EMPTY;
             val[j] = __uint_as_float((uint32_t)(x >> 32));
           }
-          auto ce = [&](int a, int b) {
-            const bool sw = key[b] < key[a];
-            const uint32_t ka = sw ? key[b] : key[a], kb = sw ? key[a] : key[b];
-            const float va = sw ? val[b] : val[a], vb = sw ? val[a] : val[b];
-            key[a] = ka; key[b] = kb; val[a] = va; val[b] = vb;
-          };
-          if (kmax == 2) {
-            ce(0, 1);
-          } else if (kmax <= 4) {
-            ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
-          } else {
-            ce(0, 1); ce(2, 3); ce(4, 5); ce(6, 7);
-            ce(0, 2); ce(1, 3); ce(4, 6); ce(5, 7);
-            ce(1, 2); ce(5, 6);
-            ce(0, 4); ce(1, 5); ce(2, 6); ce(3, 7);
-            ce(2, 4); ce(3, 5);
-            ce(1, 2); ce(3, 4); ce(5, 6);
-          }
+        }
+      };
+      auto process = [&](int i, uint32_t (&key)[8], float (&val)[8]) {
+        const int s = sb(i), k = kb(i), kmax = km[i];
+        if (kmax < 2) return;
+        auto ce = [&](int a, int b) {
+          const bool sw = key[b] < key[a];
+          const uint32_t ka = sw ? key[b] : key[a], kb2 = sw ? key[a] : key[b];
+          const float va = sw ? val[b] : val[a], vb = sw ? val[a] : val[b];
+          key[a] = ka; key[b] = kb2; val[a] = va; val[b] = vb;
+        };
+        // small sorting networks sized by the wave's largest bucket
+        if (kmax == 2) {
+          ce(0, 1);
+        } else if (kmax <= 4) {
+          ce(0, 1); ce(2, 3); ce(0, 2); ce(1, 3); ce(1, 2);
+        } else if (kmax <= 6) {
+          ce(0, 5); ce(1, 3); ce(2, 4); ce(1, 2); ce(3, 4); ce(0, 3); ce(2, 5); ce(0, 1); ce(2, 3);
+          ce(4, 5); ce(1, 2); ce(3, 4);
+        } else {
+          ce(0, 1); ce(2, 3); ce(4, 5); ce(6, 7);
+          ce(0, 2); ce(1, 3); ce(4, 6); ce(5, 7);
+          ce(1, 2); ce(5, 6);
+          ce(0, 4); ce(1, 5); ce(2, 6); ce(3, 7);
+          ce(2, 4); ce(3, 5);
+          ce(1, 2); ce(3, 4); ce(5, 6);
+        }
 #pragma unroll
-          for (int j = 7; j >= 1; --j) {   // fold equal columns into the first occurrence
-            const bool dup = key[j] != (uint32_t)EMPTY && key[j] == key[j - 1];
-            val[j - 1] += dup ? val[j] : 0.f;
-            key[j] = dup ? (uint32_t)EMPTY : key[j];
-          }
-          if (k <= 8) {
+        for (int j = 7; j >= 1; --j) {   // fold equal columns into the first occurrence
+          if (j >= kmax) continue;   // wave-uniform
+          const bool dup = key[j] != (uint32_t)EMPTY && key[j] == key[j - 1];
+          val[j - 1] += dup ? val[j] : 0.f;
+          key[j] = dup ? (uint32_t)EMPTY : key[j];
+        }
+        if (k <= 8) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (j < k) items[s + j] = ((unsigned long long)__float_as_uint(val[j]) << 32) | key[j];
-          } else {
-            // rare oversized bucket: insertion sort + fold in LDS by this lane
-            for (int a = s + 1; a < s + k; ++a) {
-              const unsigned long long x = items[a];
-              int b = a - 1;
-              while (b >= s && (uint32_t)items[b] > (uint32_t)x) { items[b + 1] = items[b]; --b; }
-              items[b + 1] = x;
-            }
-            for (int a = s + k - 1; a > s; --a) {
-              const unsigned long long x = items[a], y = items[a - 1];
-              if ((uint32_t)x == (uint32_t)y && (uint32_t)x != (uint32_t)EMPTY) {
-                const float sum = __uint_as_float((uint32_t)(y >> 32)) + __uint_as_float((uint32_t)(x >> 32));
-                items[a - 1] = ((unsigned long long)__float_as_uint(sum) << 32) | (uint32_t)y;
-                items[a] = EMPTY64;
-              }
+          for (int j = 0; j < 8; ++j)
+            if (j < k) items[s + j] = ((unsigned long long)__float_as_uint(val[j]) << 32) | key[j];
+        } else {
+          // rare oversized bucket: insertion sort + fold in LDS by this lane
+          for (int a = s + 1; a < s + k; ++a) {
+            const unsigned long long x = items[a];
+            int b = a - 1;
+            while (b >= s && (uint32_t)items[b] > (uint32_t)x) { items[b + 1] = items[b]; --b; }
+            items[b + 1] = x;
+          }
+          for (int a = s + k - 1; a > s; --a) {
+            const unsigned long long x = items[a], y = items[a - 1];
+            if ((uint32_t)x == (uint32_t)y && (uint32_t)x != (uint32_t)EMPTY) {
+              const float sum = __uint_as_float((uint32_t)(y >> 32)) + __uint_as_float((uint32_t)(x >> 32));
+              items[a - 1] = ((unsigned long long)__float_as_uint(sum) << 32) | (uint32_t)y;
+              items[a] = EMPTY64;
             }
           }
         }
-        s = e[i];
+      };
+      uint32_t kX[8];   // (a register double buffer across buckets spills: measured slower)
+      float vX[8];
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) {
+        load(i, kX, vX);
+        process(i, kX, vX);
       }
     }
     __syncthreads();
