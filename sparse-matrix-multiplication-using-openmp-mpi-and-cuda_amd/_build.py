@@ -4,6 +4,10 @@
   compiled for gfx950 only (``hipcc --offload-arch=gfx950``), C ABI launchers.
 * ``lib/libspmm_host.so`` — the C++/OpenMP host runtime in ``csrc/host``:
   reference-format and Matrix-Market I/O, the CPU backend.
+* ``bin/a4`` — the native drop-in executable (``csrc/runtime``: HIP engine,
+  RCCL / MPI communicators, chain driver), linked against both libraries,
+  RCCL and MPICH (``/opt/conda``, override with ``SPMM_MPI_HOME``).  Skipped
+  with a message when no ``mpi.h`` is found.
 
 Replaces the reference's Makefile (nvcc ``-arch=sm_35`` + mpicxx, Makefile:1-26).
 Run ``python -m spmm_amd._build`` or call :func:`build`.  Rebuilds only when a
@@ -22,6 +26,8 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libspmm_hip.so")
 HOST_LIB = os.path.join(LIB_DIR, "libspmm_host.so")
+BIN_DIR = os.path.join(PKG_DIR, "bin")
+A4_BIN = os.path.join(BIN_DIR, "a4")
 ARCH = "gfx950"
 
 
@@ -77,9 +83,41 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     return HOST_LIB
 
 
+def mpi_home() -> str:
+    return os.environ.get("SPMM_MPI_HOME", "/opt/conda")
+
+
+def build_a4(force: bool = False, verbose: bool = False):
+    """Native ``a4`` executable; returns its path or None without MPI headers."""
+    rt = os.path.join(CSRC, "runtime")
+    srcs = sorted(glob.glob(os.path.join(rt, "*.cpp"))) + sorted(glob.glob(os.path.join(rt, "*.hip")))
+    deps = srcs + glob.glob(os.path.join(rt, "*.hpp")) + [HIP_LIB, HOST_LIB]
+    mpi = mpi_home()
+    if not os.path.exists(os.path.join(mpi, "include", "mpi.h")):
+        if verbose:
+            print(f"a4: no mpi.h under {mpi}; native executable not built")
+        return None
+    if force or _stale(A4_BIN, deps):
+        os.makedirs(BIN_DIR, exist_ok=True)
+        tmp = A4_BIN + ".tmp"
+        # system libstdc++ before conda's (older) in the run path
+        rpath = ":".join(["$ORIGIN/../lib", "/usr/lib/x86_64-linux-gnu", "/opt/rocm/lib", os.path.join(mpi, "lib")])
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I", rt, "-I", os.path.join(mpi, "include"),
+               "-o", tmp] + srcs + [
+               "-L", LIB_DIR, "-lspmm_host", "-lspmm_hip", "-L/opt/rocm/lib", "-lrccl",
+               # libmpi by path: a -L into conda would also pick conda's old libstdc++ at link time
+               "-Wl," + os.path.join(mpi, "lib", "libmpi.so"), "-lpthread", f"-Wl,-rpath,{rpath}"]
+        if verbose:
+            print(" ".join(cmd))
+        _run(cmd)
+        os.replace(tmp, A4_BIN)
+    return A4_BIN
+
+
 def build(force: bool = False, verbose: bool = False) -> None:
     build_host(force, verbose)
     build_hip(force, verbose)
+    build_a4(force, verbose)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,50 @@
+// Communicators of the native `a4`.
+//
+// The reference ships partial products to rank 0 with blocking MPI_Send /
+// MPI_Recv in three messages (header tag 0, keys tag 1 in 256 Ki chunks,
+// values tag 2 in 32 MiB chunks; sparse_matrix_mult.cu:466-553).  Here a
+// partial moves in the same header-then-payload protocol, but:
+//   RcclComm   device-to-device over RCCL (xGMI P2P), communicator bootstrapped
+//              by broadcasting the ncclUniqueId over MPI; bounded waits that
+//              poll ncclCommGetAsyncError and abort on timeout
+//   MpiComm    host-staged MPI (CPU engine, or GPUs shared by several ranks);
+//              counts split below 2^31 elements per message (the reference's
+//              int counts overflow past that, :487,504)
+// Either can inject a failure for tests: SPMM_FAULT_INJECT=send:<rank> makes
+// that rank fail its first send (fail-fast path, §5.3).
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "rt.hpp"
+
+namespace a4 {
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  virtual std::string name() const = 0;
+  // host matrices (CPU engine)
+  virtual void send_host(const Mat& M, int dst) = 0;
+  virtual Mat recv_host(int src) = 0;
+  // device matrices (GPU engine), ordered on `s`
+  virtual void send_dev(const DevMat& M, int dst, hipStream_t s) = 0;
+  virtual DevMat recv_dev(int src, hipStream_t s) = 0;
+  virtual void barrier() = 0;
+  virtual double allreduce_max(double x) = 0;
+  virtual void abort(int code) = 0;
+  size_t bytes_sent = 0, bytes_recv = 0;
+
+ protected:
+  int rank_ = 0, world_ = 1;
+  void maybe_inject_fault(const char* what) const;
+};
+
+// MPI must be initialised by the caller.
+std::unique_ptr<Comm> make_mpi_comm();
+std::unique_ptr<Comm> make_rccl_comm(double timeout_s);
+
+}  // namespace a4

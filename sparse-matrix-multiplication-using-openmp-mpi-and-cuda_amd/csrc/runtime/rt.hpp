@@ -1,0 +1,136 @@
+// Native runtime core for the `a4` executable (SURVEY.md §7.1 csrc/core +
+// csrc/format): error checking, RAII device buffers, the block-sparse matrix
+// types and the engine / communicator interfaces.
+//
+// Reference parity: the reference is one C++/CUDA/MPI translation unit
+// (sparse_matrix_mult.cu) whose `one_matrix` is a std::map of k x k uint64
+// tiles (:26-32).  Here a matrix is sorted block-COO with contiguous
+// [nb][k][k] values, on the host (Mat, std::vector) or in HBM (DevMat).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace a4 {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define A4_HIP(call)                                                                                 \
+  do {                                                                                               \
+    hipError_t e_ = (call);                                                                          \
+    if (e_ != hipSuccess)                                                                            \
+      throw ::a4::Error(std::string("HIP error ") + hipGetErrorString(e_) + " at " + __FILE__ + ":" + \
+                        std::to_string(__LINE__) + ": " #call);                                      \
+  } while (0)
+
+#define A4_CHECK(cond, msg)                          \
+  do {                                               \
+    if (!(cond)) throw ::a4::Error(std::string(msg)); \
+  } while (0)
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Stream-ordered device allocation (hipMallocAsync), freed on the stream that
+// last used it.  Move-only.
+template <typename T>
+class DevBuf {
+ public:
+  DevBuf() = default;
+  DevBuf(size_t n, hipStream_t s) : n_(n), s_(s) {
+    if (n_) A4_HIP(hipMallocAsync(reinterpret_cast<void**>(&p_), n_ * sizeof(T), s_));
+  }
+  DevBuf(DevBuf&& o) noexcept : p_(o.p_), n_(o.n_), s_(o.s_) { o.p_ = nullptr; o.n_ = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { reset(); p_ = o.p_; n_ = o.n_; s_ = o.s_; o.p_ = nullptr; o.n_ = 0; }
+    return *this;
+  }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p_) (void)hipFreeAsync(p_, s_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  // later frees are ordered after the work of `s` (the last user)
+  void retarget(hipStream_t s) { s_ = s; }
+  T* get() const { return p_; }
+  size_t size() const { return n_; }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0;
+  hipStream_t s_ = nullptr;
+};
+
+// Host matrix in the reference's logical layout: tiles sorted by (r, c),
+// keys [nb][2], values [nb][k][k].
+struct Mat {
+  int64_t rows = 0, cols = 0;
+  int k = 0;
+  std::vector<int32_t> keys;
+  std::vector<uint64_t> vals;
+  int64_t nb() const { return (int64_t)keys.size() / 2; }
+  size_t bytes() const { return keys.size() * 4 + vals.size() * 8; }
+};
+
+// Device matrix (HBM resident).
+struct DevMat {
+  int64_t rows = 0, cols = 0;
+  int k = 0;
+  int64_t nb = 0;
+  DevBuf<int32_t> keys;    // [nb][2]
+  DevBuf<uint64_t> vals;   // [nb][k][k]
+  size_t bytes() const { return (size_t)nb * (8 + (size_t)k * k * 8); }
+};
+
+// Order-preserving uint64 code of a signed (r, c) pair.
+__host__ __device__ inline uint64_t encode_key(int32_t r, int32_t c) {
+  return ((uint64_t)((uint32_t)r ^ 0x80000000u) << 32) | (uint64_t)((uint32_t)c ^ 0x80000000u);
+}
+__host__ __device__ inline int32_t key_r(uint64_t code) { return (int32_t)((uint32_t)(code >> 32) ^ 0x80000000u); }
+__host__ __device__ inline int32_t key_c(uint64_t code) { return (int32_t)((uint32_t)code ^ 0x80000000u); }
+
+// ---- engines ---------------------------------------------------------------
+// GPU engine (bsr_engine.hip): C = A (x) B with the reference arithmetic,
+// zero tiles pruned.  All work is ordered on `s`; returns after the output
+// sizes are known (one host sync per phase).
+DevMat dev_multiply(const DevMat& A, const DevMat& B, hipStream_t s, int64_t* tile_pairs);
+DevMat dev_upload(const Mat& M, hipStream_t s);
+Mat dev_download(const DevMat& M, hipStream_t s);
+DevMat dev_prune(DevMat M, hipStream_t s);
+
+// CPU engine (cpu_engine.cpp, OpenMP).
+Mat cpu_multiply(const Mat& A, const Mat& B, int nthreads, int64_t* tile_pairs);
+Mat cpu_prune(Mat M);
+void canonicalize(Mat& M);   // sort by (r, c), last duplicate wins (std::map insert semantics)
+
+}  // namespace a4
+
+// Kernels exported by libspmm_hip.so / libspmm_host.so (csrc/kernels, csrc/host).
+extern "C" {
+int spmm_bsr_u64_numeric(const void* Avals, const void* Bvals, const int32_t* pa, const int32_t* pb,
+                         const int64_t* tile_ptr, void* Cvals, int32_t* nz_flag, int k, int64_t ntiles,
+                         void* stream);
+int spmm_bsr_u64_nonzero(const void* vals, int k, int64_t ntiles, int32_t* nz_flag, void* stream);
+int spmm_cpu_bsr_u64_numeric(const uint64_t* A, const uint64_t* B, const int32_t* pa, const int32_t* pb,
+                             const int64_t* tile_ptr, uint64_t* C, int32_t* nz_flag, int k, int64_t ntiles,
+                             int nthreads);
+void* spmm_ref_open(const char* path, int k, int64_t* rows, int64_t* cols, int64_t* blocks, char* err, int errlen);
+int spmm_ref_fill(void* handle, int32_t* keys, uint64_t* vals, int nthreads, char* err, int errlen);
+void spmm_ref_close(void* handle);
+int spmm_ref_write(const char* path, int64_t R, int64_t C, int64_t nb, const int32_t* keys, const uint64_t* vals,
+                   int k, int nthreads);
+}

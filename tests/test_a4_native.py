@@ -1,0 +1,113 @@
+"""Native ``a4`` executable (csrc/runtime): mpiexec-launched, byte-identical
+``./matrix`` vs the golden model at the same P, reference stdout lines,
+checkpoint/resume, fail-fast fault injection.  CPU engine + MPI here; the GPU
+engine (and RCCL at P=1) on the GPU box."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+import spmm_amd  # noqa: F401
+from spmm_amd import _build
+from spmm_amd.utils import gen, golden, refio
+
+MPIEXEC = os.path.join(_build.mpi_home(), "bin", "mpiexec")
+
+
+@pytest.fixture(scope="module")
+def a4_bin():
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("no MPICH")
+    path = _build.build_a4()
+    if path is None:
+        pytest.skip("native a4 not built (no mpi.h)")
+    return path
+
+
+def _run(a4_bin, p, folder, *args, check=True, timeout=240):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("SPMM_FAULT_INJECT", None)
+    cmd = [MPIEXEC, "-n", str(p), a4_bin, folder] + list(args)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    if check and r.returncode != 0:
+        raise AssertionError(f"a4 failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _chain(tmp_path, n, blocks=4, k=2, seed=0):
+    mats = gen.random_chain(n, blocks, k, 0.55, "adversarial", seed=seed)
+    folder = str(tmp_path / "in")
+    refio.write_folder(folder, mats, k)
+    return mats, folder
+
+
+@pytest.mark.parametrize("n,p", [(7, 2), (6, 3), (9, 4), (4, 4), (2, 3), (1, 1), (5, 1)])
+def test_a4_cpu_matches_golden(tmp_path, a4_bin, n, p):
+    mats, folder = _chain(tmp_path, n, seed=10 * n + p)
+    out = str(tmp_path / "matrix")
+    r = _run(a4_bin, p, folder, "--device", "cpu", "--out", out, "--threads", "2")
+    want = golden.chain([golden.from_bsr(m) for m in mats], p=p)
+    with open(out) as f:
+        assert f.read() == golden.to_text(want)
+    lines = r.stdout.splitlines()
+    assert sum(1 for l in lines if l.startswith("multiplying ")) == n - 1
+    assert sum(1 for l in lines if l.startswith("time taken ") and l.endswith(" seconds")) == p
+
+
+def test_a4_missing_size_file(tmp_path, a4_bin):
+    r = _run(a4_bin, 1, str(tmp_path / "nowhere"), "--device", "cpu", check=False)
+    assert r.returncode != 0
+    assert "Cannot open size file!" in r.stderr
+
+
+def test_a4_checkpoint_resume_and_metrics(tmp_path, a4_bin):
+    mats, folder = _chain(tmp_path, 8, seed=3)
+    ck = str(tmp_path / "ck")
+    out1, out2 = str(tmp_path / "m1"), str(tmp_path / "m2")
+    _run(a4_bin, 2, folder, "--device", "cpu", "--out", out1, "--save-partials", ck, "--quiet")
+    assert sorted(os.listdir(ck)) == ["partial_0", "partial_1"]
+    met = str(tmp_path / "met.json")
+    r = _run(a4_bin, 2, folder, "--device", "cpu", "--out", out2, "--load-partials", ck, "--metrics-json", met)
+    assert open(out1).read() == open(out2).read()
+    # resumed run skips the local trees: only the cross-rank product is printed
+    assert sum(1 for l in r.stdout.splitlines() if l.startswith("multiplying ")) == 1
+    m = json.load(open(met))
+    assert m["engine"] == "native" and m["ranks"] == 2 and m["products"] == 1
+
+
+def test_a4_fault_injection_fails_fast(tmp_path, a4_bin):
+    _, folder = _chain(tmp_path, 6, seed=4)
+    env = dict(os.environ, OMP_NUM_THREADS="2", SPMM_FAULT_INJECT="send:1")
+    r = subprocess.run([MPIEXEC, "-n", "2", a4_bin, folder, "--device", "cpu", "--out", str(tmp_path / "m")],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert "injected fault" in r.stderr
+
+
+def test_a4_dump(tmp_path, a4_bin):
+    _, folder = _chain(tmp_path, 2, seed=5)
+    r = _run(a4_bin, 1, folder, "--device", "cpu", "--out", str(tmp_path / "m"), "--dump")
+    assert r.stdout.count("[dump] ") == 3   # two inputs + the result
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,p,comm", [(9, 1, "auto"), (7, 2, "mpi"), (8, 4, "mpi")])
+def test_a4_gpu_matches_golden(tmp_path, a4_bin, n, p, comm):
+    mats, folder = _chain(tmp_path, n, blocks=6, k=4, seed=n + p)
+    out = str(tmp_path / "matrix")
+    _run(a4_bin, p, folder, "--device", "hip", "--comm", comm, "--out", out, "--streams", "3")
+    want = golden.chain([golden.from_bsr(m) for m in mats], p=p)
+    with open(out) as f:
+        assert f.read() == golden.to_text(want)
+
+
+@pytest.mark.gpu
+def test_a4_gpu_k32_matches_cpu_engine(tmp_path, a4_bin):
+    mats = gen.random_chain(6, 8, 32, 0.4, "full", seed=9)
+    folder = str(tmp_path / "in")
+    refio.write_folder(folder, mats, 32)
+    _run(a4_bin, 1, folder, "--device", "hip", "--out", str(tmp_path / "g"), "--quiet")
+    _run(a4_bin, 1, folder, "--device", "cpu", "--out", str(tmp_path / "c"), "--quiet")
+    assert open(tmp_path / "g").read() == open(tmp_path / "c").read()
