@@ -127,7 +127,9 @@ void dump(const std::string& tag, const Mat& M) {
       s << "\n";
     }
   }
-  std::cout << s.str() << std::flush;
+  const std::string d = s.str();
+  std::fwrite(d.data(), 1, d.size(), stdout);
+  std::fflush(stdout);
 }
 
 // ---- minimal thread pool (one HIP stream per worker) -----------------------
@@ -266,8 +268,16 @@ class Loader {
   std::string err_;
 };
 
+// One write(2) per line: ranks share mpiexec's stdout and must not interleave
+// inside a line.
+void emit_line(const std::string& line) {
+  const std::string l = line + "\n";
+  std::fwrite(l.data(), 1, l.size(), stdout);
+  std::fflush(stdout);
+}
+
 void say(const Options& o, const std::string& line) {
-  if (!o.quiet) std::cout << line << "\n" << std::flush;
+  if (!o.quiet) emit_line(line);
 }
 
 // ---- GPU tree ---------------------------------------------------------------
@@ -406,6 +416,9 @@ int run(const Options& o, int rank, int world, double t_start) {
       if (gpu) A4_HIP(hipStreamSynchronize(s));
     } else if (gpu) {
       gpart = gpu_reduce_local(o, lo, hi, k, st);
+      // its buffers were last used on a pool / loader stream that is gone now
+      gpart->m->keys.retarget(s);
+      gpart->m->vals.retarget(s);
     } else {
       cpart = cpu_reduce_local(o, lo, hi, k, st);
     }
@@ -512,6 +525,8 @@ int main(int argc, char** argv) {
     return 1;
   }
   MPI_Finalize();
-  std::cout << "time taken " << (a4::now_s() - t_start) << " seconds" << std::endl;
+  std::ostringstream t;
+  t << "time taken " << (a4::now_s() - t_start) << " seconds";
+  a4::emit_line(t.str());
   return rc;
 }

@@ -4,6 +4,7 @@ checkpoint/resume, fail-fast fault injection.  CPU engine + MPI here; the GPU
 engine (and RCCL at P=1) on the GPU box."""
 import json
 import os
+import re
 import shutil
 import subprocess
 
@@ -51,9 +52,9 @@ def test_a4_cpu_matches_golden(tmp_path, a4_bin, n, p):
     want = golden.chain([golden.from_bsr(m) for m in mats], p=p)
     with open(out) as f:
         assert f.read() == golden.to_text(want)
-    lines = r.stdout.splitlines()
-    assert sum(1 for l in lines if l.startswith("multiplying ")) == n - 1
-    assert sum(1 for l in lines if l.startswith("time taken ") and l.endswith(" seconds")) == p
+    # ranks' lines can interleave in mpiexec's merged stdout: count tokens, not lines
+    assert len(re.findall(r"multiplying \d+ \d+", r.stdout)) == n - 1
+    assert len(re.findall(r"time taken [0-9.e+-]+ seconds", r.stdout)) == p
 
 
 def test_a4_missing_size_file(tmp_path, a4_bin):
@@ -93,7 +94,7 @@ def test_a4_dump(tmp_path, a4_bin):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,p,comm", [(9, 1, "auto"), (7, 2, "mpi"), (8, 4, "mpi")])
+@pytest.mark.parametrize("n,p,comm", [(9, 1, "auto"), (5, 1, "rccl"), (7, 2, "mpi"), (8, 4, "mpi")])
 def test_a4_gpu_matches_golden(tmp_path, a4_bin, n, p, comm):
     mats, folder = _chain(tmp_path, n, blocks=6, k=4, seed=n + p)
     out = str(tmp_path / "matrix")
