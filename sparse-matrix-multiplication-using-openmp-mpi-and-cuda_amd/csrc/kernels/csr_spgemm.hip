@@ -1,27 +1,24 @@
-// CSR x CSR SpGEMM (fp32) for gfx950: row-binned hash accumulation.
+// CSR x CSR SpGEMM (fp32) for gfx950: row-binned accumulation in LDS.
 //
 // North-star engine (BASELINE.json configs 2, 4, 5).  The reference has no CSR
 // path at all; its tile-level analogue is the host join + per-tile kernel of
 // sparse_matrix_mult.cu:140-253.
 //
-// Gustavson row by row, two phases:
-//   symbolic: |union of B rows selected by A(i,:)| per row -> row pointer
-//   numeric:  accumulate a(i,j) * b(j,c) per distinct c, write sorted columns
-// Rows are binned by their intermediate-product count (symbolic) or their
-// exact output count (numeric); each bin gets a kernel instantiation whose
-// per-row hash table lives in LDS (up to 16K key/value slots = 128 KiB, one
-// 1024-thread workgroup per CU).  Rows too long for LDS (R-MAT hubs) use the
-// same algorithm with the table in an HBM workspace.
-//
-// Sorted output without a sort: the hash is MONOTONE in the column,
-// h(c) = floor(c * S / ncols), with forward linear probing into an overflow
-// tail.  A key can only land in a cluster (run of occupied slots) that starts
-// at or after its home slot, so every key of an earlier cluster is smaller:
-// a key's output position is (#occupied slots before its cluster) + (#smaller
-// keys inside its cluster), computed independently per slot.  A probe that
-// wraps past the table end sets a per-row flag; the row is then emitted in
-// slot order and re-sorted by the host (not observed at the bin load factors,
-// but correctness does not depend on it).
+// Gustavson row by row.  Rows are binned by their intermediate-product count;
+// each bin gets a kernel instantiation sized for it (every LDS footprint
+// <= 80 KB so two 512-thread workgroups share a CU):
+//   symbolic (exact nnz per row, two-phase mode): CAS-probing hash tables of
+//            128 .. 16384 keys, long rows over 1/2/4/8 column slices
+//   numeric  short rows: ordered linear probing (sorted table, output is a
+//            compaction); long rows: bucketed ESC (histogram, scatter, per-
+//            bucket register sort + fold, compaction) over 1/2/4/8 slices
+//   longest  rows (R-MAT hubs, > 8 ESC slices): column-chunked dense
+//            accumulation through an HBM scratch ("long rows" below)
+// Both LDS schemes use a MONOTONE hash / bucket function of the column,
+// h(c) = floor((c - c_lo) * S / width), so slot order is column order and
+// rows come out sorted without a sort pass.
+// One-pass mode (ops/spgemm.py) skips the symbolic phase: numeric writes at
+// product-count offsets and spgemm_compact packs the result.
 #include "common.hpp"
 
 namespace {
@@ -856,95 +853,6 @@ __global__ __launch_bounds__(256) void spgemm_row_splits(const int64_t* __restri
   }
 }
 
-// ---------------------------------------------------------------------------
-// HBM-resident table for rows beyond the LDS bins.  One 1024-thread workgroup
-// per row; table (keys + vals, TS slots each) at ws_off[b] in the workspace,
-// pre-filled with EMPTY / 0 by the host.  Every table access is an atomic or
-// an agent-scope relaxed load, so no L1 staleness can creep in.
-constexpr int GNT = 1024;
-
-template <bool NUMERIC>
-__global__ __launch_bounds__(GNT) void spgemm_global(
-    const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
-    const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
-    const int32_t* __restrict__ rows, const int64_t* __restrict__ ws_off, const int64_t* __restrict__ ws_size,
-    int32_t* __restrict__ ws_keys, float* __restrict__ ws_vals, int ncols, int32_t* __restrict__ row_nnz,
-    const int64_t* __restrict__ Crp, int32_t* __restrict__ Cci, float* __restrict__ Cv,
-    int32_t* __restrict__ unsorted) {
-  constexpr int NW = GNT / 64;
-  __shared__ int wsum[NW];
-  __shared__ int s_count, s_wrapped;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int row = rows[blockIdx.x];
-  const int64_t TS = ws_size[blockIdx.x];
-  const int64_t S = TS - GNT;
-  int32_t* keys = ws_keys + ws_off[blockIdx.x];
-  float* vals = ws_vals + ws_off[blockIdx.x];
-  if (tid == 0) { s_count = 0; s_wrapped = 0; }
-  __syncthreads();
-  const uint32_t mult = hash_mult(S, ncols);
-  int mine = 0;
-  const int64_t a0 = Arp[row], a1 = Arp[row + 1];
-  for (int64_t e = a0 + w; e < a1; e += NW) {
-    const int j = Aci[e];
-    const float a = NUMERIC ? Av[e] : 0.f;
-    for (int64_t f = Brp[j] + lane; f < Brp[j + 1]; f += 64) {
-      const int c = Bci[f];
-      int64_t h = hash_home(c, mult);
-      while (true) {
-        int k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == c) break;
-        if (k == EMPTY) {
-          int old = atomicCAS(&keys[h], EMPTY, c);
-          if (old == EMPTY) { ++mine; break; }
-          if (old == c) break;
-        }
-        if (++h == TS) { h = 0; s_wrapped = 1; }
-      }
-      if (NUMERIC) atomicAdd(&vals[h], a * Bv[f]);
-    }
-  }
-  if (!NUMERIC) {
-    if (mine) atomicAdd(&s_count, mine);
-    __syncthreads();
-    if (tid == 0) row_nnz[row] = s_count;
-    return;
-  }
-  __syncthreads();
-  auto ld = [](const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  auto ldf = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  auto st = [](int32_t* p, int32_t x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  auto stf = [](float* p, float x) { __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  for (int64_t s = tid; s < TS; s += GNT) {
-    if (ld(&keys[s]) != EMPTY && (s == 0 || ld(&keys[s - 1]) == EMPTY)) {
-      int64_t e = s;
-      while (e + 1 < TS && ld(&keys[e + 1]) != EMPTY) ++e;
-      for (int64_t i = s + 1; i <= e; ++i) {
-        const int kk = ld(&keys[i]);
-        const float vv = ldf(&vals[i]);
-        int64_t q = i - 1;
-        while (q >= s && ld(&keys[q]) > kk) { st(&keys[q + 1], ld(&keys[q])); stf(&vals[q + 1], ldf(&vals[q])); --q; }
-        st(&keys[q + 1], kk);
-        stf(&vals[q + 1], vv);
-      }
-    }
-  }
-  __syncthreads();
-  const int64_t per = (TS + GNT - 1) / GNT;
-  const int64_t s0 = tid * per, s1 = (s0 + per < TS) ? s0 + per : TS;
-  int cnt = 0;
-  for (int64_t s = s0; s < s1; ++s) cnt += ld(&keys[s]) != EMPTY;
-  int total;
-  int o = block_excl_scan<GNT, int>(cnt, wsum, &total);
-  const int64_t base = Crp[row] + o;
-  int64_t q = 0;
-  for (int64_t s = s0; s < s1; ++s) {
-    const int k = ld(&keys[s]);
-    if (k != EMPTY) { Cci[base + q] = k; Cv[base + q] = ldf(&vals[s]); ++q; }
-  }
-  if (tid == 0 && s_wrapped) unsorted[row] = 1;
-}
-
 // One-pass mode: rows were written at their product-count offsets (src_off);
 // copy each row's n[i] entries to the final CSR (dst_off).  One wave per row.
 __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict__ src_off,
@@ -965,6 +873,134 @@ __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict_
   for (; i < n; i += 64) {
     dci[d0 + i] = sci[s0 + i];
     dv[d0 + i] = sv[s0 + i];
+  }
+}
+
+// ------------------------------------------------------------ long rows ---
+// Rows beyond the LDS bins (R-MAT hubs: up to ~10^7 products, ~5*10^5
+// outputs) go through a column-chunked dense pipeline with an HBM scratch:
+//   route  (pass 1) every workgroup takes <= LONG_EPW A entries of ONE row and
+//          histograms its products by column chunk (W columns) in LDS
+//   scan   (host/torch) per-(row, chunk) regions in the scratch and each
+//          workgroup's slot range inside them: no global atomics
+//   route  (pass 2) the same products are scattered into their (row, chunk)
+//          region as (column | a*b bits), slots from LDS cursors
+//   dense  one workgroup per (row, chunk): LDS dense accumulator (W floats +
+//          occupancy bits), then the occupied columns are written back in
+//          column order over the chunk's region, count in rt_nnz
+//   place  chunk results copied to their final CSR positions
+// Traffic per product: 4 + 8 B of B reads, 8 B scratch write + 8 B read.
+constexpr int LONG_NT = 512;
+constexpr int LONG_EPW = 64;            // A entries per routing workgroup
+constexpr int LONG_LGW = 14;            // W = 16384 columns per chunk
+constexpr int LONG_W = 1 << LONG_LGW;
+constexpr int LONG_MAXCH = 4096;        // chunks per row (ncols <= 2^26)
+
+template <bool SCATTER>
+__global__ __launch_bounds__(LONG_NT) void long_route(
+    const int32_t* __restrict__ Aci, const float* __restrict__ Av, const int64_t* __restrict__ Brp,
+    const int32_t* __restrict__ Bci, const float* __restrict__ Bv, const int64_t* __restrict__ wg_e0,
+    const int64_t* __restrict__ wg_e1, int nch, int32_t* __restrict__ wg_hist,
+    const int64_t* __restrict__ wg_base, unsigned long long* __restrict__ scratch) {
+  __shared__ unsigned long long cur[SCATTER ? LONG_MAXCH : 1];
+  __shared__ int hist[SCATTER ? 1 : LONG_MAXCH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t wg = blockIdx.x;
+  for (int t = tid; t < nch; t += LONG_NT) {
+    if constexpr (SCATTER) cur[t] = (unsigned long long)wg_base[wg * nch + t];
+    else hist[t] = 0;
+  }
+  __syncthreads();
+  const int64_t e1 = wg_e1[wg];
+  for (int64_t e = wg_e0[wg] + w; e < e1; e += LONG_NT / 64) {
+    const int j = Aci[e];
+    const float a = SCATTER ? Av[e] : 0.f;
+    const int64_t b0 = Brp[j], b1 = Brp[j + 1];
+    for (int64_t f0 = b0; f0 < b1; f0 += 256) {   // 4 loads in flight per lane
+      int c[4];
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t f = f0 + u * 64 + lane;
+        const bool ok = f < b1;
+        c[u] = ok ? Bci[f] : -1;
+        if constexpr (SCATTER) v[u] = ok ? Bv[f] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (c[u] < 0) continue;
+        const int t = c[u] >> LONG_LGW;
+        if constexpr (SCATTER) {
+          const unsigned long long pos = atomicAdd(&cur[t], 1ull);
+          scratch[pos] = ((unsigned long long)__float_as_uint(a * v[u]) << 32) | (uint32_t)c[u];
+        } else {
+          atomicAdd(&hist[t], 1);
+        }
+      }
+    }
+  }
+  if constexpr (!SCATTER) {
+    __syncthreads();
+    for (int t = tid; t < nch; t += LONG_NT) wg_hist[wg * nch + t] = hist[t];
+  }
+}
+
+template <bool VALUES>
+__global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restrict__ rt_off,
+                                                         const int64_t* __restrict__ rt_cnt, int nch,
+                                                         unsigned long long* __restrict__ scratch,
+                                                         int64_t* __restrict__ rt_nnz) {
+  __shared__ float vals[VALUES ? LONG_W : 1];
+  __shared__ uint32_t bits[LONG_W / 32];
+  __shared__ int wsum[LONG_NT / 64];
+  const int64_t rt = blockIdx.x;
+  const int64_t n = rt_cnt[rt];
+  if (n == 0) {
+    if (threadIdx.x == 0) rt_nnz[rt] = 0;
+    return;
+  }
+  const int tid = threadIdx.x;
+  const int64_t base = rt_off[rt];
+  const int c0 = (int)(rt % nch) << LONG_LGW;
+  for (int i = tid; i < LONG_W / 32; i += LONG_NT) bits[i] = 0u;
+  if constexpr (VALUES)
+    for (int i = tid; i < LONG_W / 4; i += LONG_NT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += LONG_NT) {
+    const unsigned long long x = scratch[base + i];
+    const int c = (int)(uint32_t)x - c0;
+    atomicOr(&bits[c >> 5], 1u << (c & 31));
+    if constexpr (VALUES) atomicAdd(&vals[c], __uint_as_float((uint32_t)(x >> 32)));
+  }
+  __syncthreads();
+  // one bit word per thread (LONG_W / 32 == LONG_NT): occupied columns in order
+  static_assert(LONG_W / 32 == LONG_NT, "one occupancy word per thread");
+  const uint32_t word = bits[tid];
+  int total;
+  const int pos = block_excl_scan<LONG_NT, int>(__popc(word), wsum, &total);
+  int k = 0;
+  for (uint32_t m = word; m; m &= m - 1, ++k) {
+    const int b = __ffs(m) - 1;
+    const int cl = tid * 32 + b;
+    const float v = VALUES ? vals[cl] : 0.f;
+    scratch[base + pos + k] = ((unsigned long long)__float_as_uint(v) << 32) | (uint32_t)(c0 + cl);
+  }
+  if (tid == 0) rt_nnz[rt] = total;
+}
+
+// chunk results -> final CSR positions (one wave per (row, chunk))
+__global__ __launch_bounds__(256) void long_place(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                  const int64_t* __restrict__ cnt, int64_t nrt,
+                                                  const unsigned long long* __restrict__ scratch,
+                                                  int32_t* __restrict__ Cci, float* __restrict__ Cv) {
+  const int64_t rt = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (rt >= nrt) return;
+  const int64_t s = src[rt], d = dst[rt], n = cnt[rt];
+  for (int64_t i = lane; i < n; i += 64) {
+    const unsigned long long x = scratch[s + i];
+    Cci[d + i] = (int32_t)(uint32_t)x;
+    Cv[d + i] = __uint_as_float((uint32_t)(x >> 32));
   }
 }
 
@@ -1097,20 +1133,52 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
 #undef SPMM_SARGS
 }
 
-SPMM_EXPORT int spmm_spgemm_global(int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
-                                   const int64_t* Brp, const int32_t* Bci, const float* Bv, const int32_t* rows,
-                                   int64_t nrows, const int64_t* ws_off, const int64_t* ws_size, int32_t* ws_keys,
-                                   float* ws_vals, int ncols, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci,
-                                   float* Cv, int32_t* unsorted, void* stream) {
-  if (nrows <= 0) return 0;
+
+// ---- long rows (see the kernels' comment) -----------------------------------
+SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp,
+                                       const int32_t* Bci, const float* Bv, const int64_t* wg_e0,
+                                       const int64_t* wg_e1, int64_t nwg, int nch, int32_t* wg_hist,
+                                       const int64_t* wg_base, void* scratch, void* stream) {
+  if (nwg <= 0) return 0;
+  if (nch > LONG_MAXCH) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (numeric)
-    hipLaunchKernelGGL(spgemm_global<true>, dim3((unsigned)nrows), dim3(GNT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
-                       rows, ws_off, ws_size, ws_keys, ws_vals, ncols, row_nnz, Crp, Cci, Cv, unsorted);
+  if (scatter)
+    hipLaunchKernelGGL(long_route<true>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0, wg_e1,
+                       nch, wg_hist, wg_base, (unsigned long long*)scratch);
   else
-    hipLaunchKernelGGL(spgemm_global<false>, dim3((unsigned)nrows), dim3(GNT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
-                       rows, ws_off, ws_size, ws_keys, ws_vals, ncols, row_nnz, Crp, Cci, Cv, unsorted);
+    hipLaunchKernelGGL(long_route<false>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0,
+                       wg_e1, nch, wg_hist, wg_base, (unsigned long long*)scratch);
   SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_cnt, int64_t nrt, int nch,
+                                       void* scratch, int64_t* rt_nnz, void* stream) {
+  if (nrt <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (values)
+    hipLaunchKernelGGL(long_dense<true>, dim3((unsigned)nrt), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nch,
+                       (unsigned long long*)scratch, rt_nnz);
+  else
+    hipLaunchKernelGGL(long_dense<false>, dim3((unsigned)nrt), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nch,
+                       (unsigned long long*)scratch, rt_nnz);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_spgemm_long_place(const int64_t* src, const int64_t* dst, const int64_t* cnt, int64_t nrt,
+                                       const void* scratch, int32_t* Cci, float* Cv, void* stream) {
+  if (nrt <= 0) return 0;
+  hipLaunchKernelGGL(long_place, dim3((unsigned)((nrt + 3) / 4)), dim3(256), 0, (hipStream_t)stream, src, dst, cnt,
+                     nrt, (const unsigned long long*)scratch, Cci, Cv);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch) {
+  *lgw = LONG_LGW;
+  *epw = LONG_EPW;
+  *maxch = LONG_MAXCH;
   return 0;
 }
 

@@ -37,9 +37,12 @@ _native.register_hip("spmm_spgemm_row_splits", c_vp, c_vp, C_I64, C_INT, c_vp, c
 _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_compact", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, c_vp,
+                     c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
-_native.register_hip("spmm_spgemm_global", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp,
-                     c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -59,7 +62,7 @@ LOAD = CONFIG.spgemm_load              # max load factor of a single-pass LDS ta
 LOAD_SLICED = CONFIG.spgemm_load_sliced   # ... of the big (column-sliced) tables
 ESC_MIN = CONFIG.spgemm_esc_min        # numeric rows with more products use the ESC kernel
 ESC_LOAD = 0.9                         # per-slice margin of the multi-slice ESC bins
-GLOBAL_WS_BYTES = int(CONFIG.spgemm_global_ws_gb * (1 << 30))   # HBM budget per batch of global-table rows
+GLOBAL_WS_BYTES = int(CONFIG.spgemm_global_ws_gb * (1 << 30))   # HBM scratch budget per batch of long rows
 
 
 @dataclass
@@ -110,37 +113,6 @@ def row_nprod(A: CSR, B: CSR) -> torch.Tensor:
     return nprod
 
 
-def _global_rows(numeric: int, A: CSR, B: CSR, rows: torch.Tensor, counts: torch.Tensor, row_nnz, Crp, Cci, Cv,
-                 unsorted, stream) -> None:
-    """Rows whose table exceeds LDS: HBM hash tables, processed in batches."""
-    dev = A.device
-    lib = _native.hip()
-    P = _native.ptr
-    cap = 1 << max(15, (max(B.n, 1) - 1).bit_length())
-    cnt = counts.tolist()
-    sizes = []
-    for c in cnt:
-        s = 1 << max(15, (int(c / 0.5) - 1).bit_length())
-        sizes.append(min(s, cap * 2) + 1024)
-    i = 0
-    empty_f = torch.empty(0, dtype=torch.float32, device=dev)
-    while i < len(sizes):
-        j, tot = i, 0
-        while j < len(sizes) and (j == i or (tot + sizes[j]) * 8 <= GLOBAL_WS_BYTES):
-            tot += sizes[j]
-            j += 1
-        sz = torch.tensor(sizes[i:j], dtype=torch.int64, device=dev)
-        off = torch.cumsum(sz, 0) - sz
-        keys = torch.full((tot,), -1, dtype=torch.int32, device=dev)
-        vals = torch.zeros(tot, dtype=torch.float32, device=dev) if numeric else empty_f
-        r = rows[i:j].contiguous()
-        _native.check(lib.spmm_spgemm_global(numeric, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
-                                             P(B.val), P(r), j - i, P(off), P(sz), P(keys), P(vals), B.n,
-                                             P(row_nnz), P(Crp), P(Cci), P(Cv), P(unsorted), stream),
-                      "spgemm_global")
-        i = j
-
-
 def _onepass_fits(total_products: int, dev: torch.device) -> bool:
     """One-pass mode needs a product-count-sized staging buffer next to C."""
     mode = CONFIG.spgemm_onepass
@@ -151,6 +123,89 @@ def _onepass_fits(total_products: int, dev: torch.device) -> bool:
     free, _ = torch.cuda.mem_get_info(dev)
     free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)   # the caching allocator's spare
     return 2 * total_products * 8 <= 0.8 * free
+
+
+_LONG = None
+
+
+def _long_params():
+    global _LONG
+    if _LONG is None:
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        _native.hip().spmm_spgemm_long_params(C.byref(a), C.byref(b), C.byref(c))
+        _LONG = (a.value, b.value, c.value)
+    return _LONG
+
+
+def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torch.Tensor, stream,
+               out_nnz: Optional[torch.Tensor] = None, Crp=None, Cci=None, Cv=None,
+               expect_nnz: Optional[torch.Tensor] = None) -> None:
+    """Rows beyond the LDS bins: column-chunked dense accumulation through an
+    HBM scratch (csr_spgemm.hip "long rows").  ``values=0`` only counts
+    (writes ``out_nnz[rows]``); ``values=1`` also writes each row at
+    ``Crp[row]`` (and its count to ``out_nnz`` when given).  Rows are
+    processed in batches whose products fit the scratch budget."""
+    dev = A.device
+    lib = _native.hip()
+    P = _native.ptr
+    lgw, epw, maxch = _long_params()
+    nch = (B.n + (1 << lgw) - 1) >> lgw
+    if nch > maxch:
+        raise ValueError(f"long-row path supports at most {maxch << lgw} columns, got {B.n}")
+    cap = max(GLOBAL_WS_BYTES // 8, int(nprod_rows.max()))
+    rows = rows.long()
+    csum = torch.cumsum(nprod_rows.long(), 0).tolist()
+    start, done = 0, 0
+    while start < rows.numel():
+        end = start
+        while end < rows.numel() and (end == start or csum[end] - done <= cap):
+            end += 1
+        rb = rows[start:end]
+        R = end - start
+        a0 = A.rowptr[rb]
+        na = A.rowptr[rb + 1] - a0
+        nwg_r = torch.clamp((na + epw - 1) // epw, min=1)
+        nwg = int(nwg_r.sum())
+        row_of_wg = torch.repeat_interleave(torch.arange(R, device=dev), nwg_r)
+        first_wg = torch.cumsum(nwg_r, 0) - nwg_r
+        kk = torch.arange(nwg, device=dev) - first_wg[row_of_wg]
+        wg_e0 = (a0[row_of_wg] + kk * epw).contiguous()
+        wg_e1 = torch.minimum(wg_e0 + epw, (a0 + na)[row_of_wg]).contiguous()
+        wg_hist = torch.empty(nwg * nch, dtype=torch.int32, device=dev)
+        nil = None
+        _native.check(lib.spmm_spgemm_long_route(0, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
+                                                 P(wg_e1), nwg, nch, P(wg_hist), nil, nil, stream), "long_route")
+        H = wg_hist.view(nwg, nch).long()
+        T = torch.zeros((R, nch), dtype=torch.int64, device=dev).index_add_(0, row_of_wg, H)
+        chunk_off = torch.cumsum(T, 1) - T
+        row_tot = T.sum(1)
+        row_base = torch.cumsum(row_tot, 0) - row_tot
+        Hc = torch.cumsum(H, 0) - H
+        Hc = Hc - Hc[first_wg][row_of_wg]
+        wg_base = (row_base[row_of_wg, None] + chunk_off[row_of_wg] + Hc).contiguous()
+        scratch = torch.empty(int(row_tot.sum()), dtype=torch.int64, device=dev)
+        _native.check(lib.spmm_spgemm_long_route(1, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
+                                                 P(wg_e1), nwg, nch, nil, P(wg_base), P(scratch), stream),
+                      "long_route")
+        del wg_base, Hc, H, wg_hist
+        rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()
+        rt_cnt = T.reshape(-1).contiguous()
+        rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
+        _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
+                                                 stream), "long_dense")
+        nnz_rt = rt_nnz.view(R, nch)
+        nnz_r = nnz_rt.sum(1)
+        if expect_nnz is not None and not torch.equal(nnz_r, expect_nnz[rb].long()):
+            raise RuntimeError("spgemm long rows: numeric count differs from the symbolic count")
+        if out_nnz is not None:
+            out_nnz[rb] = nnz_r.to(out_nnz.dtype)
+        if values:
+            dst = (Crp[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
+            _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
+                                                     P(Cv), stream), "long_place")
+        del scratch
+        done = csum[end - 1]
+        start = end
 
 
 def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
@@ -242,7 +297,8 @@ def _splits(B: CSR) -> torch.Tensor:
 
 
 def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins,
-              mean_seg: float = 0.0, out_nnz: Optional[torch.Tensor] = None):
+              mean_seg: float = 0.0, out_nnz: Optional[torch.Tensor] = None,
+              nprod: Optional[torch.Tensor] = None):
     """Run the LDS bins, then the HBM path for the rest.  Numeric: ``row_nnz`` is
     each row's capacity in the output (exact nnz, or the product count in
     one-pass mode where ``out_nnz`` receives the real counts)."""
@@ -277,10 +333,13 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
         global_rows.append(spill)
     if global_rows:
         rows = torch.cat(global_rows)
-        if out_nnz is not None:   # one-pass: exact counts of these rows first
-            d64, d32, df = _dummies(dev)
-            _global_rows(0, A, B, rows, counts[rows.long()], out_nnz, d64, d32, df, flags, stream)
-        _global_rows(numeric, A, B, rows, counts[rows.long()], row_nnz, Crp, Cci, Cv, flags, stream)
+        nprod_rows = nprod[rows.long()] if nprod is not None else counts[rows.long()]
+        if not numeric:            # symbolic: exact counts
+            _long_rows(0, A, B, rows, nprod_rows, stream, out_nnz=row_nnz)
+        elif out_nnz is not None:  # one-pass: values at product-count offsets, real counts out
+            _long_rows(1, A, B, rows, nprod_rows, stream, out_nnz=out_nnz, Crp=Crp, Cci=Cci, Cv=Cv)
+        else:                      # two-phase numeric: into the layout fixed by symbolic
+            _long_rows(1, A, B, rows, nprod_rows, stream, Crp=Crp, Cci=Cci, Cv=Cv, expect_nnz=row_nnz)
 
 
 def symbolic(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> torch.Tensor:
