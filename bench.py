@@ -138,6 +138,8 @@ def main() -> None:
     ap.add_argument("--scale", type=int, default=20)   # scale 24 A.A^T does not fit 8x288 GB (C ~ 10^11+ nnz)
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend (gloo on GPUs: rehearse several ranks on one card)")
     args = ap.parse_args()
 
     import torch
@@ -146,7 +148,7 @@ def main() -> None:
     from spmm_amd import _native
     from spmm_amd.parallel import comm as CM
 
-    comm = CM.init(backend="auto", device="auto")
+    comm = CM.init(backend=args.backend, device="auto")
     if comm.device.type == "cuda":
         _native.hip()
     if args.workload == "spgemm":

@@ -104,7 +104,7 @@ def build_a4(force: bool = False, verbose: bool = False):
         rpath = ":".join(["$ORIGIN/../lib", "/usr/lib/x86_64-linux-gnu", "/opt/rocm/lib", os.path.join(mpi, "lib")])
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I", rt, "-I", os.path.join(mpi, "include"),
                "-o", tmp] + srcs + [
-               "-L", LIB_DIR, "-lspmm_host", "-lspmm_hip", "-L/opt/rocm/lib", "-lrccl",
+               "-L", LIB_DIR, "-lspmm_host", "-lspmm_hip", "-L/opt/rocm/lib", "-lrccl", "-lrocprofiler-sdk-roctx",
                # libmpi by path: a -L into conda would also pick conda's old libstdc++ at link time
                "-Wl," + os.path.join(mpi, "lib", "libmpi.so"), "-lpthread", f"-Wl,-rpath,{rpath}"]
         if verbose:

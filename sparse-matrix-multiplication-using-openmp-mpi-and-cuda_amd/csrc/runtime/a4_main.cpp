@@ -132,14 +132,37 @@ void dump(const std::string& tag, const Mat& M) {
   std::fflush(stdout);
 }
 
+// Every HIP stream of the run, created up front and destroyed only after the
+// arena has been trimmed: buffers cross streams (loader -> pool -> main) and
+// a release records its event on the stream of the buffer's last use.
+struct Streams {
+  hipStream_t main = nullptr, load = nullptr;
+  std::vector<hipStream_t> pool;
+  Streams(int npool, bool gpu) {
+    if (!gpu) return;
+    A4_HIP(hipStreamCreateWithFlags(&main, hipStreamNonBlocking));
+    A4_HIP(hipStreamCreateWithFlags(&load, hipStreamNonBlocking));
+    pool.resize((size_t)npool);
+    for (auto& s : pool) A4_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  ~Streams() {
+    if (!main) return;
+    try {
+      Arena::get().trim();
+    } catch (const std::exception&) {
+    }
+    for (auto s : pool) (void)hipStreamDestroy(s);
+    (void)hipStreamDestroy(load);
+    (void)hipStreamDestroy(main);
+  }
+};
+
 // ---- minimal thread pool (one HIP stream per worker) -----------------------
 class Pool {
  public:
-  Pool(int n, bool gpu) {
+  Pool(int n, const std::vector<hipStream_t>& streams) {
     for (int i = 0; i < n; ++i) {
-      hipStream_t s = nullptr;
-      if (gpu) A4_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-      streams_.push_back(s);
+      streams_.push_back(i < (int)streams.size() ? streams[(size_t)i] : nullptr);
       workers_.emplace_back([this, i] { loop(i); });
     }
   }
@@ -150,8 +173,6 @@ class Pool {
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
-    for (auto s : streams_)
-      if (s) (void)hipStreamDestroy(s);
   }
   template <typename F>
   auto submit(F f) -> std::future<decltype(f(hipStream_t{}))> {
@@ -214,12 +235,12 @@ struct Stats {
 template <typename T>
 class Loader {
  public:
-  Loader(const Options& o, int lo, int hi, int k, bool gpu, Stats& st) {
+  // s: the upload stream (outlives the loader), nullptr for the CPU engine
+  Loader(const Options& o, int lo, int hi, int k, hipStream_t s, Stats& st) {
     th_ = std::thread([=, &o, &st] {
-      hipStream_t s = nullptr;
-      if (gpu) (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
       try {
         for (int i = lo; i <= hi; ++i) {
+          Range r("load matrix" + std::to_string(i + 1));
           Mat M = read_ref(o.folder + "/matrix" + std::to_string(i + 1), k, o.threads);
           if (o.dump) dump("matrix" + std::to_string(i + 1), M);
           {
@@ -240,7 +261,6 @@ class Loader {
         err_ = e.what();
         cv_.notify_all();
       }
-      if (s) (void)hipStreamDestroy(s);
     });
   }
   ~Loader() {
@@ -287,10 +307,13 @@ std::future<Node> gpu_product(Pool& pool, std::shared_future<Node> fa, std::shar
     A4_HIP(hipStreamWaitEvent(s, a.ev, 0));
     A4_HIP(hipStreamWaitEvent(s, b.ev, 0));
     int64_t pairs = 0;
+    Range r("multiply");
     DevMat C = dev_multiply(*a.m, *b.m, s, &pairs);
-    // operands die on this stream, after the product's kernels
+    // operands die on this stream, after the product's kernels; the product
+    // is drained first so a later free never races a pending kernel
     a.m->keys.retarget(s); a.m->vals.retarget(s);
     b.m->keys.retarget(s); b.m->vals.retarget(s);
+    A4_HIP(hipStreamSynchronize(s));
     (void)hipEventDestroy(a.ev);
     (void)hipEventDestroy(b.ev);
     {
@@ -302,9 +325,9 @@ std::future<Node> gpu_product(Pool& pool, std::shared_future<Node> fa, std::shar
   });
 }
 
-Node gpu_reduce_local(const Options& o, int lo, int hi, int k, Stats& st) {
-  Loader<Node> loader(o, lo, hi, k, true, st);
-  Pool pool(o.streams, true);
+Node gpu_reduce_local(const Options& o, int lo, int hi, int k, const Streams& ss, Stats& st) {
+  Loader<Node> loader(o, lo, hi, k, ss.load, st);
+  Pool pool(o.streams, ss.pool);
   const int n = hi - lo + 1;
   std::vector<std::shared_future<Node>> arr;
   auto ready = [](Node x) {
@@ -332,7 +355,7 @@ Node gpu_reduce_local(const Options& o, int lo, int hi, int k, Stats& st) {
 
 // ---- CPU tree ---------------------------------------------------------------
 Mat cpu_reduce_local(const Options& o, int lo, int hi, int k, Stats& st) {
-  Loader<Mat> loader(o, lo, hi, k, false, st);
+  Loader<Mat> loader(o, lo, hi, k, nullptr, st);
   const int n = hi - lo + 1;
   auto mul = [&](const Mat& a, const Mat& b) {
     int64_t pairs = 0;
@@ -403,8 +426,8 @@ int run(const Options& o, int rank, int world, double t_start) {
     lo = (int)(rank * op);
     hi = (int)(rank == world - 1 ? N - 1 : (rank + 1) * op - 1);
   }
-  hipStream_t s = nullptr;
-  if (gpu) A4_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  Streams ss(o.streams, gpu);   // destroyed after gpart (declared below) is released
+  hipStream_t s = ss.main;
   std::optional<Node> gpart;
   std::optional<Mat> cpart;
   const double t0 = now_s();
@@ -415,8 +438,9 @@ int run(const Options& o, int rank, int world, double t_start) {
       if (gpu) gpart = make_node(dev_upload(M, s), s); else cpart = std::move(M);
       if (gpu) A4_HIP(hipStreamSynchronize(s));
     } else if (gpu) {
-      gpart = gpu_reduce_local(o, lo, hi, k, st);
-      // its buffers were last used on a pool / loader stream that is gone now
+      gpart = gpu_reduce_local(o, lo, hi, k, ss, st);
+      // from here on the main stream is the user of the partial
+      A4_HIP(hipStreamWaitEvent(s, gpart->ev, 0));
       gpart->m->keys.retarget(s);
       gpart->m->vals.retarget(s);
     } else {
@@ -441,6 +465,7 @@ int run(const Options& o, int rank, int world, double t_start) {
   bool alive = true;
   if (N / world != 0 && world > 1) {
     for (int step = 1; step < world && alive; step *= 2) {
+      Range rstep("cross-rank step " + std::to_string(step));
       if (rank % (2 * step) == 0) {
         if (rank + step < world) {
           if (gpu) {
@@ -478,6 +503,7 @@ int run(const Options& o, int rank, int world, double t_start) {
   st.t_comm = now_s() - t1;
 
   if (rank == 0) {
+    Range r("prune + write");
     const double t2 = now_s();
     Mat final_;
     if (gpu) {
@@ -501,7 +527,6 @@ int run(const Options& o, int rank, int world, double t_start) {
     }
   }
   gpart.reset();
-  if (s) (void)hipStreamDestroy(s);
   comm->barrier();
   return 0;
 }

@@ -87,6 +87,26 @@ __global__ void k_gather_tiles(const int32_t* __restrict__ keys, const uint64_t*
   for (int64_t e = threadIdx.x; e < kk; e += blockDim.x) ovals[d * kk + e] = vals[t * kk + e];
 }
 
+// Largest A / B tile index referenced by the sorted pairs, + 1 (0 = none):
+// the host checks them against the operand sizes before the numeric kernel
+// gathers tiles by these indices.
+__global__ void k_pair_bounds(const uint64_t* __restrict__ ab, int64_t n, unsigned long long* __restrict__ bounds) {
+  const int64_t p = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  unsigned long long a = 0, b = 0;
+  if (p < n) {
+    a = (ab[p] >> 32) + 1;
+    b = (ab[p] & 0xffffffffu) + 1;
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    a = max(a, (unsigned long long)__shfl_xor(a, d));
+    b = max(b, (unsigned long long)__shfl_xor(b, d));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&bounds[0], a);
+    atomicMax(&bounds[1], b);
+  }
+}
+
 // A few pinned int64 slots per host thread for the size read-backs.
 int64_t* pinned_scratch() {
   thread_local int64_t* p = nullptr;
@@ -94,12 +114,15 @@ int64_t* pinned_scratch() {
   return p;
 }
 
-int64_t read_back(const int64_t* dptr, hipStream_t s) {
+// Copies n (<= 8) int64 values from the device and waits for them.
+const int64_t* read_back_n(const int64_t* dptr, int n, hipStream_t s) {
   int64_t* h = pinned_scratch();
-  A4_HIP(hipMemcpyAsync(h, dptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  A4_HIP(hipMemcpyAsync(h, dptr, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   A4_HIP(hipStreamSynchronize(s));
-  return h[0];
+  return h;
 }
+
+int64_t read_back(const int64_t* dptr, hipStream_t s) { return read_back_n(dptr, 1, s)[0]; }
 
 template <typename F>
 DevBuf<char> cub_temp(F&& query, hipStream_t s) {
@@ -243,6 +266,21 @@ DevMat dev_multiply(const DevMat& A, const DevMat& B, hipStream_t s, int64_t* ti
     A4_HIP(hipcub::DeviceScan::InclusiveSum(tmp.get(), b, runs.get() + 1, tile_ptr.get() + 1, (int)nt, s));
   }
   runs.reset();
+  // Host-side guard of the numeric kernel's assumptions: the groups cover
+  // exactly the np pairs and every pair indexes existing A / B tiles.
+  {
+    DevBuf<int64_t> chk(3, s);
+    A4_HIP(hipMemsetAsync(chk.get(), 0, 2 * sizeof(int64_t), s));
+    hipLaunchKernelGGL(k_pair_bounds, dim3(blocks_for(np)), dim3(TPB), 0, s, ab2.get(), np,
+                       reinterpret_cast<unsigned long long*>(chk.get()));
+    A4_HIP(hipGetLastError());
+    A4_HIP(hipMemcpyAsync(chk.get() + 2, tile_ptr.get() + nt, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    const int64_t* h = read_back_n(chk.get(), 3, s);
+    A4_CHECK(h[2] == np && h[0] >= 1 && h[0] <= na && h[1] >= 1 && h[1] <= nbB,
+             "bsr symbolic phase produced inconsistent pairs (groups " + std::to_string(h[2]) + "/" +
+                 std::to_string(np) + ", max A tile " + std::to_string(h[0] - 1) + "/" + std::to_string(na) +
+                 ", max B tile " + std::to_string(h[1] - 1) + "/" + std::to_string(nbB) + ")");
+  }
   DevBuf<int32_t> pa((size_t)np, s), pb((size_t)np, s);
   hipLaunchKernelGGL(k_split, dim3(blocks_for(np)), dim3(TPB), 0, s, ab2.get(), np, pa.get(), pb.get());
   A4_HIP(hipGetLastError());

@@ -9,11 +9,13 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -42,14 +44,52 @@ inline double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Stream-ordered device allocation (hipMallocAsync), freed on the stream that
-// last used it.  Move-only.
+// Scoped roctx range: the phases the reference times with chrono and never
+// prints (sparse_matrix_mult.cu:160-274) show up as named ranges in
+// `rocprofv3 --marker-trace` timelines (load / multiply / send / recv / write).
+class Range {
+ public:
+  explicit Range(const std::string& name) { roctxRangePushA(name.c_str()); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
+
+// Device memory arena (alloc.cpp): a caching allocator with explicit event
+// ordering, in place of HIP's stream-ordered pool (hipMallocAsync).  A
+// released block carries an event recorded on the stream of its last use; the
+// next allocation that takes it makes its own stream wait on that event, so
+// reuse is ordered after every earlier use whatever streams are involved, and
+// nothing is returned to the driver before trim() (HBM is 288 GB).
+// Streams that recorded a release must stay alive until trim().
+class Arena {
+ public:
+  static Arena& get();
+  void* alloc(size_t bytes, hipStream_t s);
+  void release(void* p, size_t bytes, hipStream_t s);
+  void trim();   // device-synchronises, frees every cached block
+  size_t cached_bytes() const { return cached_; }
+  size_t peak_bytes() const { return peak_; }
+
+ private:
+  struct Block {
+    void* p;
+    size_t bytes;
+    hipEvent_t ev;
+  };
+  std::vector<Block> free_;   // small: a linear best-fit scan is cheap
+  size_t cached_ = 0, live_ = 0, peak_ = 0;
+  std::mutex mu_;
+};
+
+// Device buffer from the arena, released on the stream that last used it.
+// Move-only.
 template <typename T>
 class DevBuf {
  public:
   DevBuf() = default;
   DevBuf(size_t n, hipStream_t s) : n_(n), s_(s) {
-    if (n_) A4_HIP(hipMallocAsync(reinterpret_cast<void**>(&p_), n_ * sizeof(T), s_));
+    if (n_) p_ = static_cast<T*>(Arena::get().alloc(n_ * sizeof(T), s_));
   }
   DevBuf(DevBuf&& o) noexcept : p_(o.p_), n_(o.n_), s_(o.s_) { o.p_ = nullptr; o.n_ = 0; }
   DevBuf& operator=(DevBuf&& o) noexcept {
@@ -60,11 +100,11 @@ class DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { reset(); }
   void reset() {
-    if (p_) (void)hipFreeAsync(p_, s_);
+    if (p_) Arena::get().release(p_, n_ * sizeof(T), s_);
     p_ = nullptr;
     n_ = 0;
   }
-  // later frees are ordered after the work of `s` (the last user)
+  // the release is ordered after the work of `s` (the last user)
   void retarget(hipStream_t s) { s_ = s; }
   T* get() const { return p_; }
   size_t size() const { return n_; }
@@ -111,7 +151,6 @@ DevMat dev_multiply(const DevMat& A, const DevMat& B, hipStream_t s, int64_t* ti
 DevMat dev_upload(const Mat& M, hipStream_t s);
 Mat dev_download(const DevMat& M, hipStream_t s);
 DevMat dev_prune(DevMat M, hipStream_t s);
-
 // CPU engine (cpu_engine.cpp, OpenMP).
 Mat cpu_multiply(const Mat& A, const Mat& B, int nthreads, int64_t* tile_pairs);
 Mat cpu_prune(Mat M);

@@ -105,6 +105,24 @@ def test_a4_gpu_matches_golden(tmp_path, a4_bin, n, p, comm):
 
 
 @pytest.mark.gpu
+def test_a4_gpu_concurrent_levels_match_python_engine(tmp_path, a4_bin):
+    """Dense-filling chain: four concurrent level-0 products on the stream pool,
+    loader uploads in flight, stream-ordered buffers freed across streams;
+    output must equal the in-process GPU engine (same P=1 association)."""
+    import torch
+
+    from spmm_amd.models.chain import chain_product
+
+    mats = gen.random_chain(8, 40, 32, 0.2, "full", seed=21)
+    folder = str(tmp_path / "in")
+    refio.write_folder(folder, mats, 32)
+    _run(a4_bin, 1, folder, "--device", "hip", "--out", str(tmp_path / "g"), "--quiet", "--streams", "4")
+    want = chain_product([m.to(torch.device("cuda", 0)) for m in mats])
+    refio.write_matrix(str(tmp_path / "p"), want)
+    assert open(tmp_path / "g").read() == open(tmp_path / "p").read()
+
+
+@pytest.mark.gpu
 def test_a4_gpu_k32_matches_cpu_engine(tmp_path, a4_bin):
     mats = gen.random_chain(6, 8, 32, 0.4, "full", seed=9)
     folder = str(tmp_path / "in")
