@@ -11,12 +11,13 @@
 //
 // Reader: mmap + parallel two-pass tokenizer (textio.hpp), values parsed
 // straight into caller-provided (typically pinned) buffers so the device
-// upload can start without another host copy.  Writer: tiles are formatted by
-// all threads into private buffers, then written with pwrite at prefix-summed
-// offsets.
+// upload can start without another host copy; 8 digits per step (SWAR).
+// Writer: a sizing pass gives every thread its exact byte range, then all
+// threads format straight into a shared mapping of the output file.
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <charconv>
 #include <cstdio>
 #include <cstring>
@@ -78,19 +79,28 @@ SPMM_HOST_EXPORT int spmm_ref_fill(void* handle, int32_t* keys, uint64_t* vals, 
   const int64_t kk = (int64_t)h->k * h->k;
   const int64_t per = 2 + kk;
   const int64_t need = h->blocks * per;
-  const int64_t ntok = parallel_tokens(
-      h->f.data, h->body, h->f.size, nthreads,
-      [&](int64_t g, const char* p, const char* end) {
-        if (g >= need) return;   // trailing tokens are ignored, as `>>` would never read them
-        const int64_t b = g / per, o = g % per;
-        if (o < 2) {
-          int64_t x;
-          parse_i64(p, end, &x);
-          keys[2 * b + o] = (int32_t)x;
-        } else {
-          parse_u64(p, end, &vals[b * kk + (o - 2)]);
-        }
-      });
+  // Per-thread position in the block stream: block b, token o of the block
+  // (0, 1 = tile key, 2.. = values).
+  struct Cursor {
+    int32_t* keys;
+    uint64_t* vals;
+    int64_t kk, per, blocks, b = 0, o = 0;
+    void seek(int64_t g) { b = g / per; o = g % per; }
+    const char* token(const char* p, const char* end) {
+      if (b >= blocks) return p;   // trailing tokens are ignored, as `>>` would never read them
+      if (o < 2) {
+        int64_t x;
+        p = parse_i64(p, end, &x);
+        keys[2 * b + o] = (int32_t)x;
+      } else {
+        p = parse_u64_fast(p, end, &vals[b * kk + (o - 2)]);
+      }
+      if (++o == per) { o = 0; ++b; }
+      return p;
+    }
+  };
+  const int64_t ntok = parallel_scan(h->f.data, h->body, h->f.size, nthreads,
+                                     Cursor{keys, vals, kk, per, h->blocks});
   if (ntok < need) {
     set_err(err, errlen, "file has " + std::to_string(ntok) + " block tokens, expected " +
                              std::to_string(need));
@@ -101,11 +111,97 @@ SPMM_HOST_EXPORT int spmm_ref_fill(void* handle, int32_t* keys, uint64_t* vals, 
 
 SPMM_HOST_EXPORT void spmm_ref_close(void* handle) { delete (RefHandle*)handle; }
 
-// Writes the reference output layout.  keys/vals must already be sorted and
-// pruned by the caller.  Returns 0 or -errno.
+namespace {
+
+// Decimal digits of v (1..20): bit length -> estimate, one table compare.
+inline int u64_digits(uint64_t v) {
+  static const uint64_t p10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                   100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
+                                   1000000000000ull, 10000000000000ull, 100000000000000ull,
+                                   1000000000000000ull, 10000000000000000ull, 100000000000000000ull,
+                                   1000000000000000000ull, 10000000000000000000ull};
+  const int bits = 64 - __builtin_clzll(v | 1);   // 1..64
+  const int t = (bits * 1233) >> 12;              // 0..19, digits are t or t + 1
+  return t + (v >= p10[t] ? 1 : 0) + (v == 0 ? 1 : 0);
+}
+
+inline int i32_len(int32_t x) {
+  char b[16];
+  return (int)(std::to_chars(b, b + 16, x).ptr - b);
+}
+
+// Bytes of tile b in the output layout: "r c\n" + k lines of k values.
+inline int64_t tile_bytes(const int32_t* keys, const uint64_t* v, int64_t kk, int64_t b) {
+  int64_t n = i32_len(keys[2 * b]) + 1 + i32_len(keys[2 * b + 1]) + 1;
+  for (int64_t e = 0; e < kk; ++e) n += u64_digits(v[b * kk + e]) + 1;   // value + ' ' or '\n'
+  return n;
+}
+
+}  // namespace
+
+SPMM_HOST_EXPORT int spmm_ref_write_buffered(const char* path, int64_t R, int64_t C, int64_t nb,
+                                             const int32_t* keys, const uint64_t* vals, int k, int nthreads);
+
+// Writes the reference output layout with every thread formatting straight
+// into a shared mapping of the output file: a sizing pass gives each thread's
+// exact byte range, so there is no intermediate buffer and no serialised
+// write(2).  Returns 0 or -errno.
 SPMM_HOST_EXPORT int spmm_ref_write(const char* path, int64_t R, int64_t C, int64_t nb,
                                     const int32_t* keys, const uint64_t* vals, int k,
                                     int nthreads) {
+  const int64_t kk = (int64_t)k * k;
+  int T = nthreads > 0 ? nthreads : omp_get_max_threads();
+  if (nb < 64) T = 1;
+  char head[64];
+  const int hl = std::snprintf(head, sizeof head, "%lld %lld\n%lld\n", (long long)R, (long long)C, (long long)nb);
+  std::vector<int64_t> off((size_t)T + 1, 0);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t b0 = nb * t / T, b1 = nb * (t + 1) / T;
+    int64_t n = 0;
+    for (int64_t b = b0; b < b1; ++b) n += tile_bytes(keys, vals, kk, b);
+    off[(size_t)t + 1] = n;
+  }
+  off[0] = hl;
+  for (int t = 0; t < T; ++t) off[(size_t)t + 1] += off[(size_t)t];
+  const int64_t total = off[(size_t)T];
+
+  int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return -errno;
+  if (::ftruncate(fd, (off_t)total) != 0) { const int e = errno; ::close(fd); return -e; }
+  void* map = mmap(nullptr, (size_t)total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (map == MAP_FAILED) { ::close(fd); return spmm_ref_write_buffered(path, R, C, nb, keys, vals, k, nthreads); }
+  char* out = static_cast<char*>(map);
+  std::memcpy(out, head, (size_t)hl);
+  int bad = 0;
+#pragma omp parallel num_threads(T) reduction(| : bad)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t b0 = nb * t / T, b1 = nb * (t + 1) / T;
+    char* o = out + off[(size_t)t];
+    char* lim = out + off[(size_t)t + 1];
+    for (int64_t b = b0; b < b1; ++b) {
+      o = std::to_chars(o, lim, keys[2 * b]).ptr; *o++ = ' ';
+      o = std::to_chars(o, lim, keys[2 * b + 1]).ptr; *o++ = '\n';
+      const uint64_t* v = vals + b * kk;
+      for (int r = 0; r < k; ++r)
+        for (int c = 0; c < k; ++c) {
+          o = std::to_chars(o, lim, v[r * k + c]).ptr;
+          *o++ = (c + 1 < k) ? ' ' : '\n';
+        }
+    }
+    bad |= (o != lim);
+  }
+  int rc = bad ? -EIO : 0;
+  if (munmap(map, (size_t)total) != 0 && rc == 0) rc = -errno;
+  if (::close(fd) != 0 && rc == 0) rc = -EIO;
+  return rc;
+}
+
+// Buffered fallback (filesystems that cannot map the output).
+SPMM_HOST_EXPORT int spmm_ref_write_buffered(const char* path, int64_t R, int64_t C, int64_t nb,
+                                             const int32_t* keys, const uint64_t* vals, int k, int nthreads) {
   const int64_t kk = (int64_t)k * k;
   int T = nthreads > 0 ? nthreads : omp_get_max_threads();
   if (nb < 64) T = 1;

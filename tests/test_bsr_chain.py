@@ -155,6 +155,28 @@ def test_refio_large_file_parallel_parse(tmp_path):
     assert torch.equal(R.keys, M.keys) and torch.equal(R.vals, M.vals)
 
 
+def test_refio_writer_digit_boundaries_and_swar_parser(tmp_path):
+    """Every decimal length 1..20 (incl. 0, 10^n - 1, 10^n, 2^64 - 1) through the
+    multi-threaded mapped writer (sizing pass) and the 8-digit SWAR parser."""
+    k = 6
+    edge = [0, 2 ** 64 - 1, 2 ** 63, 2 ** 63 - 1]
+    for n in range(1, 20):
+        edge += [10 ** n - 1, 10 ** n, 10 ** n + 1]
+    edge += [10 ** 19, 10 ** 19 - 1, 18446744073709551614]
+    rng = np.random.default_rng(4)
+    nb = 300
+    vals = rng.choice(np.array(edge, dtype=np.uint64), size=(nb, k, k))
+    keys = np.stack(np.divmod(np.arange(nb), 20), 1).astype(np.int32) * k
+    keys[::7, 1] *= -1                       # negative tile coordinates print with '-'
+    M = B.BSR(120 * k, 20 * k, k, *B.canonicalize(torch.from_numpy(keys), torch.from_numpy(vals.view(np.int64))))
+    p = str(tmp_path / "m")
+    refio.write_matrix(p, M, nthreads=5)
+    with open(p) as f:
+        assert f.read() == golden.to_text(golden.from_bsr(M))
+    R = refio.read_matrix(p, k, nthreads=3)
+    assert torch.equal(R.keys, M.keys) and torch.equal(R.vals, M.vals)
+
+
 def test_refio_short_file_errors(tmp_path):
     p = tmp_path / "m"
     p.write_text("2 2\n1\n0 0\n1 2 3\n")
