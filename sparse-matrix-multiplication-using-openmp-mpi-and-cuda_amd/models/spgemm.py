@@ -76,9 +76,44 @@ def gather_rows(panel: CSR, comm: Comm, dst: int = 0) -> Optional[CSR]:
     return full if comm.rank == dst else None
 
 
+def allgather_operand(panel: CSR, comm: Comm) -> CSR:
+    """Right operand of the row-block SpGEMM: every rank's B row panel, with ONE
+    collective of the payload (instead of one per array).
+
+    Each rank packs [row counts (int64 as 2 x int32) | columns | value bits]
+    into one int32 buffer of a common size S; a single ``all_gather_into_tensor``
+    (ring over the xGMI links) replicates it, then the panels' columns and
+    values are packed back-to-back (two device copies, ~0.4 ms for the 1M
+    config's 0.9 GB against a multi-ms collective) so row r ends where row r+1
+    starts, as every CSR consumer expects.
+    """
+    if not comm.is_dist:
+        return panel
+    wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
+    meta = _allgather_equal(comm, torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)).view(-1, 2)
+    ms, nnzs = meta[:, 0].tolist(), meta[:, 1].tolist()
+    mmax, emax = max(ms), max(nnzs)
+    S = 2 * mmax + 2 * emax
+    buf = torch.zeros(S, dtype=torch.int32, device=wd)
+    buf[:2 * mmax].view(torch.int64)[:panel.m] = (panel.rowptr[1:] - panel.rowptr[:-1]).to(wd)
+    buf[2 * mmax:2 * mmax + panel.nnz] = panel.col.to(wd)
+    buf[2 * mmax + emax:2 * mmax + emax + panel.nnz] = panel.val.float().to(wd).view(torch.int32)
+    G = _allgather_equal(comm, buf).to(panel.device)
+    Gv = G.view(comm.world, S)
+    cnt = Gv[:, :2 * mmax].contiguous().view(torch.int64)          # [world, mmax]
+    W = range(comm.world)
+    counts = cnt.reshape(-1) if all(x == mmax for x in ms) else torch.cat([cnt[r, :ms[r]] for r in W])
+    col = torch.cat([Gv[r, 2 * mmax:2 * mmax + nnzs[r]] for r in W])
+    val = torch.cat([Gv[r, 2 * mmax + emax:2 * mmax + emax + nnzs[r]] for r in W]).view(torch.float32)
+    m = sum(ms)
+    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=G.device)
+    torch.cumsum(counts, 0, out=rowptr[1:])
+    return CSR(m, panel.n, rowptr, col, val)
+
+
 def rowblock_spgemm(A_panel: CSR, B_panel: CSR, comm: Comm, info: Optional[SpgemmInfo] = None) -> CSR:
     """C_panel = A_panel . B, where B = rows of every rank's B_panel."""
-    B = allgather_csr_rows(B_panel, comm)
+    B = allgather_operand(B_panel, comm)
     return spgemm(A_panel, B, info)
 
 
