@@ -10,7 +10,8 @@
 //   stream while the engine already multiplies level 0 -> pairwise tree of the
 //   reference's shape (helper2, :287-327; products of one level run
 //   concurrently on a pool of HIP streams) -> binomial tree across ranks over
-//   RCCL (the reference funnels everything to rank 0 with MPI, :466-571) ->
+//   RCCL, every product of a tree step row-panel split over the ranks of its
+//   group (the reference funnels everything to rank 0 with MPI, :466-571) ->
 //   zero-tile prune -> ./matrix in the reference's byte format.
 // stdout: "multiplying i i+1" per product and "time taken X seconds" on every
 // rank, as the reference prints them.
@@ -27,6 +28,7 @@
 //   --save-partials DIR   write this rank's partial product (checkpoint)
 //   --load-partials DIR   resume from saved partials, skipping load + local tree
 //   --timeout S           RCCL transfer timeout (fail fast, default 600)
+//   --no-split            cross-rank products on one rank each (no row-panel split)
 #include <mpi.h>
 #include <sys/stat.h>
 
@@ -54,7 +56,7 @@ namespace {
 struct Options {
   std::string folder, out = "matrix", device = "auto", comm = "auto", metrics, save_dir, load_dir;
   int threads = 0, streams = 4;
-  bool quiet = false, dump = false;
+  bool quiet = false, dump = false, split = true;
   double timeout = 600.0;
 };
 
@@ -62,7 +64,7 @@ struct Options {
   std::cerr << "a4: " << why << "\n"
             << "usage: a4 <folder> [--out PATH] [--device auto|hip|cpu] [--comm auto|rccl|mpi] [--threads N]\n"
                "          [--streams N] [--quiet] [--dump] [--metrics-json PATH] [--save-partials DIR]\n"
-               "          [--load-partials DIR] [--timeout S]\n";
+               "          [--load-partials DIR] [--timeout S] [--no-split]\n";
   std::exit(2);
 }
 
@@ -80,6 +82,7 @@ Options parse_args(int argc, char** argv) {
     else if (a == "--threads") o.threads = std::atoi(val().c_str());
     else if (a == "--streams") o.streams = std::max(1, std::atoi(val().c_str()));
     else if (a == "--quiet") o.quiet = true;
+    else if (a == "--no-split") o.split = false;
     else if (a == "--dump") o.dump = true;
     else if (a == "--metrics-json") o.metrics = val();
     else if (a == "--save-partials") o.save_dir = val();
@@ -464,6 +467,171 @@ Mat cpu_reduce_local(const Options& o, int lo, int hi, int k, Stats& st) {
   return std::move(arr[0]);
 }
 
+// ---- cross-rank tree ---------------------------------------------------------
+// Engine adapters: the tree below is written once for the GPU engine (DevMat,
+// RCCL or host-staged MPI transport) and the CPU engine (Mat, MPI).
+struct GpuOps {
+  using M = DevMat;
+  hipStream_t s;
+  Comm* comm;
+  M mul(const M& a, const M& b, int64_t* pairs) { return dev_multiply(a, b, s, pairs); }
+  void send(const M& m, int dst) { comm->send_dev(m, dst, s); }
+  M recv(int src) { return comm->recv_dev(src, s); }
+  std::vector<int32_t> keys(const M& m) {
+    std::vector<int32_t> h((size_t)m.nb * 2);
+    if (m.nb) A4_HIP(hipMemcpyAsync(h.data(), m.keys.get(), h.size() * 4, hipMemcpyDeviceToHost, s));
+    A4_HIP(hipStreamSynchronize(s));
+    return h;
+  }
+  M slice(const M& m, int64_t t0, int64_t t1) {
+    const int64_t n = t1 - t0, kk = (int64_t)m.k * m.k;
+    M p;
+    p.rows = m.rows; p.cols = m.cols; p.k = m.k; p.nb = n;
+    p.keys = DevBuf<int32_t>((size_t)n * 2, s);
+    p.vals = DevBuf<uint64_t>((size_t)(n * kk), s);
+    if (n) {
+      A4_HIP(hipMemcpyAsync(p.keys.get(), m.keys.get() + 2 * t0, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
+      A4_HIP(hipMemcpyAsync(p.vals.get(), m.vals.get() + t0 * kk, (size_t)(n * kk) * 8, hipMemcpyDeviceToDevice, s));
+    }
+    return p;
+  }
+  M concat(std::vector<M>& parts) {
+    M c;
+    c.rows = parts[0].rows; c.cols = parts[0].cols; c.k = parts[0].k; c.nb = 0;
+    for (auto& p : parts) c.nb += p.nb;
+    const int64_t kk = (int64_t)c.k * c.k;
+    c.keys = DevBuf<int32_t>((size_t)c.nb * 2, s);
+    c.vals = DevBuf<uint64_t>((size_t)(c.nb * kk), s);
+    int64_t at = 0;
+    for (auto& p : parts) {
+      if (p.nb) {
+        A4_HIP(hipMemcpyAsync(c.keys.get() + 2 * at, p.keys.get(), (size_t)p.nb * 8, hipMemcpyDeviceToDevice, s));
+        A4_HIP(hipMemcpyAsync(c.vals.get() + at * kk, p.vals.get(), (size_t)(p.nb * kk) * 8, hipMemcpyDeviceToDevice,
+                              s));
+      }
+      at += p.nb;
+    }
+    return c;
+  }
+};
+
+struct CpuOps {
+  using M = Mat;
+  Comm* comm;
+  int threads;
+  M mul(const M& a, const M& b, int64_t* pairs) { return cpu_multiply(a, b, threads, pairs); }
+  void send(const M& m, int dst) { comm->send_host(m, dst); }
+  M recv(int src) { return comm->recv_host(src); }
+  std::vector<int32_t> keys(const M& m) { return m.keys; }
+  M slice(const M& m, int64_t t0, int64_t t1) {
+    const int64_t kk = (int64_t)m.k * m.k;
+    M p;
+    p.rows = m.rows; p.cols = m.cols; p.k = m.k;
+    p.keys.assign(m.keys.begin() + 2 * t0, m.keys.begin() + 2 * t1);
+    p.vals.assign(m.vals.begin() + t0 * kk, m.vals.begin() + t1 * kk);
+    return p;
+  }
+  M concat(std::vector<M>& parts) {
+    M c;
+    c.rows = parts[0].rows; c.cols = parts[0].cols; c.k = parts[0].k;
+    for (auto& p : parts) {
+      c.keys.insert(c.keys.end(), p.keys.begin(), p.keys.end());
+      c.vals.insert(c.vals.end(), p.vals.begin(), p.vals.end());
+    }
+    return c;
+  }
+};
+
+// np + 1 tile offsets cutting sorted tiles into np panels of whole tile rows,
+// balanced by tile count (an output tile (i, c) depends on tile row i of the
+// left operand only, so whole rows keep every output tile on one rank).
+std::vector<int64_t> row_cuts(const std::vector<int32_t>& keys, int np) {
+  const int64_t nb = (int64_t)keys.size() / 2;
+  std::vector<int64_t> cut((size_t)np + 1, nb);
+  cut[0] = 0;
+  for (int i = 1; i < np; ++i) {
+    int64_t t = std::max(cut[(size_t)i - 1], nb * i / np);
+    while (t > 0 && t < nb && keys[2 * t] == keys[2 * t - 2]) ++t;   // forward to a row boundary
+    cut[(size_t)i] = t;
+  }
+  return cut;
+}
+
+// Binomial tree over the ranks' partials, the reference's final helper2 over
+// the P partials (sparse_matrix_mult.cu:569-571) with its association: at step
+// s the partial of rank g0 (g0 % 2s == 0) is multiplied by rank g0+s's.  The
+// reference gathers every partial to rank 0 and multiplies there while P-1
+// GPUs idle; here, with `split`, every product of a step is computed by all
+// 2s ranks of its group [g0, g0+2s), which would otherwise be idle from this
+// step on: g0 cuts its partial L into row panels and sends one to each member,
+// g0+s sends its partial R to every member, each member returns L_i . R, and
+// g0 concatenates (panels are disjoint tile-row ranges in order, so the result
+// is the sorted product, bit-identical to the unsplit one).  Message order
+// (everyone first receives its L panel, then R) is deadlock-free with
+// blocking point-to-point transports.
+template <class Ops>
+std::optional<typename Ops::M> cross_rank_tree(Ops& ops, std::optional<typename Ops::M> part, int rank, int world,
+                                               bool split, const Options& o, Stats& st) {
+  using M = typename Ops::M;
+  auto count = [&](int64_t pairs) {
+    std::lock_guard<std::mutex> g(st.mu);
+    st.products += 1;
+    st.tile_pairs += pairs;
+  };
+  for (int step = 1; step < world; step *= 2) {
+    const int g0 = rank - rank % (2 * step), partner = g0 + step;
+    if (partner >= world) continue;   // no product in this group at this step
+    Range rstep("cross-rank step " + std::to_string(step));
+    const int gend = std::min(world, g0 + 2 * step);
+    int64_t pairs = 0;
+    if (!split || gend - g0 < 2) {
+      if (rank == g0) {
+        M other = ops.recv(partner);
+        say(o, "multiplying " + std::to_string(g0 / step) + " " + std::to_string(g0 / step + 1));
+        part = ops.mul(*part, other, &pairs);
+        count(pairs);
+      } else if (rank == partner) {
+        ops.send(*part, g0);
+        part.reset();
+      }
+      continue;
+    }
+    const int np = gend - g0;
+    if (rank == g0) {
+      say(o, "multiplying " + std::to_string(g0 / step) + " " + std::to_string(g0 / step + 1));
+      const std::vector<int64_t> cut = row_cuts(ops.keys(*part), np);
+      for (int i = 1; i < np; ++i) ops.send(ops.slice(*part, cut[(size_t)i], cut[(size_t)i + 1]), g0 + i);
+      M R = ops.recv(partner);
+      std::vector<M> C;
+      {
+        M L0 = ops.slice(*part, cut[0], cut[1]);
+        part.reset();
+        C.push_back(ops.mul(L0, R, &pairs));
+        count(pairs);
+      }
+      for (int i = 1; i < np; ++i) C.push_back(ops.recv(g0 + i));
+      part = ops.concat(C);
+    } else if (rank < gend) {
+      M Li = ops.recv(g0);
+      if (rank == partner) {
+        for (int h = g0 + 1; h < gend; ++h)
+          if (h != partner) ops.send(*part, h);
+        ops.send(*part, g0);
+        M Ci = ops.mul(Li, *part, &pairs);
+        part.reset();
+        count(pairs);
+        ops.send(Ci, g0);
+      } else {
+        M R = ops.recv(partner);
+        M Ci = ops.mul(Li, R, &pairs);
+        count(pairs);
+        ops.send(Ci, g0);
+      }
+    }
+  }
+  return part;
+}
+
 int local_rank() {
   for (const char* v : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "SLURM_LOCALID"}) {
     const char* x = std::getenv(v);
@@ -543,41 +711,20 @@ int run(const Options& o, int rank, int world, double t_start) {
   // binomial tree across ranks: at step s rank r (r % 2s == 0) multiplies its
   // partial by rank r+s's (the reference's final helper2 over partials, :571)
   const double t1 = now_s();
-  bool alive = true;
+  std::optional<DevMat> gm;   // the GPU partial as a plain matrix on the main stream
+  if (gpart) {
+    A4_HIP(hipStreamWaitEvent(s, gpart->ev, 0));
+    gm = std::move(*gpart->m);
+    (void)hipEventDestroy(gpart->ev);
+    gpart.reset();
+  }
   if (N / world != 0 && world > 1) {
-    for (int step = 1; step < world && alive; step *= 2) {
-      Range rstep("cross-rank step " + std::to_string(step));
-      if (rank % (2 * step) == 0) {
-        if (rank + step < world) {
-          if (gpu) {
-            A4_HIP(hipStreamWaitEvent(s, gpart->ev, 0));
-            DevMat other = comm->recv_dev(rank + step, s);
-            say(o, "multiplying " + std::to_string(rank / step) + " " + std::to_string(rank / step + 1));
-            int64_t pairs = 0;
-            DevMat C = dev_multiply(*gpart->m, other, s, &pairs);
-            st.products += 1;
-            st.tile_pairs += pairs;
-            gpart->m->keys.retarget(s); gpart->m->vals.retarget(s);
-            (void)hipEventDestroy(gpart->ev);
-            gpart = make_node(std::move(C), s);
-          } else {
-            Mat other = comm->recv_host(rank + step);
-            say(o, "multiplying " + std::to_string(rank / step) + " " + std::to_string(rank / step + 1));
-            int64_t pairs = 0;
-            cpart = cpu_multiply(*cpart, other, o.threads, &pairs);
-            st.products += 1;
-            st.tile_pairs += pairs;
-          }
-        }
-      } else {
-        if (gpu) {
-          A4_HIP(hipStreamWaitEvent(s, gpart->ev, 0));
-          comm->send_dev(*gpart->m, rank - step, s);
-        } else {
-          comm->send_host(*cpart, rank - step);
-        }
-        alive = false;
-      }
+    if (gpu) {
+      GpuOps ops{s, comm.get()};
+      gm = cross_rank_tree(ops, std::move(gm), rank, world, o.split, o, st);
+    } else {
+      CpuOps ops{comm.get(), o.threads};
+      cpart = cross_rank_tree(ops, std::move(cpart), rank, world, o.split, o, st);
     }
   }
   if (gpu) A4_HIP(hipDeviceSynchronize());
@@ -588,8 +735,7 @@ int run(const Options& o, int rank, int world, double t_start) {
     const double t2 = now_s();
     Mat final_;
     if (gpu) {
-      A4_HIP(hipStreamWaitEvent(s, gpart->ev, 0));
-      final_ = dev_download(dev_prune(std::move(*gpart->m), s), s);
+      final_ = dev_download(dev_prune(std::move(*gm), s), s);
     } else {
       final_ = cpu_prune(std::move(*cpart));
     }
@@ -600,7 +746,7 @@ int run(const Options& o, int rank, int world, double t_start) {
       std::ofstream m(o.metrics);
       const double ops = (double)st.tile_pairs * 2.0 * k * k * k;
       m << "{\"engine\": \"native\", \"device\": \"" << (gpu ? "hip" : "cpu") << "\", \"comm\": \"" << comm->name()
-        << "\", \"ranks\": " << world << ", \"n\": " << N << ", \"k\": " << k << ", \"products\": " << st.products
+        << "\", \"ranks\": " << world << ", \"split\": " << (o.split ? "true" : "false") << ", \"n\": " << N << ", \"k\": " << k << ", \"products\": " << st.products
         << ", \"tile_pairs\": " << st.tile_pairs << ", \"int_ops\": " << ops << ", \"t_reduce_s\": " << st.t_reduce
         << ", \"t_comm_s\": " << st.t_comm << ", \"t_write_s\": " << st.t_write << ", \"bytes_h2d\": " << st.bytes_h2d
         << ", \"bytes_p2p\": " << (comm->bytes_sent + comm->bytes_recv) << ", \"reduce_gops\": "
@@ -608,6 +754,7 @@ int run(const Options& o, int rank, int world, double t_start) {
     }
   }
   gpart.reset();
+  gm.reset();
   comm->barrier();
   return 0;
 }

@@ -19,7 +19,8 @@ MI355X design:
   exact arithmetic), but every product runs on the GPU with no host round
   trip; independent products of one level overlap on separate HIP streams.
 * The cross-rank reduction is a distributed binomial tree over RCCL (see
-  :mod:`..parallel.comm`), so no single GPU funnels all partials.
+  :mod:`..parallel.comm`), so no single GPU funnels all partials, and each
+  tree product is row-panel split over the ranks its step leaves idle.
 """
 from __future__ import annotations
 
@@ -145,7 +146,7 @@ def _sync(dev: torch.device) -> None:
 
 
 def run_chain(folder: str, comm: Comm, out_path: Optional[str] = "matrix", log: Optional[Log] = print,
-              nthreads: int = 0, stats: Optional[ChainStats] = None) -> Optional[BSR]:
+              nthreads: int = 0, stats: Optional[ChainStats] = None, split: bool = True) -> Optional[BSR]:
     """The full reference pipeline on this rank.  Returns the final product on
     rank 0 (pruned), None elsewhere.  Writes ``out_path`` on rank 0 unless None."""
     stats = stats if stats is not None else ChainStats()
@@ -166,7 +167,7 @@ def run_chain(folder: str, comm: Comm, out_path: Optional[str] = "matrix", log: 
 
     if n // comm.world != 0 and comm.world > 1:
         t0 = time.perf_counter()
-        part = _binomial_reduce(part, comm, log, stats)
+        part = _binomial_reduce(part, comm, log, stats, split=split)
         _sync(dev)
         stats.t_comm += time.perf_counter() - t0
 
@@ -180,26 +181,85 @@ def run_chain(folder: str, comm: Comm, out_path: Optional[str] = "matrix", log: 
     return final
 
 
-def _binomial_reduce(part: BSR, comm: Comm, log: Optional[Log], stats: ChainStats) -> Optional[BSR]:
+def row_cuts(keys: torch.Tensor, parts: int) -> List[int]:
+    """parts + 1 tile offsets cutting sorted tiles into panels of whole tile
+    rows, balanced by tile count (output tile (i, c) only needs tile row i of
+    the left operand)."""
+    nb = int(keys.shape[0])
+    rows = keys[:, 0].tolist()
+    cut = [0]
+    for i in range(1, parts):
+        t = max(cut[-1], nb * i // parts)
+        while 0 < t < nb and rows[t] == rows[t - 1]:
+            t += 1
+        cut.append(t)
+    cut.append(nb)
+    return cut
+
+
+def _slice(M: BSR, t0: int, t1: int) -> BSR:
+    return BSR(M.rows, M.cols, M.k, M.keys[t0:t1].contiguous(), M.vals[t0:t1].contiguous())
+
+
+def _binomial_reduce(part: Optional[BSR], comm: Comm, log: Optional[Log], stats: ChainStats,
+                     split: bool = True) -> Optional[BSR]:
     """Cross-rank tree with the shape of the reference's helper2 over the P
-    partials (:569-571): at step s, rank r (r % 2s == 0) multiplies its partial
-    by rank r+s's.  Printed indices are the reference's level-relative ones."""
+    partials (:569-571): at step s, the partial of rank g0 (g0 % 2s == 0) is
+    multiplied by rank g0+s's.  With ``split`` the product is shared by every
+    rank of the group [g0, g0 + 2s) (they would idle otherwise): g0 sends each
+    a row panel of its partial, g0+s sends its partial to all, each returns its
+    panel of the product and g0 concatenates the panels (disjoint tile-row
+    ranges in order: the same bytes as the unsplit product).  Every member
+    receives its panel before R, so blocking transports cannot deadlock.
+    Printed indices are the reference's level-relative ones."""
     r, p = comm.rank, comm.world
     s = 1
     while s < p:
-        if r % (2 * s) == 0:
-            if r + s < p:
-                other = comm.recv_bsr(r + s)
+        g0 = r - r % (2 * s)
+        partner = g0 + s
+        gend = min(p, g0 + 2 * s)
+        if partner >= p:
+            s *= 2
+            continue
+        if not split:
+            if r == g0:
+                other = comm.recv_bsr(partner)
                 stats.bytes_p2p += other.nbytes()
                 if log:
-                    log(f"multiplying {r // s} {r // s + 1}")
+                    log(f"multiplying {g0 // s} {g0 // s + 1}")
                 part = _mul(part, other, stats)
-        else:
-            comm.send_bsr(part, r - s)
-            stats.bytes_p2p += part.nbytes()
-            return None
+            elif r == partner:
+                comm.send_bsr(part, g0)
+                stats.bytes_p2p += part.nbytes()
+                part = None
+        elif r == g0:
+            if log:
+                log(f"multiplying {g0 // s} {g0 // s + 1}")
+            cut = row_cuts(part.keys, gend - g0)
+            for i in range(1, gend - g0):
+                piece = _slice(part, cut[i], cut[i + 1])
+                comm.send_bsr(piece, g0 + i)
+                stats.bytes_p2p += piece.nbytes()
+            R = comm.recv_bsr(partner)
+            panels = [_mul(_slice(part, cut[0], cut[1]), R, stats)]
+            panels += [comm.recv_bsr(g0 + i) for i in range(1, gend - g0)]
+            part = BSR(panels[0].rows, panels[0].cols, part.k, torch.cat([q.keys for q in panels]),
+                       torch.cat([q.vals for q in panels]))
+        elif r < gend:
+            L = comm.recv_bsr(g0)
+            if r == partner:
+                for h in list(range(g0 + 1, gend)) + [g0]:
+                    if h != partner:
+                        comm.send_bsr(part, h)
+                        stats.bytes_p2p += part.nbytes()
+                R, part = part, None
+            else:
+                R = comm.recv_bsr(partner)
+            C = _mul(L, R, stats)
+            comm.send_bsr(C, g0)
+            stats.bytes_p2p += C.nbytes()
         s *= 2
-    return part
+    return part if r == 0 else None
 
 
 def chain_product(mats: List[BSR], log: Optional[Log] = None) -> BSR:

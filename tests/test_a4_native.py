@@ -57,6 +57,22 @@ def test_a4_cpu_matches_golden(tmp_path, a4_bin, n, p):
     assert len(re.findall(r"time taken [0-9.e+-]+ seconds", r.stdout)) == p
 
 
+@pytest.mark.parametrize("n,p", [(9, 4), (12, 3), (16, 8)])
+def test_a4_cpu_row_panel_split_matches_unsplit(tmp_path, a4_bin, n, p):
+    """Cross-rank products split by row panels over the idle ranks of each tree
+    group give the same bytes as one rank per product (and the golden model)."""
+    mats, folder = _chain(tmp_path, n, blocks=7, seed=100 + n)
+    outs = []
+    for flag in ([], ["--no-split"]):
+        out = str(tmp_path / f"matrix{len(outs)}")
+        met = str(tmp_path / f"m{len(outs)}.json")
+        r = _run(a4_bin, p, folder, "--device", "cpu", "--out", out, "--threads", "1", "--metrics-json", met, *flag)
+        assert len(re.findall(r"multiplying \d+ \d+", r.stdout)) == n - 1
+        outs.append(open(out).read())
+        assert json.load(open(met))["split"] == (not flag)
+    assert outs[0] == outs[1] == golden.to_text(golden.chain([golden.from_bsr(m) for m in mats], p=p))
+
+
 def test_a4_missing_size_file(tmp_path, a4_bin):
     r = _run(a4_bin, 1, str(tmp_path / "nowhere"), "--device", "cpu", check=False)
     assert r.returncode != 0
