@@ -7,8 +7,9 @@ ranks (sparse_matrix_mult.cu:437-456) and funnels partials to rank 0
 
 * rank r owns row panel r of A and of B (contiguous rows, chunk-aligned so the
   synthetic matrices do not depend on P);
-* B's row panels are all-gathered (one ``all_gather_into_tensor`` per array,
-  ring over the xGMI links — B is ~0.8 GB for the 1M config, small against
+* B's row panels are all-gathered (row counts first, then columns + values in
+  one packed ``all_gather_into_tensor`` over the xGMI ring that overlaps the
+  local product counting — B is ~0.9 GB for the 1M config, small against
   288 GB of HBM, so replicating it is the right trade);
 * each rank computes its C row panel = A_panel . B with the local gfx950
   SpGEMM; C stays distributed (no reduce needed: rows are disjoint).
@@ -18,7 +19,7 @@ ranks (sparse_matrix_mult.cu:437-456) and funnels partials to rank 0
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Tuple
+from typing import Callable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -76,45 +77,86 @@ def gather_rows(panel: CSR, comm: Comm, dst: int = 0) -> Optional[CSR]:
     return full if comm.rank == dst else None
 
 
-def allgather_operand(panel: CSR, comm: Comm) -> CSR:
-    """Right operand of the row-block SpGEMM: every rank's B row panel, with ONE
-    collective of the payload (instead of one per array).
+def _allgather_async(comm: Comm, t: torch.Tensor):
+    """Start an all-gather of equally sized 1-D tensors; returns a function that
+    waits for it and yields the [world * t.numel()] result (rank order)."""
+    if comm.backend == "nccl":
+        out = torch.empty(comm.world * t.numel(), dtype=t.dtype, device=t.device)
+        work = dist.all_gather_into_tensor(out, t.contiguous(), async_op=True)
 
-    Each rank packs [row counts (int64 as 2 x int32) | columns | value bits]
-    into one int32 buffer of a common size S; a single ``all_gather_into_tensor``
-    (ring over the xGMI links) replicates it, then the panels' columns and
-    values are packed back-to-back (two device copies, ~0.4 ms for the 1M
-    config's 0.9 GB against a multi-ms collective) so row r ends where row r+1
-    starts, as every CSR consumer expects.
+        def finish():
+            work.wait()   # the current stream waits; the host does not
+            return out
+        return finish
+    parts = [torch.empty_like(t) for _ in range(comm.world)]
+    work = dist.all_gather(parts, t.contiguous(), async_op=True)
+
+    def finish_gloo():
+        work.wait()
+        return torch.cat(parts)
+    return finish_gloo
+
+
+def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], CSR]]:
+    """Right operand of the row-block SpGEMM (every rank's B row panel), in two
+    stages so the gather overlaps the SpGEMM's setup.
+
+    1. sizes, then the row counts of every panel (small collectives): B's row
+       pointer is complete, which is all the product-count / binning / memory
+       planning phase of ``spgemm`` reads;
+    2. columns and values of every panel in ONE packed collective (each rank
+       contributes [cols | value bits] as int32 of a common size), started
+       asynchronously: RCCL moves the ~0.9 GB of the 1M config over the xGMI
+       ring while the compute stream runs the per-row product counts.
+
+    Returns (B with row pointer only, ready) where ``ready()`` makes the
+    current stream wait for the payload and returns the full CSR (panels'
+    columns and values packed back-to-back: two device copies, ~0.4 ms).
     """
     if not comm.is_dist:
-        return panel
+        return panel, lambda: panel
     wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
     meta = _allgather_equal(comm, torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)).view(-1, 2)
     ms, nnzs = meta[:, 0].tolist(), meta[:, 1].tolist()
     mmax, emax = max(ms), max(nnzs)
-    S = 2 * mmax + 2 * emax
-    buf = torch.zeros(S, dtype=torch.int32, device=wd)
-    buf[:2 * mmax].view(torch.int64)[:panel.m] = (panel.rowptr[1:] - panel.rowptr[:-1]).to(wd)
-    buf[2 * mmax:2 * mmax + panel.nnz] = panel.col.to(wd)
-    buf[2 * mmax + emax:2 * mmax + emax + panel.nnz] = panel.val.float().to(wd).view(torch.int32)
-    G = _allgather_equal(comm, buf).to(panel.device)
-    Gv = G.view(comm.world, S)
-    cnt = Gv[:, :2 * mmax].contiguous().view(torch.int64)          # [world, mmax]
     W = range(comm.world)
+    cbuf = torch.zeros(mmax, dtype=torch.int64, device=wd)
+    cbuf[:panel.m] = (panel.rowptr[1:] - panel.rowptr[:-1]).to(wd)
+    buf = torch.zeros(2 * emax, dtype=torch.int32, device=wd)
+    buf[:panel.nnz] = panel.col.to(wd)
+    buf[emax:emax + panel.nnz] = panel.val.float().to(wd).view(torch.int32)
+    # counts first: collectives of one group run in issue order, so the small
+    # one must not queue behind the payload
+    cnt = _allgather_equal(comm, cbuf).to(panel.device).view(comm.world, mmax)
+    payload = _allgather_async(comm, buf)
     counts = cnt.reshape(-1) if all(x == mmax for x in ms) else torch.cat([cnt[r, :ms[r]] for r in W])
-    col = torch.cat([Gv[r, 2 * mmax:2 * mmax + nnzs[r]] for r in W])
-    val = torch.cat([Gv[r, 2 * mmax + emax:2 * mmax + emax + nnzs[r]] for r in W]).view(torch.float32)
     m = sum(ms)
-    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=G.device)
+    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=panel.device)
     torch.cumsum(counts, 0, out=rowptr[1:])
-    return CSR(m, panel.n, rowptr, col, val)
+    empty_c = torch.empty(0, dtype=torch.int32, device=panel.device)
+    meta_B = CSR(m, panel.n, rowptr, empty_c, torch.empty(0, dtype=torch.float32, device=panel.device))
+
+    def ready() -> CSR:
+        Gv = payload().to(panel.device).view(comm.world, 2 * emax)
+        col = torch.cat([Gv[r, :nnzs[r]] for r in W])
+        val = torch.cat([Gv[r, emax:emax + nnzs[r]] for r in W]).view(torch.float32)
+        return CSR(m, panel.n, rowptr, col, val)
+    return meta_B, ready
+
+
+def allgather_operand(panel: CSR, comm: Comm) -> CSR:
+    """Every rank's B row panel as one CSR (blocking form of
+    :func:`allgather_operand_async`)."""
+    _, ready = allgather_operand_async(panel, comm)
+    return ready()
 
 
 def rowblock_spgemm(A_panel: CSR, B_panel: CSR, comm: Comm, info: Optional[SpgemmInfo] = None) -> CSR:
-    """C_panel = A_panel . B, where B = rows of every rank's B_panel."""
-    B = allgather_operand(B_panel, comm)
-    return spgemm(A_panel, B, info)
+    """C_panel = A_panel . B, where B = rows of every rank's B_panel; the
+    payload of B's all-gather is in flight while the local product counts
+    and row binning run."""
+    B_meta, ready = allgather_operand_async(B_panel, comm)
+    return spgemm(A_panel, B_meta, info, B_ready=ready)
 
 
 @dataclass

@@ -208,26 +208,32 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         start = end
 
 
-def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None) -> CSR:
+def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> CSR:
+    """C = A . B.  ``B_ready``: B's columns / values are still in flight (a
+    distributed gather); ``B`` then only needs a valid row pointer, and
+    ``B_ready()`` is called for the complete operand right before the first
+    kernel that reads them (product counts and row binning overlap it)."""
     if A.n != B.m:
         raise ValueError(f"inner dimensions differ: {A.n} vs {B.m}")
     if A.device != B.device:
         raise ValueError("operands on different devices")
     info = info if info is not None else SpgemmInfo()
     if A.device.type != "cuda":
-        return _spgemm_cpu(A, B, info)
+        return _spgemm_cpu(A, B_ready() if B_ready is not None else B, info)
     A = A if A.val.dtype == torch.float32 else A.with_values(A.val.float())
     B = B if B.val.dtype == torch.float32 else B.with_values(B.val.float())
     nprod = row_nprod(A, B)
     info.flops = 2 * int(nprod.sum())
     info.mean_seg = info.flops / 2 / max(A.nnz, 1)
     if _onepass_fits(info.flops // 2, A.device):
-        return onepass(A, B, nprod, info)
+        return onepass(A, B, nprod, info, B_ready)
+    if B_ready is not None:
+        B = B_ready()
     row_nnz = symbolic(A, B, nprod, info)
     return numeric(A, B, row_nnz, info, nprod)
 
 
-def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> CSR:
+def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None) -> CSR:
     """Numeric without a symbolic phase: rows are binned by their product count
     and written at product-count offsets (an upper bound of their nnz), then
     compacted into the final CSR by one copy kernel.  Trades one extra pass
@@ -242,7 +248,8 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo) -> CSR:
     out_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
     flags = torch.zeros(m, dtype=torch.int32, device=dev)
     cap = nprod.to(torch.int32)
-    _run_bins(1, A, B, nprod, cap, ub, Uci, Uv, flags, info.rows_per_bin_num, info.mean_seg, out_nnz=out_nnz)
+    _run_bins(1, A, B, nprod, cap, ub, Uci, Uv, flags, info.rows_per_bin_num, info.mean_seg, out_nnz=out_nnz,
+              B_ready=B_ready)
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     torch.cumsum(out_nnz, 0, out=rowptr[1:])
     nnz = int(rowptr[-1])
@@ -298,7 +305,7 @@ def _splits(B: CSR) -> torch.Tensor:
 
 def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins,
               mean_seg: float = 0.0, out_nnz: Optional[torch.Tensor] = None,
-              nprod: Optional[torch.Tensor] = None):
+              nprod: Optional[torch.Tensor] = None, B_ready=None):
     """Run the LDS bins, then the HBM path for the rest.  Numeric: ``row_nnz`` is
     each row's capacity in the output (exact nnz, or the product count in
     one-pass mode where ``out_nnz`` receives the real counts)."""
@@ -308,6 +315,8 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
     stream = _native.stream_ptr(dev)
     sliced, glob = (NUM_SLICED, NUM_GLOBAL) if numeric else (SYM_SLICED, SYM_GLOBAL)
     order, groups = _group(_bins(counts, numeric), glob + 1)
+    if B_ready is not None:   # operand payload in flight until here (distributed gather)
+        B = B_ready()
     splits = None
     global_rows = []
     seg = mean_seg if mean_seg > 0 else B.nnz / max(B.m, 1)
