@@ -7,10 +7,14 @@ GPU path (gfx950, ``csrc/kernels/csr_spgemm.hip``):
      <= LOAD_SLICED); longer rows go to the HBM-workspace kernel.  Output:
      exact nnz per row.
   3. Row pointer by a device scan; C allocated once.
-  4. Numeric: rows re-binned by their exact nnz (128 .. 8192 slot tables,
-     8192 slots over 2/4/8 slices for long rows); ordered linear probing with
-     a monotone hash keeps every table sorted, so the output is a compaction
-     of the table, no sort pass.
+  4. Numeric: short rows in ordered-linear-probing LDS tables (a monotone
+     hash keeps every table sorted: the output is a compaction of the table),
+     long rows in the bucketed ESC kernel over 1/2/4/8 column slices, hub rows
+     through the HBM column-chunked path.
+  One-pass mode (default when memory allows) skips 2-3: rows are written at
+  product-count offsets and compacted ("plain"), or, when that staging does
+  not fit, processed in row chunks with two chunk-sized staging buffers and
+  the compaction overlapped on a side stream ("pipelined").
 CPU path: OpenMP Gustavson (``libspmm_host.so``), identical output layout.
 
 FLOPs are counted as 2 * sum(nprod) (one multiply + one add per intermediate
@@ -113,16 +117,26 @@ def row_nprod(A: CSR, B: CSR) -> torch.Tensor:
     return nprod
 
 
-def _onepass_fits(total_products: int, dev: torch.device) -> bool:
-    """One-pass mode needs a product-count-sized staging buffer next to C."""
+def _onepass_mode(total_products: int, dev: torch.device, allow_pipeline: bool = True) -> Optional[str]:
+    """"plain": a product-count-sized staging buffer next to C (fastest);
+    "pipelined": C at its product-count bound plus two chunk-sized staging
+    buffers (~half the memory, ~3 % slower: the overlapped compaction and
+    the numeric kernels compete for HBM); None: symbolic + numeric."""
     mode = CONFIG.spgemm_onepass
     if mode == "off":
-        return False
+        return None
+    pipe_ok = allow_pipeline and total_products >= PIPE_MIN_PRODUCTS and CONFIG.spgemm_pipeline != "off"
+    if CONFIG.spgemm_pipeline == "on" and pipe_ok:
+        return "pipelined"
     if mode == "on":
-        return True
+        return "plain"
     free, _ = torch.cuda.mem_get_info(dev)
     free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)   # the caching allocator's spare
-    return 2 * total_products * 8 <= 0.8 * free
+    if 2 * total_products * 8 <= 0.8 * free:
+        return "plain"
+    if pipe_ok and (total_products + 2 * PIPE_CHUNK_PRODUCTS) * 8 <= 0.8 * free:
+        return "pipelined"
+    return None
 
 
 _LONG = None
@@ -225,7 +239,23 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     nprod = row_nprod(A, B)
     info.flops = 2 * int(nprod.sum())
     info.mean_seg = info.flops / 2 / max(A.nnz, 1)
-    if _onepass_fits(info.flops // 2, A.device):
+    if B_ready is not None:
+        cached = []
+        fetch = B_ready
+
+        def B_ready():   # noqa: F811  (resolve the gathered operand once)
+            if not cached:
+                cached.append(fetch())
+            return cached[0]
+    mode = _onepass_mode(info.flops // 2, A.device)
+    if mode == "pipelined":
+        C_ = onepass_pipelined(A, B, nprod, info, B_ready)
+        if C_ is not None:
+            return C_
+        info.rows_per_bin_num = {}
+        if _onepass_mode(info.flops // 2, A.device, allow_pipeline=False) == "plain":   # long / spilled rows
+            mode = "plain"
+    if mode == "plain":
         return onepass(A, B, nprod, info, B_ready)
     if B_ready is not None:
         B = B_ready()
@@ -261,6 +291,107 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None)
                                                      _native.stream_ptr(dev)), "spgemm_compact")
     del Uci, Uv
     return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
+
+
+PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper
+PIPE_CHUNK_PRODUCTS = 1 << 29      # staging per chunk (x 8 B = 4 GiB), two chunks in flight
+_SIDE = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None) -> Optional[CSR]:
+    """One-pass numeric over contiguous row chunks with the compaction of chunk
+    i (a copy kernel, HBM-bandwidth bound) on a side stream while the numeric
+    kernels of chunk i+1 (LDS / latency bound, ~1.7 TB/s) run on the main one.
+
+    Each chunk stages its rows at chunk-relative product-count offsets in one
+    of two staging buffers (so staging is 2 x PIPE_CHUNK_PRODUCTS instead of
+    every product of the matrix); its row pointer segment is a device-side
+    cumsum carried from the previous chunk, so no host synchronisation sits
+    between chunks.  C is allocated at the product-count bound and returned as
+    a view of its first nnz entries.  Returns None (caller falls back to the
+    plain path) when a row needs the HBM long-row path or overflowed an LDS
+    bin, which this pipeline does not stage."""
+    dev = A.device
+    m = A.m
+    tot = info.flops // 2
+    bins = _bins(nprod, 1)
+    ub = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nprod, 0, out=ub[1:])
+    nch = max(2, -(-tot // PIPE_CHUNK_PRODUCTS))
+    cuts = torch.searchsorted(ub[1:], torch.arange(1, nch, device=dev, dtype=torch.int64) * (tot // nch))
+    bounds = [0] + sorted(set(min(max(int(c), 1), m - 1) for c in cuts.tolist())) + [m]
+    nch = len(bounds) - 1
+    bt = torch.tensor(bounds, dtype=torch.int64, device=dev)
+    chunk_of = torch.bucketize(torch.arange(m, device=dev), bt[1:-1], right=True)
+    key = chunk_of * 16 + (bins + 1)
+    order = torch.argsort(key, stable=True).to(torch.int32)
+    hist = torch.bincount(key, minlength=nch * 16).tolist()
+    ub_at = ub[bt].tolist()
+    if any(hist[c * 16 + NUM_GLOBAL + 1] for c in range(nch)):
+        return None
+    for c in range(nch):
+        for b in range(NUM_GLOBAL + 1):
+            if hist[c * 16 + b + 1]:
+                info.rows_per_bin_num[b] = info.rows_per_bin_num.get(b, 0) + hist[c * 16 + b + 1]
+    ub_rel = ub[:-1] - ub[bt[:-1]][chunk_of]          # staging offset of each row inside its chunk
+    cap = max(ub_at[i + 1] - ub_at[i] for i in range(nch))
+    stage = [(torch.empty(cap, dtype=torch.int32, device=dev), torch.empty(cap, dtype=torch.float32, device=dev))
+             for _ in range(2)]
+    Cci = torch.empty(tot, dtype=torch.int32, device=dev)
+    Cv = torch.empty(tot, dtype=torch.float32, device=dev)
+    out_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
+    flags = torch.zeros(m, dtype=torch.int32, device=dev)
+    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    rcap = nprod.to(torch.int32)
+    if B_ready is not None:
+        B = B_ready()
+    lib = _native.hip()
+    P = _native.ptr
+    splits = _splits(B) if any(hist[c * 16 + b + 1] for c in range(nch) for b in NUM_SLICED) else None
+    seg = info.mean_seg if info.mean_seg > 0 else B.nnz / max(B.m, 1)
+    sA = torch.cuda.current_stream(dev)
+    sB = _side_stream(dev)
+    sB.wait_stream(sA)
+    free = [None, None]
+    off = hist[0]
+    for c in range(nch):
+        lo, hi = bounds[c], bounds[c + 1]
+        sci, sv = stage[c % 2]
+        if free[c % 2] is not None:
+            sA.wait_event(free[c % 2])              # chunk c-2's compaction has read this buffer
+        for b in range(NUM_GLOBAL + 1):
+            cnt = hist[c * 16 + b + 1]
+            if cnt:
+                _native.check(lib.spmm_spgemm_lds(b, 1, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
+                                                  P(B.val), P(splits) if splits is not None else None,
+                                                  P(order) + 4 * off, cnt, B.n, _group_log2(seg / _slices(b, 1)),
+                                                  P(rcap), P(out_nnz), P(ub_rel), P(sci), P(sv), P(flags),
+                                                  sA.cuda_stream), "spgemm_lds(numeric, pipelined)")
+            off += cnt
+        off += hist[(c + 1) * 16] if c + 1 < nch else 0   # empty rows of the next chunk (bin -1)
+        done = torch.cuda.Event()
+        done.record(sA)
+        with torch.cuda.stream(sB):
+            sB.wait_event(done)
+            torch.cumsum(out_nnz[lo:hi], 0, dtype=torch.int64, out=rowptr[lo + 1:hi + 1])
+            rowptr[lo + 1:hi + 1] += rowptr[lo]
+            _native.check(lib.spmm_spgemm_compact(P(ub_rel) + 8 * lo, P(rowptr) + 8 * lo, hi - lo, P(sci), P(sv),
+                                                  P(Cci), P(Cv), sB.cuda_stream), "spgemm_compact(pipelined)")
+            free[c % 2] = torch.cuda.Event()
+            free[c % 2].record(sB)
+    sA.wait_stream(sB)
+    if bool(((flags & 2) != 0).any()):
+        return None
+    nnz = int(rowptr[-1])
+    info.nnz = nnz
+    return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)
 
 
 def _finish(C_: CSR, flags: torch.Tensor, info: SpgemmInfo) -> CSR:

@@ -32,6 +32,9 @@ class Config:
     # "auto" = when twice the product count fits in 80% of free memory
     spgemm_onepass: str = field(default_factory=lambda: _env("SPMM_SPGEMM_ONEPASS", "auto", str))
     spgemm_esc_min: int = field(default_factory=lambda: _env("SPMM_SPGEMM_ESC_MIN", 2048, int))
+    # one-pass over row chunks, compaction overlapped on a side stream: "auto" = when the plain
+    # one-pass does not fit in memory, "on" = whenever the product is large enough, "off"
+    spgemm_pipeline: str = field(default_factory=lambda: _env("SPMM_SPGEMM_PIPELINE", "auto", str))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

@@ -191,3 +191,33 @@ def test_spgemm_gpu_onepass_matches_two_phase(monkeypatch, m, k, n, d):
     assert torch.equal(C1.col, C2.col)
     assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
     check(C1.to("cpu"), A.to("cpu"), B.to("cpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["uniform", "rmat"])
+def test_spgemm_gpu_pipelined_onepass_matches_plain(monkeypatch, kind):
+    """Row-chunked one-pass with the compaction overlapped on a side stream
+    (forced to many small chunks) gives the same CSR as the plain one-pass;
+    a matrix with hub rows (HBM long-row path) falls back to the plain path."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    if kind == "uniform":
+        A = gen_csr.uniform_csr(40000, 40000, 2e-3, seed=31, device=dev)
+        B = gen_csr.uniform_csr(40000, 40000, 2e-3, seed=32, device=dev)
+    else:
+        A = gen_csr.rmat_csr(13, 16, seed=33, device=dev)
+        B = A.transpose()
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", "on")
+    monkeypatch.setattr(SG, "PIPE_MIN_PRODUCTS", 1 << 20)
+    monkeypatch.setattr(SG, "PIPE_CHUNK_PRODUCTS", 1 << 22)
+    monkeypatch.setattr(CONFIG, "spgemm_pipeline", "on")
+    C1 = SG.spgemm(A, B)
+    monkeypatch.setattr(CONFIG, "spgemm_pipeline", "off")
+    C2 = SG.spgemm(A, B)
+    assert torch.equal(C1.rowptr, C2.rowptr)
+    assert torch.equal(C1.col, C2.col)
+    assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    if kind == "uniform":
+        nz = C1.val.numel()
+        assert nz == int(C1.rowptr[-1])
