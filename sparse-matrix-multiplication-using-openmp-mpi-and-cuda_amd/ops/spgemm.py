@@ -194,7 +194,10 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         chunk_off = torch.cumsum(T, 1) - T
         row_tot = T.sum(1)
         row_base = torch.cumsum(row_tot, 0) - row_tot
-        Hc = torch.cumsum(H, 0) - H
+        # per-chunk running sum over workgroups; scanned along the inner
+        # dimension (torch's outer-dimension scan runs one thread per column:
+        # 480 ms per R-MAT step for this line before the transpose)
+        Hc = torch.cumsum(H.t().contiguous(), 1).t() - H
         Hc = Hc - Hc[first_wg][row_of_wg]
         wg_base = (row_base[row_of_wg, None] + chunk_off[row_of_wg] + Hc).contiguous()
         scratch = torch.empty(int(row_tot.sum()), dtype=torch.int64, device=dev)
@@ -315,9 +318,9 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
     every product of the matrix); its row pointer segment is a device-side
     cumsum carried from the previous chunk, so no host synchronisation sits
     between chunks.  C is allocated at the product-count bound and returned as
-    a view of its first nnz entries.  Returns None (caller falls back to the
-    plain path) when a row needs the HBM long-row path or overflowed an LDS
-    bin, which this pipeline does not stage."""
+    a view of its first nnz entries.  Hub rows (HBM long-row path) and rows
+    that overflowed an LDS bin are staged inside their chunk too (one host
+    synchronisation per chunk for the overflow check)."""
     dev = A.device
     m = A.m
     tot = info.flops // 2
@@ -334,8 +337,6 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
     order = torch.argsort(key, stable=True).to(torch.int32)
     hist = torch.bincount(key, minlength=nch * 16).tolist()
     ub_at = ub[bt].tolist()
-    if any(hist[c * 16 + NUM_GLOBAL + 1] for c in range(nch)):
-        return None
     for c in range(nch):
         for b in range(NUM_GLOBAL + 1):
             if hist[c * 16 + b + 1]:
@@ -366,9 +367,12 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
         sci, sv = stage[c % 2]
         if free[c % 2] is not None:
             sA.wait_event(free[c % 2])              # chunk c-2's compaction has read this buffer
+        long_rows = []
         for b in range(NUM_GLOBAL + 1):
             cnt = hist[c * 16 + b + 1]
-            if cnt:
+            if cnt and b == NUM_GLOBAL:
+                long_rows.append(order[off:off + cnt])
+            elif cnt:
                 _native.check(lib.spmm_spgemm_lds(b, 1, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
                                                   P(B.val), P(splits) if splits is not None else None,
                                                   P(order) + 4 * off, cnt, B.n, _group_log2(seg / _slices(b, 1)),
@@ -376,6 +380,14 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
                                                   sA.cuda_stream), "spgemm_lds(numeric, pipelined)")
             off += cnt
         off += hist[(c + 1) * 16] if c + 1 < nch else 0   # empty rows of the next chunk (bin -1)
+        spill = ((flags[lo:hi] & 2) != 0).nonzero().flatten()
+        if spill.numel():
+            info.rows_per_bin_num["lds_overflow"] = info.rows_per_bin_num.get("lds_overflow", 0) + int(spill.numel())
+            long_rows.append((spill + lo).to(torch.int32))
+        if long_rows:
+            rows = torch.cat(long_rows)
+            _long_rows(1, A, B, rows, nprod[rows.long()], sA.cuda_stream, out_nnz=out_nnz, Crp=ub_rel, Cci=sci,
+                       Cv=sv)
         done = torch.cuda.Event()
         done.record(sA)
         with torch.cuda.stream(sB):
@@ -387,8 +399,6 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
             free[c % 2] = torch.cuda.Event()
             free[c % 2].record(sB)
     sA.wait_stream(sB)
-    if bool(((flags & 2) != 0).any()):
-        return None
     nnz = int(rowptr[-1])
     info.nnz = nnz
     return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)
