@@ -17,6 +17,8 @@ Extra options (all optional; env equivalents SPMM_*):
   --threads N         host parser/writer threads (default: all)
   --quiet             suppress the "multiplying" lines
   --metrics-json PATH per-rank phase times, bytes moved and throughput
+  --no-split          cross-rank tree products on one rank each (default: each
+                      product is row-panel split over the ranks of its group)
 """
 from __future__ import annotations
 
@@ -37,6 +39,7 @@ def main(argv=None) -> int:
     ap.add_argument("--threads", type=int, default=int(os.environ.get("SPMM_THREADS", "0")))
     ap.add_argument("--quiet", action="store_true", default=bool(os.environ.get("SPMM_QUIET")))
     ap.add_argument("--metrics-json", default=os.environ.get("SPMM_METRICS_JSON"))
+    ap.add_argument("--no-split", action="store_true", default=bool(os.environ.get("SPMM_NO_SPLIT")))
     args = ap.parse_args(argv)
 
     import torch  # noqa: F401  (after argparse so --help is instant)
@@ -50,7 +53,8 @@ def main(argv=None) -> int:
     rc = 0
     try:
         log = None if args.quiet else (lambda s: print(s, flush=True))
-        run_chain(args.folder, comm, out_path=args.out, log=log, nthreads=args.threads, stats=stats)
+        run_chain(args.folder, comm, out_path=args.out, log=log, nthreads=args.threads, stats=stats,
+                  split=not args.no_split)
     except refio.FormatError as e:
         print(str(e), file=sys.stderr)
         rc = 1
@@ -63,7 +67,8 @@ def main(argv=None) -> int:
             k = refio.read_size(args.folder)[1]
         except refio.FormatError:
             k = 0
-        rec = dict(rank=comm.rank, world=comm.world, device=str(comm.device), wall_s=elapsed, **stats.as_dict(k))
+        rec = dict(rank=comm.rank, world=comm.world, device=str(comm.device), split=not args.no_split, wall_s=elapsed,
+                   **stats.as_dict(k))
         path = args.metrics_json if comm.world == 1 else f"{args.metrics_json}.rank{comm.rank}"
         with open(path, "w") as f:
             json.dump(rec, f, indent=1)
