@@ -124,8 +124,10 @@ def init(backend: str = "auto", device: str = "auto", timeout_s: float = 600.0) 
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    if world <= 1:
+    if world <= 1 and not os.environ.get("SPMM_FORCE_DIST"):
         return Comm(0, 1, 0, dev, None)
+    # SPMM_FORCE_DIST=1: a one-rank process group, so the collective code paths
+    # (RCCL on a GPU box with a single card) run for real in tests
     if backend == "auto":
         backend = "nccl" if use_gpu else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
