@@ -221,3 +221,30 @@ def test_spgemm_gpu_pipelined_onepass_matches_plain(monkeypatch, kind):
     if kind == "uniform":
         nz = C1.val.numel()
         assert nz == int(C1.rowptr[-1])
+
+
+@pytest.mark.gpu
+def test_rowblock_spgemm_rccl_one_rank(monkeypatch):
+    """The distributed SpGEMM path (count gather, async packed payload gather
+    over RCCL, deferred operand) in a one-rank RCCL group equals the local
+    product."""
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.parallel import comm as CM
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    for k, v in dict(SPMM_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                     WORLD_SIZE="1", LOCAL_RANK="0").items():
+        monkeypatch.setenv(k, v)
+    comm = CM.init(backend="nccl", device="cuda")
+    try:
+        assert comm.is_dist and comm.backend == "nccl"
+        prob = MS.UniformProblem.build(50000, 4e-4, comm, seed=5)
+        C1 = MS.rowblock_spgemm(prob.A, prob.B, comm)
+        C2 = SG.spgemm(prob.A, prob.B)
+        assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+        assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    finally:
+        comm.close()
