@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops.csr import CSR, from_coo
-from ..ops.spmm import PanelPlan, plan_panels, spmm
+from ..ops.spmm import PanelPlan, SpmmGraph, plan_panels, spmm
 from ..parallel.comm import Comm
 from ..parallel.partition import row_panels
 from ..utils.gen_csr import uniform_csr
@@ -103,6 +103,10 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     counts = [b - a for a, b in panels]
     plan = plan_panels(A) if comm.device.type == "cuda" and method == "mfma" else None
     step = lambda: rowblock_spmm(A, Xp, comm, counts, plan=plan, method=method if plan is not None else "auto")  # noqa: E731
+    if not comm.is_dist and comm.device.type == "cuda":
+        # one GPU: the step is a single launch-bound SpMM -> replay it from a HIP graph
+        graph = SpmmGraph(A, Xp, method=method if plan is not None else "auto", plan=plan)
+        step = graph.run
     flops_local = 2.0 * A.nnz * cols
     if comm.is_dist:
         t = torch.tensor([flops_local], dtype=torch.float64,
@@ -111,7 +115,8 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
         flops = float(t.item())
     else:
         flops = flops_local
-    extra = dict(nnz_A=int(A.nnz), spmm_method=method, panel_reuse=(plan.reuse if plan is not None else None))
+    extra = dict(nnz_A=int(A.nnz), spmm_method=method, panel_reuse=(plan.reuse if plan is not None else None),
+                 hip_graph=not comm.is_dist and comm.device.type == "cuda")
     cfg = dict(model=f"{n}x{n} CSR SpMM (sparse x dense {cols}-col) at {density * 100:g}% density, bf16 MFMA",
                n=n, density=density, cols=cols, global_batch=1, seq_len=n, parallelism=f"rowblock{comm.world}")
     return step, flops, extra, cfg

@@ -127,3 +127,34 @@ def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
     else:
         raise ValueError(f"unknown method {method!r}")
     return Y
+
+
+class SpmmGraph:
+    """Y = A . X replayed from a captured HIP graph.
+
+    The inspected SpMM has no host synchronisation, so its launches (input
+    cast, output allocation, MFMA or row kernel) are captured once into a
+    graph and replayed: a launch-bound 65536^2 x 128 step (~0.15 ms of GPU
+    work) stops paying per-kernel launch and Python dispatch costs.  ``X`` is
+    a static input buffer: copy new operands into ``graph.X`` before
+    ``run()``; ``run()`` returns the static output tensor.
+    """
+
+    def __init__(self, A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
+                 plan: Optional[PanelPlan] = None):
+        if A.device.type != "cuda":
+            raise ValueError("SpmmGraph needs a GPU operand")
+        self.X = X.to(torch.bfloat16).contiguous().clone()
+        side = torch.cuda.Stream(A.device)
+        side.wait_stream(torch.cuda.current_stream(A.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):   # warm-up outside the capture (allocator, lazy library state)
+                spmm(A, self.X, out_dtype, method, plan)
+        torch.cuda.current_stream(A.device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.Y = spmm(A, self.X, out_dtype, method, plan)
+
+    def run(self) -> torch.Tensor:
+        self.graph.replay()
+        return self.Y

@@ -116,3 +116,20 @@ def test_spmm_mfma_exact_small_integers():
     X = (torch.arange(n * D, device=dev).view(n, D) % 11 - 5).to(torch.bfloat16)
     Y = SM.spmm(A, X, method="mfma")
     assert torch.equal(Y, ref(A, X))
+
+
+@pytest.mark.gpu
+def test_spmm_graph_replay_matches_eager():
+    """The HIP-graph replay of the SpMM step gives the eager result, also after
+    new operands are copied into the static input."""
+    from spmm_amd.ops.spmm import SpmmGraph, plan_panels, spmm
+
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(3000, 2500, 0.01, seed=41, device=dev, dtype=torch.bfloat16)
+    X = (torch.rand((2500, 128), device=dev) * 2 - 1).to(torch.bfloat16)
+    plan = plan_panels(A)
+    g = SpmmGraph(A, X, method="mfma", plan=plan)
+    assert torch.equal(g.run(), spmm(A, X, method="mfma", plan=plan))
+    X2 = (torch.rand((2500, 128), device=dev) * 2 - 1).to(torch.bfloat16)
+    g.X.copy_(X2)
+    assert torch.equal(g.run(), spmm(A, X2, method="mfma", plan=plan))
