@@ -79,12 +79,16 @@ def run_rmat(comm, args):
 
     from spmm_amd.models import spgemm as MS
     from spmm_amd.ops.spgemm import SpgemmInfo, spgemm
-    from spmm_amd.parallel.partition import row_panels
     from spmm_amd.utils import gen_csr
 
     A = gen_csr.rmat_csr(args.scale, args.edge_factor, seed=args.seed, device=comm.device)
     At = A.transpose()
-    lo, hi = row_panels(A.m, comm.world)[comm.rank]
+    if comm.world > 1:   # hub rows sit at low indices: split rows at equal product counts, not equal rows
+        from spmm_amd.ops.spgemm import row_nprod
+        from spmm_amd.parallel.partition import weighted_row_panels
+        lo, hi = weighted_row_panels(torch.cumsum(row_nprod(A, At), 0).tolist(), comm.world)[comm.rank]
+    else:
+        lo, hi = 0, A.m
     Ap = A.row_slice(lo, hi)
     del A
     info = SpgemmInfo()
@@ -94,7 +98,7 @@ def run_rmat(comm, args):
     torch.cuda.empty_cache()
     return step, _allreduce_sum(comm, info.flops), dict(nnz_C=int(_allreduce_sum(comm, info.nnz))), dict(
         model=f"R-MAT scale-{args.scale} A.A^T", scale=args.scale, edge_factor=args.edge_factor, global_batch=1,
-        seq_len=1 << args.scale, parallelism=f"rowblock{comm.world}")
+        seq_len=1 << args.scale, parallelism=f"rowblock{comm.world}-product-balanced")
 
 
 def run_spmm(comm, args):

@@ -12,7 +12,10 @@ balanced by an estimated per-matrix cost (not bit-compatible with the
 reference for adversarial data; identical for inputs whose partial sums never
 hit 2^64-1).
 
-``row_panels`` splits rows for the 1D row-block SpGEMM / SpMM decomposition.
+``row_panels`` splits rows for the 1D row-block SpGEMM / SpMM decomposition;
+``weighted_row_panels`` splits them at equal cumulative work (e.g. the
+per-row product counts of a SpGEMM), which is what power-law matrices (R-MAT
+hub rows at low indices) need for balance.
 """
 from __future__ import annotations
 
@@ -67,6 +70,22 @@ def row_panels(m: int, p: int, align: int = 1) -> List[Tuple[int, int]]:
         hi = m if r == p - 1 else (m * (r + 1) // p) // align * align
         out.append((lo, hi))
     return out
+
+
+def weighted_row_panels(prefix: Sequence[int], p: int) -> List[Tuple[int, int]]:
+    """[lo, hi) row ranges with near-equal work: ``prefix`` is the inclusive
+    cumulative work per row (length m, non-decreasing).  Cut r is the first row
+    whose prefix reaches r/p of the total; panels may be empty."""
+    import bisect
+
+    m = len(prefix)
+    total = prefix[-1] if m else 0
+    cuts = [0]
+    for r in range(1, p):
+        c = bisect.bisect_left(prefix, total * r / p) + 1 if total else m * r // p
+        cuts.append(min(max(c, cuts[-1]), m))
+    cuts.append(m)
+    return [(cuts[r], cuts[r + 1]) for r in range(p)]
 
 
 def binomial_tree_schedule(p: int):

@@ -267,3 +267,15 @@ def test_run_chain_gpu_k32(tmp_path):
     want = golden.chain([golden.from_bsr(m) for m in mats], p=1)
     with open(out) as f:
         assert f.read() == golden.to_text(want)
+
+
+def test_weighted_row_panels_balance():
+    from spmm_amd.parallel.partition import weighted_row_panels
+
+    w = [1] * 100 + [50] * 4 + [1] * 96          # a hub block in the middle
+    pre = list(np.cumsum(w))
+    panels = weighted_row_panels(pre, 4)
+    assert panels[0][0] == 0 and panels[-1][1] == len(w)
+    assert all(a[1] == b[0] for a, b in zip(panels, panels[1:]))
+    loads = [sum(w[lo:hi]) for lo, hi in panels]
+    assert max(loads) <= sum(w) / 4 + 50          # within one heavy row of perfect
