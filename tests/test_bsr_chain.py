@@ -157,7 +157,7 @@ def test_refio_large_file_parallel_parse(tmp_path):
 
 def test_refio_writer_digit_boundaries_and_swar_parser(tmp_path):
     """Every decimal length 1..20 (incl. 0, 10^n - 1, 10^n, 2^64 - 1) through the
-    multi-threaded mapped writer (sizing pass) and the 8-digit SWAR parser."""
+    multi-threaded writer (sizing pass, exact offsets) and the 8-digit SWAR parser."""
     k = 6
     edge = [0, 2 ** 64 - 1, 2 ** 63, 2 ** 63 - 1]
     for n in range(1, 20):
