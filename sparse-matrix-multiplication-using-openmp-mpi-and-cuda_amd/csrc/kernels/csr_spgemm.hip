@@ -928,13 +928,24 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (c[u] < 0) continue;
-        const int t = c[u] >> LONG_LGW;
+        // Lanes holding the same chunk form runs (a sorted B row puts ~64
+        // consecutive columns in a handful of chunks): one LDS atomic per
+        // run instead of 64 same-address atomics, which serialise.
+        const int t = c[u] < 0 ? -1 : c[u] >> LONG_LGW;
+        const int tp = __shfl_up(t, 1);
+        const unsigned long long heads = __ballot(lane == 0 || t != tp);
+        const unsigned long long below = heads & (~0ull >> (63 - lane));   // heads at lanes <= lane
+        const int head = 63 - __clzll((long long)below);
+        const unsigned long long after = heads & ~(~0ull >> (63 - lane));  // heads at lanes > lane
+        const int next = after ? __ffsll((long long)after) - 1 : 64;
         if constexpr (SCATTER) {
-          const unsigned long long pos = atomicAdd(&cur[t], 1ull);
-          scratch[pos] = ((unsigned long long)__float_as_uint(a * v[u]) << 32) | (uint32_t)c[u];
+          unsigned long long base = 0;
+          if (head == lane && t >= 0) base = atomicAdd(&cur[t], (unsigned long long)(next - lane));
+          base = __shfl(base, head);
+          if (t >= 0)
+            scratch[base + (lane - head)] = ((unsigned long long)__float_as_uint(a * v[u]) << 32) | (uint32_t)c[u];
         } else {
-          atomicAdd(&hist[t], 1);
+          if (head == lane && t >= 0) atomicAdd(&hist[t], next - lane);
         }
       }
     }

@@ -224,6 +224,46 @@ def test_spgemm_gpu_pipelined_onepass_matches_plain(monkeypatch, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("onepass", ["on", "off"])
+def test_spgemm_gpu_long_rows_keep_cancelled_and_signed_zero_entries(monkeypatch, onepass):
+    """Hub rows (HBM long-row path) whose products cancel exactly or are -0.0
+    still store every structural entry: the long-row accumulator marks
+    occupancy with a -0.0 sentinel, so a -0 product or an exact cancellation
+    must not read as an empty slot."""
+    from spmm_amd.utils.config import CONFIG
+
+    k, n = 2000, 40000
+    B0 = gen_csr.uniform_csr(k // 2, n, 0.01, seed=41)
+    # B rows 2i and 2i+1 identical: A entries +1 / -1 on them cancel to exactly
+    # 0 in any summation order (values are multiples of 1/8: every partial sum is exact)
+    v0 = torch.round(B0.val * 8) / 8 + 0.125
+    v0[::7] = -0.0
+    rows = torch.cat([B0.row_ids() * 2, B0.row_ids() * 2 + 1])
+    cols = torch.cat([B0.col, B0.col]).long()
+    vals = torch.cat([v0, v0])
+    B = CS.from_coo(rows, cols, vals, k, n, sum_duplicates=False)
+    ar, ac, av = [], [], []
+    for r in range(4):   # 4 hub rows over all of B: ~800k products each
+        ar.append(torch.full((k,), r))
+        ac.append(torch.arange(k))
+        av.append(torch.where(torch.arange(k) % 2 == 0, 1.0, -1.0) if r % 2 == 0 else torch.rand(k) - 0.5)
+    A = CS.from_coo(torch.cat(ar), torch.cat(ac), torch.cat(av), 4, k)
+    Cc = SG.spgemm(A, B)
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", onepass)
+    info = SG.SpgemmInfo()
+    dev = torch.device("cuda")
+    Cg = SG.spgemm(A.to(dev), B.to(dev), info)
+    assert SG.NUM_GLOBAL in info.rows_per_bin_num
+    pat = (A.to_dense() != 0).double() @ torch.sparse_coo_tensor(
+        torch.stack([B.row_ids(), B.col.long()]), torch.ones(B.nnz, dtype=torch.float64), (k, n)).to_dense()
+    assert Cg.nnz == int((pat != 0).sum()) == Cc.nnz
+    assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+    assert torch.equal(Cg.col.cpu(), Cc.col)
+    assert torch.allclose(Cg.val.cpu(), Cc.val, atol=1e-3, rtol=1e-4)
+    assert int((Cg.val[:int(Cg.rowptr[1])] == 0).sum()) == int(Cg.rowptr[1])   # row 0 cancels exactly
+
+
+@pytest.mark.gpu
 def test_rowblock_spgemm_rccl_one_rank(monkeypatch):
     """The distributed SpGEMM path (count gather, async packed payload gather
     over RCCL, deferred operand) in a one-rank RCCL group equals the local

@@ -26,7 +26,7 @@ def main() -> None:
         k = r["Kernel_Name"]
         if filt not in k:
             continue
-        short = k.split("(")[0][-90:]
+        short = k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][-90:]
         agg[short][r["Counter_Name"]] += float(r["Counter_Value"])
         calls[short].add(r["Dispatch_Id"])
         dur[short][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
