@@ -15,8 +15,8 @@ FLOPs = 2 x intermediate products (BASELINE.md convention), summed over ranks;
 value = total FLOPs / max-over-ranks step time.
 
 Other workloads (--workload): ``spmm`` (65536^2 CSR x dense 128 cols, bf16,
-config 3), ``spgemm64k`` (65536^2 @ 0.1 %, config 2), ``rmat`` (R-MAT A.A^T,
-config 5), ``chain`` (the reference's block-sparse uint64 chain, report
+config 3), ``spgemm64k`` (65536^2 @ 0.1 %, config 2), ``rmat`` (R-MAT scale-24
+A.A^T, config 5; ``--scale 20`` keeps C resident on one GPU), ``chain`` (the reference's block-sparse uint64 chain, report
 Table 1 Medium preset).  BASELINE.json publishes no number for the CSR
 configs, so vs_baseline is null for them; for ``chain`` it is the speed-up
 over the report's P100 kernel throughput (500 GOP/s, report.pdf p.3 §4.2).
@@ -75,30 +75,47 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
 
 
 def run_rmat(comm, args):
+    """BASELINE config 5: R-MAT A.A^T, rows split over ranks at equal
+    intermediate-product counts.  C is kept resident when its product-count
+    bound fits this GPU; otherwise (scale 24: ~10^12 products, C of several
+    TB) it is produced in row panels that are consumed and freed one at a time
+    (``streamed_spgemm``; every product is still computed)."""
     import torch
 
     from spmm_amd.models import spgemm as MS
-    from spmm_amd.ops.spgemm import SpgemmInfo, spgemm
+    from spmm_amd.ops.spgemm import SpgemmInfo, row_nprod, spgemm
+    from spmm_amd.parallel.partition import weighted_row_panels
     from spmm_amd.utils import gen_csr
 
     A = gen_csr.rmat_csr(args.scale, args.edge_factor, seed=args.seed, device=comm.device)
     At = A.transpose()
-    if comm.world > 1:   # hub rows sit at low indices: split rows at equal product counts, not equal rows
-        from spmm_amd.ops.spgemm import row_nprod
-        from spmm_amd.parallel.partition import weighted_row_panels
-        lo, hi = weighted_row_panels(torch.cumsum(row_nprod(A, At), 0).tolist(), comm.world)[comm.rank]
-    else:
-        lo, hi = 0, A.m
+    nprod = row_nprod(A, At)
+    lo, hi = weighted_row_panels(torch.cumsum(nprod, 0), comm.world)[comm.rank]
+    local_products = int(nprod[lo:hi].sum())
+    del nprod
     Ap = A.row_slice(lo, hi)
     del A
+    torch.cuda.empty_cache() if comm.device.type == "cuda" else None
+    stream = args.rmat_stream == "on" or (args.rmat_stream == "auto" and local_products > MS.stream_budget(comm.device))
     info = SpgemmInfo()
-    C = spgemm(Ap, At, info)
-    del C
-    step = lambda: spgemm(Ap, At)  # noqa: E731
-    torch.cuda.empty_cache()
-    return step, _allreduce_sum(comm, info.flops), dict(nnz_C=int(_allreduce_sum(comm, info.nnz))), dict(
+    if stream:
+        nnz = [0]
+
+        def consume(_lo, _hi, C):   # C's row panel is complete here; count it and let it go
+            nnz[0] += C.nnz
+
+        MS.streamed_spgemm(Ap, At, consume, info=info)
+        step = lambda: MS.streamed_spgemm(Ap, At, consume)  # noqa: E731
+    else:
+        C = spgemm(Ap, At, info)
+        del C
+        step = lambda: spgemm(Ap, At)  # noqa: E731
+    if comm.device.type == "cuda":
+        torch.cuda.empty_cache()
+    par = f"rowblock{comm.world}-product-balanced" + ("-streamed-C" if stream else "")
+    return step, _allreduce_sum(comm, info.flops), dict(nnz_C=int(_allreduce_sum(comm, info.nnz)), c_streamed=stream), dict(
         model=f"R-MAT scale-{args.scale} A.A^T", scale=args.scale, edge_factor=args.edge_factor, global_batch=1,
-        seq_len=1 << args.scale, parallelism=f"rowblock{comm.world}-product-balanced")
+        seq_len=1 << args.scale, parallelism=par)
 
 
 def run_spmm(comm, args):
@@ -139,7 +156,9 @@ def main() -> None:
     ap.add_argument("--matrix-density", dest="density", type=float, default=1e-4)
     ap.add_argument("--spmm-n", type=int, default=65536)
     ap.add_argument("--spmm-density", type=float, default=1e-3)
-    ap.add_argument("--scale", type=int, default=20)   # scale 24 A.A^T does not fit 8x288 GB (C ~ 10^11+ nnz)
+    ap.add_argument("--scale", type=int, default=24, help="R-MAT scale (BASELINE config 5: 24)")
+    ap.add_argument("--rmat-stream", default="auto", choices=["auto", "on", "off"],
+                    help="produce C in consumed row panels (auto: when its product bound does not fit)")
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],

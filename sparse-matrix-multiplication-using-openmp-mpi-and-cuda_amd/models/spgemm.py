@@ -159,6 +159,69 @@ def rowblock_spgemm(A_panel: CSR, B_panel: CSR, comm: Comm, info: Optional[Spgem
     return spgemm(A_panel, B_meta, info, B_ready=ready)
 
 
+STREAM_MEM_FRACTION = 0.4   # of free device memory for one panel's C bound + staging (16 B / product)
+
+
+def stream_budget(dev: torch.device) -> int:
+    """Intermediate products per streamed row panel: the panel's product-count
+    bound C plus an equal staging buffer (the one-pass mode) in a fixed share
+    of the free device memory."""
+    if dev.type != "cuda":
+        return 1 << 28
+    free, _ = torch.cuda.mem_get_info(dev)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    return max(1 << 24, int(STREAM_MEM_FRACTION * free) // 16)
+
+
+def stream_panels(nprod: torch.Tensor, budget: int) -> List[Tuple[int, int]]:
+    """Contiguous row panels of at most ``budget`` products each (a row with
+    more products is a panel of its own)."""
+    m = nprod.numel()
+    if m == 0:
+        return []
+    prefix = torch.cumsum(nprod.long(), 0)
+    total = int(prefix[-1])
+    if total <= budget:
+        return [(0, m)]
+    panels, lo, done = [], 0, 0
+    while lo < m:
+        # last row whose prefix stays within done + budget (at least one row)
+        hi = int(torch.searchsorted(prefix, torch.tensor([done + budget], device=prefix.device), right=True))
+        hi = min(max(hi, lo + 1), m)
+        panels.append((lo, hi))
+        done = int(prefix[hi - 1])
+        lo = hi
+    return panels
+
+
+def streamed_spgemm(A: CSR, B: CSR, consume: Callable[[int, int, CSR], None], budget: Optional[int] = None,
+                    info: Optional[SpgemmInfo] = None) -> SpgemmInfo:
+    """C = A . B produced in row panels and handed to ``consume(lo, hi,
+    C[lo:hi])`` one at a time, so C never has to be resident: R-MAT scale-24
+    A.A^T has ~10^12 intermediate products and a C of several TB, more than
+    8 x 288 GB of HBM.  Every panel is a complete SpGEMM of A's rows lo..hi
+    against all of B (nothing is skipped); only C's lifetime is bounded.  The
+    reference bounds its device footprint the same way, with rounds of <= 500
+    output tiles copied back to the host (sparse_matrix_mult.cu:181-270)."""
+    info = info if info is not None else SpgemmInfo()
+    from ..ops.spgemm import row_nprod
+
+    nprod = row_nprod(A, B)
+    budget = budget if budget is not None else stream_budget(A.device)
+    for lo, hi in stream_panels(nprod, budget):
+        pi = SpgemmInfo()
+        C = spgemm(A.row_slice(lo, hi), B, pi)
+        info.flops += pi.flops
+        info.nnz += pi.nnz
+        info.resorted_rows += pi.resorted_rows
+        for b, c in pi.rows_per_bin_num.items():
+            info.rows_per_bin_num[b] = info.rows_per_bin_num.get(b, 0) + c
+        consume(lo, hi, C)
+        del C
+    info.mean_seg = info.flops / 2 / max(A.nnz, 1)
+    return info
+
+
 @dataclass
 class UniformProblem:
     """A, B uniform random n x n at ``density``; this rank's row panels."""

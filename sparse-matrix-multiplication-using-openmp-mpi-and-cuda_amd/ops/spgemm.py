@@ -240,7 +240,10 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     A = A if A.val.dtype == torch.float32 else A.with_values(A.val.float())
     B = B if B.val.dtype == torch.float32 else B.with_values(B.val.float())
     nprod = row_nprod(A, B)
-    info.flops = 2 * int(nprod.sum())
+    tot, mx = torch.stack([nprod.sum(), nprod.max() if A.m else nprod.sum()]).tolist()
+    if mx >= 1 << 31:   # per-row capacities and counts are int32 in the kernels
+        raise ValueError(f"a row of A.B has {mx} intermediate products (limit 2^31 - 1)")
+    info.flops = 2 * tot
     info.mean_seg = info.flops / 2 / max(A.nnz, 1)
     if B_ready is not None:
         cached = []

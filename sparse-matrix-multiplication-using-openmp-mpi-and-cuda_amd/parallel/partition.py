@@ -75,14 +75,23 @@ def row_panels(m: int, p: int, align: int = 1) -> List[Tuple[int, int]]:
 def weighted_row_panels(prefix: Sequence[int], p: int) -> List[Tuple[int, int]]:
     """[lo, hi) row ranges with near-equal work: ``prefix`` is the inclusive
     cumulative work per row (length m, non-decreasing).  Cut r is the first row
-    whose prefix reaches r/p of the total; panels may be empty."""
+    whose prefix reaches r/p of the total; panels may be empty.  ``prefix``
+    may be an integer tensor (searched where it lives: no host copy of a
+    16M-row prefix)."""
     import bisect
 
     m = len(prefix)
-    total = prefix[-1] if m else 0
+    total = int(prefix[-1]) if m else 0
+    import torch
+
+    if m and isinstance(prefix, torch.Tensor):
+        targets = torch.tensor([-(-total * r // p) for r in range(1, p)], dtype=prefix.dtype, device=prefix.device)
+        found = torch.searchsorted(prefix, targets).tolist() if p > 1 else []
+    else:
+        found = [bisect.bisect_left(prefix, total * r / p) for r in range(1, p)]
     cuts = [0]
     for r in range(1, p):
-        c = bisect.bisect_left(prefix, total * r / p) + 1 if total else m * r // p
+        c = found[r - 1] + 1 if total else m * r // p
         cuts.append(min(max(c, cuts[-1]), m))
     cuts.append(m)
     return [(cuts[r], cuts[r + 1]) for r in range(p)]

@@ -279,3 +279,6 @@ def test_weighted_row_panels_balance():
     assert all(a[1] == b[0] for a, b in zip(panels, panels[1:]))
     loads = [sum(w[lo:hi]) for lo, hi in panels]
     assert max(loads) <= sum(w) / 4 + 50          # within one heavy row of perfect
+    import torch
+    for p in (1, 2, 3, 4, 7):                     # device-tensor prefix: same cuts as the list
+        assert weighted_row_panels(torch.tensor(pre), p) == weighted_row_panels(pre, p)

@@ -288,3 +288,28 @@ def test_rowblock_spgemm_rccl_one_rank(monkeypatch):
         assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
     finally:
         comm.close()
+
+
+def test_streamed_spgemm_panels_concatenate_to_full_product():
+    """C produced in product-bounded row panels (C never resident) equals the
+    one-shot product, panel by panel, and every panel respects the budget
+    unless it is a single row."""
+    from spmm_amd.models import spgemm as MS
+
+    A = gen_csr.rmat_csr(10, 8, seed=3)
+    At = A.transpose()
+    full = SG.spgemm(A, At)
+    nprod = SG.row_nprod(A, At)
+    budget = int(nprod.sum()) // 7
+    panels = MS.stream_panels(nprod, budget)
+    assert panels[0][0] == 0 and panels[-1][1] == A.m and len(panels) >= 7
+    assert all(a[1] == b[0] for a, b in zip(panels, panels[1:]))
+    assert all(int(nprod[lo:hi].sum()) <= budget or hi - lo == 1 for lo, hi in panels)
+    got = []
+    info = MS.streamed_spgemm(A, At, lambda lo, hi, C: got.append((lo, hi, C)), budget=budget)
+    assert [(lo, hi) for lo, hi, _ in got] == panels
+    assert info.nnz == full.nnz and info.flops == 2 * int(nprod.sum())
+    for lo, hi, C in got:
+        ref = full.row_slice(lo, hi)
+        assert torch.equal(C.rowptr, ref.rowptr) and torch.equal(C.col, ref.col)
+        assert torch.allclose(C.val, ref.val)
