@@ -956,47 +956,119 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
   }
 }
 
+// 64-lane inclusive prefix sum on the DPP network (VALU; no LDS traffic):
+// row_shr 1/2/4/8 inside 16-lane rows, then row_bcast:15 / row_bcast:31.
+__device__ __forceinline__ int wave_incl_scan_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// Persistent: a workgroup walks (row, chunk) items rt = blockIdx.x,
+// + gridDim.x, ...  At R-MAT scale 24 (2^24 columns = 1024 chunks per hub
+// row) an item averages ~500 products, so the fixed per-item LDS work of a
+// one-item-per-workgroup kernel (clear 64 KB, scan 512 occupancy words)
+// outweighed the product atomics ~10:1.  Here the accumulator is cleared by
+// the write-back itself (only occupied columns are non-zero; the 64 KB clear
+// runs once per workgroup), the block scan runs on DPP instead of LDS
+// permutes, empty items cost nothing, and the next item's counts and first
+// scratch loads are in flight during the current write-back.
 template <bool VALUES>
 __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restrict__ rt_off,
-                                                         const int64_t* __restrict__ rt_cnt, int nch,
+                                                         const int64_t* __restrict__ rt_cnt, int64_t nrt, int nch,
                                                          unsigned long long* __restrict__ scratch,
                                                          int64_t* __restrict__ rt_nnz) {
   __shared__ float vals[VALUES ? LONG_W : 1];
   __shared__ uint32_t bits[LONG_W / 32];
   __shared__ int wsum[LONG_NT / 64];
-  const int64_t rt = blockIdx.x;
-  const int64_t n = rt_cnt[rt];
-  if (n == 0) {
-    if (threadIdx.x == 0) rt_nnz[rt] = 0;
-    return;
-  }
-  const int tid = threadIdx.x;
-  const int64_t base = rt_off[rt];
-  const int c0 = (int)(rt % nch) << LONG_LGW;
-  for (int i = tid; i < LONG_W / 32; i += LONG_NT) bits[i] = 0u;
+  static_assert(LONG_W / 32 == LONG_NT, "one occupancy word per thread");
+  constexpr int NW = LONG_NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bits[tid] = 0u;
   if constexpr (VALUES)
     for (int i = tid; i < LONG_W / 4; i += LONG_NT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-  for (int64_t i = tid; i < n; i += LONG_NT) {
-    const unsigned long long x = scratch[base + i];
-    const int c = (int)(uint32_t)x - c0;
-    atomicOr(&bits[c >> 5], 1u << (c & 31));
-    if constexpr (VALUES) atomicAdd(&vals[c], __uint_as_float((uint32_t)(x >> 32)));
+  int64_t rt = blockIdx.x;
+  int64_t n = 0, base = 0;
+  if (rt < nrt) { n = rt_cnt[rt]; base = rt_off[rt]; }
+  unsigned long long x[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = tid + u * LONG_NT;
+    x[u] = i < n ? scratch[base + i] : ~0ull;
   }
   __syncthreads();
-  // one bit word per thread (LONG_W / 32 == LONG_NT): occupied columns in order
-  static_assert(LONG_W / 32 == LONG_NT, "one occupancy word per thread");
-  const uint32_t word = bits[tid];
-  int total;
-  const int pos = block_excl_scan<LONG_NT, int>(__popc(word), wsum, &total);
-  int k = 0;
-  for (uint32_t m = word; m; m &= m - 1, ++k) {
-    const int b = __ffs(m) - 1;
-    const int cl = tid * 32 + b;
-    const float v = VALUES ? vals[cl] : 0.f;
-    scratch[base + pos + k] = ((unsigned long long)__float_as_uint(v) << 32) | (uint32_t)(c0 + cl);
+  while (rt < nrt) {
+    const int64_t rt2 = rt + gridDim.x;
+    if (n == 0) {   // uniform over the workgroup: no LDS state touched
+      if (tid == 0) rt_nnz[rt] = 0;
+      rt = rt2;
+      n = 0;
+      if (rt < nrt) { n = rt_cnt[rt]; base = rt_off[rt]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = tid + u * LONG_NT;
+        x[u] = i < n ? scratch[base + i] : ~0ull;
+      }
+      continue;
+    }
+    const int c0 = (int)(rt % nch) << LONG_LGW;
+    for (int64_t i0 = tid;;) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (x[u] == ~0ull) continue;
+        const int c = (int)(uint32_t)x[u] - c0;
+        atomicOr(&bits[c >> 5], 1u << (c & 31));
+        if constexpr (VALUES) atomicAdd(&vals[c], __uint_as_float((uint32_t)(x[u] >> 32)));
+      }
+      i0 += 4 * LONG_NT;
+      if (i0 >= n) break;
+      // 4 scratch loads in flight per lane before the LDS updates
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * LONG_NT;
+        x[u] = i < n ? scratch[base + i] : ~0ull;
+      }
+    }
+    __syncthreads();
+    int64_t n2 = 0, base2 = 0;
+    if (rt2 < nrt) { n2 = rt_cnt[rt2]; base2 = rt_off[rt2]; }
+    // one occupancy word per thread: its columns in order; the write-back
+    // clears what it reads
+    const uint32_t word = bits[tid];
+    bits[tid] = 0u;
+    const int cnt = __popc(word);
+    const int incl = wave_incl_scan_dpp(cnt);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int pre = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int sw = wsum[i];
+      pre += (i < w) ? sw : 0;
+      total += sw;
+    }
+    const int pos = pre + incl - cnt;
+    int k = 0;
+    for (uint32_t m = word; m; m &= m - 1, ++k) {
+      const int b = __ffs(m) - 1;
+      const int cl = tid * 32 + b;
+      float v = 0.f;
+      if constexpr (VALUES) { v = vals[cl]; vals[cl] = 0.f; }
+      scratch[base + pos + k] = ((unsigned long long)__float_as_uint(v) << 32) | (uint32_t)(c0 + cl);
+    }
+    if (tid == 0) rt_nnz[rt] = total;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = tid + u * LONG_NT;
+      x[u] = i < n2 ? scratch[base2 + i] : ~0ull;
+    }
+    rt = rt2; n = n2; base = base2;
+    __syncthreads();   // write-back clears and wsum reads done before the next item's atomics / wsum writes
   }
-  if (tid == 0) rt_nnz[rt] = total;
 }
 
 // chunk results -> final CSR positions (one wave per (row, chunk))
@@ -1167,11 +1239,21 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
                                        void* scratch, int64_t* rt_nnz, void* stream) {
   if (nrt <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  // persistent grid: the resident capacity (two 66 KB workgroups per CU with
+  // values, LDS-light count pass: more)
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>(nrt, (values ? 2 : 4) * (int64_t)ncu);
   if (values)
-    hipLaunchKernelGGL(long_dense<true>, dim3((unsigned)nrt), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nch,
+    hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nrt, nch,
                        (unsigned long long*)scratch, rt_nnz);
   else
-    hipLaunchKernelGGL(long_dense<false>, dim3((unsigned)nrt), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nch,
+    hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nrt, nch,
                        (unsigned long long*)scratch, rt_nnz);
   SPMM_LAUNCH_CHECK();
   return 0;
