@@ -520,13 +520,68 @@ __device__ __forceinline__ int wave_max(int x) {
   return max(max(a, b), max(c, d));
 }
 
-template <int PCAP, int NT, int NP>
+// Ordered mode (one-pass without the compaction copy): the grid walks
+// "units" = (row, column-eighth range) in row order; a workgroup takes the
+// next unit from a ticket counter (so every earlier unit is already running
+// or done), and its output position comes from a decoupled look-back over
+// the units' published counts.  Rows land directly at their final CSR
+// offsets: no staging buffer, no compaction pass.
+struct EscOrd {
+  const int32_t* unit_row;
+  const uint8_t* unit_q;            // q0 | q1 << 4 (column eighths [q0, q1))
+  uint32_t* ticket;
+  unsigned long long* status;       // per unit: flag (2 bits) | count or inclusive prefix (62 bits)
+  int64_t cap;                      // entries allocated for C
+  int32_t* err;                     // bit 0: a unit overflowed its LDS slice, bit 1: C capacity
+};
+
+// Publish this unit's count, sum the predecessors back to the first
+// inclusive prefix, publish the inclusive prefix; returns the exclusive one.
+// Run by one whole wave: the 64 nearest predecessors' status words are loaded
+// at once (one memory round trip instead of one per predecessor), and the
+// window slides back only while all 64 are counts without a prefix.
+__device__ __forceinline__ int64_t ord_lookback(unsigned long long* status, int64_t u, int64_t count, int lane) {
+  constexpr unsigned long long AGG = 1ull << 62, INC = 2ull << 62, VM = (1ull << 62) - 1;
+  if (u == 0) {
+    if (lane == 0)
+      __hip_atomic_store(&status[0], INC | (unsigned long long)count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&status[u], AGG | (unsigned long long)count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int64_t pre = 0;
+  for (int64_t end = u;;) {
+    const int64_t j = end - 1 - lane;   // lane 0 = nearest predecessor
+    const unsigned long long st =
+        j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : INC;
+    const unsigned f = (unsigned)(st >> 62);
+    const unsigned long long inc = __ballot(f == 2), notready = __ballot(f == 0);
+    const int first = inc ? __ffsll((long long)inc) - 1 : 64;
+    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1);   // lanes 0..first
+    if (notready & need) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    int64_t v = lane <= first ? (int64_t)(st & VM) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    pre += v;
+    if (first < 64) break;
+    end -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&status[u], INC | (unsigned long long)(pre + count), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return pre;
+}
+
+template <int PCAP, int NT, int NP, bool ORD = false>
 __global__ __launch_bounds__(NT, 4) void spgemm_esc(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
     const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
     const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols, int lg,
     const int32_t* __restrict__ row_cap, int32_t* __restrict__ out_nnz, const int64_t* __restrict__ Crp,
-    int32_t* __restrict__ Cci, float* __restrict__ Cv, int32_t* __restrict__ flags) {
+    int32_t* __restrict__ Cci, float* __restrict__ Cv, int32_t* __restrict__ flags, EscOrd ord) {
   constexpr int NW = NT / 64, ACAP = NT, CCAP = 2 * NT, NB = ESC_NB;
   constexpr int BPT = NB / NT;                 // buckets per thread in the scan / sort
   constexpr int QSTEP = 8 / NP;
@@ -543,10 +598,23 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
   __shared__ int clist[CCAP];
   __shared__ float aval[ACAP];
   __shared__ int64_t wsum[NW];
+  __shared__ int64_t ord_sh;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int row = rows[blockIdx.x];
+  int row, uq0 = 0, uq1 = 8;
+  int64_t unit = 0;
+  if constexpr (ORD) {
+    if (tid == 0) ord_sh = (int64_t)atomicAdd(ord.ticket, 1u);
+    __syncthreads();
+    unit = ord_sh;
+    row = ord.unit_row[unit];
+    const int q = ord.unit_q[unit];
+    uq0 = q & 15;
+    uq1 = q >> 4;
+  } else {
+    row = rows[blockIdx.x];
+  }
   const int64_t a0 = Arp[row], na = Arp[row + 1] - a0;
   const int lgE = lg > LG_MIN ? lg : LG_MIN;
   const int ngrp = NW << (6 - lgE);
@@ -567,12 +635,18 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
   if (single && tid < na) {
     ej = Aci[a0 + tid];
     eav = Av[a0 + tid];
-    eb0 = Brp[ej];
-    eb1 = (NP == 1) ? Brp[ej + 1] : bsplit[(int64_t)ej * 7 + QSTEP - 1];
+    if constexpr (ORD) {
+      eb0 = uq0 == 0 ? Brp[ej] : bsplit[(int64_t)ej * 7 + uq0 - 1];
+      eb1 = uq1 == 8 ? Brp[ej + 1] : bsplit[(int64_t)ej * 7 + uq1 - 1];
+    } else {
+      eb0 = Brp[ej];
+      eb1 = (NP == 1) ? Brp[ej + 1] : bsplit[(int64_t)ej * 7 + QSTEP - 1];
+    }
   }
 
-  for (int sl = 0; sl < NP; ++sl) {
-    const int q0 = sl * QSTEP, q1 = q0 + QSTEP;
+  constexpr int NSL = ORD ? 1 : NP;
+  for (int sl = 0; sl < NSL; ++sl) {
+    const int q0 = ORD ? uq0 : sl * QSTEP, q1 = ORD ? uq1 : q0 + QSTEP;
     const int clo = (int)(((int64_t)q0 * ncols) >> 3), chi = (int)(((int64_t)q1 * ncols) >> 3);
     const uint32_t mult = hash_mult(NB, chi - clo);
     for (int i = tid; i < NB / 8; i += NT) reinterpret_cast<uint4*>(hist)[i] = make_uint4(0, 0, 0, 0);
@@ -593,13 +667,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
               abeg[tid] = eb0;
               aval[tid] = eav;
               eb0 = eb1;   // next slice starts where this one ends
-              if (sl + 1 < NP)   // prefetch the next slice's end
+              if (!ORD && sl + 1 < NP)   // prefetch the next slice's end
                 eb1 = (sl + 2 == NP) ? Brp[ej + 1] : bsplit[(int64_t)ej * 7 + (sl + 2) * QSTEP - 1];
             }
             scan_chunks<NT>(len, lgE, wsum, nch, pre, TC, tot);
           } else {
-            stage_batch<NT, NP, true>(Aci, Av, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, aval, wsum, len, nch,
-                                      pre, TC, tot);
+            stage_batch<NT, (ORD ? 2 : NP), true>(Aci, Av, Brp, bsplit, a0 + bat, nb, q0, q1, lgE, abeg, aval, wsum,
+                                                  len, nch, pre, TC, tot);
           }
           if (pass == 0) {
             slice_products += tot;
@@ -686,6 +760,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
     }
     if (overflow) {
       if (tid == 0) atomicOr(&flags[row], 2);
+      if constexpr (ORD) {   // successors still need this unit's count: publish 0, the host recomputes
+        if (tid == 0) atomicOr(ord.err, 1);
+        if (w == 0) ord_lookback(ord.status, unit, 0, lane);
+      }
       return;   // uniform: every thread saw the same totals
     }
     // hist[b] now holds the END offset of bucket b.  Sort + fold each bucket.
@@ -801,10 +879,25 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
       if (tid < NWIN) clist[tid] = bw;
     }
     __syncthreads();
-    const int64_t base = Crp[row] + written;
-    const int room = row_cap[row] - written;
-    const int lim = total < room ? total : room;
-    if (tid == 0 && total > room) atomicOr(&flags[row], 4);
+    int64_t base;
+    int lim;
+    if constexpr (ORD) {
+      if (w == 0) {
+        const int64_t b = ord_lookback(ord.status, unit, total, lane);
+        if (lane == 0) ord_sh = b;
+      }
+      __syncthreads();
+      base = ord_sh;
+      SPMM_STAMP(4);   // unit count scan + look-back
+      const int64_t room = ord.cap - base;
+      lim = total <= room ? total : (int)(room > 0 ? room : 0);
+      if (tid == 0 && total > room) atomicOr(ord.err, 2);
+    } else {
+      base = Crp[row] + written;
+      const int room = row_cap[row] - written;
+      lim = total < room ? total : room;
+      if (tid == 0 && total > room) atomicOr(&flags[row], 4);
+    }
 #pragma unroll
     for (int j = 0; j < WPW; ++j) {
       const int W = w + j * NW;
@@ -828,7 +921,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
     written += total;
     __syncthreads();   // slice done before the next slice reuses the buffers
   }
-  if (out_nnz != nullptr && tid == 0) out_nnz[row] = written;
+  if (out_nnz != nullptr && tid == 0) {
+    if constexpr (ORD) atomicAdd(&out_nnz[row], written);   // several units per row
+    else out_nnz[row] = written;
+  }
   if (stamp_on && tid == 0) atomicAdd(&g_stamps[7], 1ull);
 }
 
@@ -1123,7 +1219,7 @@ int launch_esc(const int64_t* Arp, const int32_t* Aci, const float* Av, const in
                int32_t* flags, hipStream_t s) {
   if (nrows <= 0) return 0;
   hipLaunchKernelGGL((spgemm_esc<PCAP, NT, NP>), dim3((unsigned)nrows), dim3(NT), 0, s, Arp, Aci, Av, Brp, Bci, Bv,
-                     bsplit, rows, ncols, lg, row_cap, out_nnz, Crp, Cci, Cv, flags);
+                     bsplit, rows, ncols, lg, row_cap, out_nnz, Crp, Cci, Cv, flags, EscOrd{});
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -1216,6 +1312,23 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
 #undef SPMM_SARGS
 }
 
+
+// Ordered one-pass ESC over units (see EscOrd).  ticket / status / err /
+// out_nnz must be zero; unit_q holds q0 | q1 << 4.
+SPMM_EXPORT int spmm_spgemm_esc_ordered(const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp,
+                                        const int32_t* Bci, const float* Bv, const int64_t* bsplit,
+                                        const int32_t* unit_row, const uint8_t* unit_q, int64_t nunits, int ncols,
+                                        int lg, uint32_t* ticket, unsigned long long* status, int64_t cap,
+                                        int32_t* err, int32_t* out_nnz, int32_t* Cci, float* Cv, int32_t* flags,
+                                        void* stream) {
+  if (nunits <= 0) return 0;
+  if (lg < 4 || lg > 6 || nunits > 0xffffffffll) return (int)hipErrorInvalidValue;
+  EscOrd o{unit_row, unit_q, ticket, status, cap, err};
+  hipLaunchKernelGGL((spgemm_esc<7680, 512, 2, true>), dim3((unsigned)nunits), dim3(512), 0, (hipStream_t)stream, Arp,
+                     Aci, Av, Brp, Bci, Bv, bsplit, nullptr, ncols, lg, nullptr, out_nnz, nullptr, Cci, Cv, flags, o);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
 
 // ---- long rows (see the kernels' comment) -----------------------------------
 SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp,

@@ -46,6 +46,8 @@ _native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_
 _native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
+                     C_INT, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
@@ -254,6 +256,11 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
                 cached.append(fetch())
             return cached[0]
     mode = _onepass_mode(info.flops // 2, A.device)
+    if mode is not None and _ordered_ok(nprod, info.flops // 2, A.device):
+        C_ = onepass_ordered(A, B, nprod, info, B_ready)
+        if C_ is not None:
+            return C_
+        info.rows_per_bin_num = {}
     if mode == "pipelined":
         C_ = onepass_pipelined(A, B, nprod, info, B_ready)
         if C_ is not None:
@@ -297,6 +304,89 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None)
                                                      _native.stream_ptr(dev)), "spgemm_compact")
     del Uci, Uv
     return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
+
+
+ORDERED_MAX_LIGHT = 0.05           # ordered mode: at most this share of non-empty rows below the ESC bins
+
+
+def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device) -> bool:
+    """Ordered one-pass: every non-empty row fits the bucketed-ESC kernel
+    (no HBM long rows), few rows would be better served by the small LDS
+    tables, and C fits at its product-count bound."""
+    mode = CONFIG.spgemm_ordered
+    if mode == "off" or total_products == 0:
+        return False
+    mx = int(nprod.max())
+    if mx > int(ESC_LOAD * ESC_PCAP) * 8:
+        return False
+    if mode != "on":
+        nz = int((nprod > 0).sum())
+        light = int(((nprod > 0) & (nprod <= ESC_MIN)).sum())
+        if light > ORDERED_MAX_LIGHT * nz:
+            return False
+        free, _ = torch.cuda.mem_get_info(dev)
+        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        if total_products * 8 > 0.8 * free:
+            return False
+    return True
+
+
+def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None) -> Optional[CSR]:
+    """One-pass numeric that writes every row at its FINAL offset: rows are
+    split into units (row, column-eighth range) of the bucketed-ESC kernel
+    (1 / 2 / 4 / 8 per row by product count), walked in row order, and each
+    unit's position comes from a decoupled look-back over the counts of the
+    units before it (csr_spgemm.hip ``EscOrd``).  No staging buffer and no
+    compaction copy: C is written once.  Returns None if a unit overflowed its
+    LDS slice (skewed columns); the caller then runs the binned path."""
+    dev = A.device
+    m = A.m
+    tot = info.flops // 2
+    caps = torch.tensor([int(ESC_LOAD * ESC_PCAP) * k for k in (1, 2, 4)], device=dev, dtype=nprod.dtype)
+    nsl = torch.pow(2, torch.bucketize(nprod, caps)).to(torch.int64)      # 1, 2, 4, 8 slices
+    nsl = torch.where(nprod > 0, nsl, torch.zeros_like(nsl))
+    rows = torch.arange(m, device=dev, dtype=torch.int32)
+    unit_row = torch.repeat_interleave(rows, nsl)
+    nunits = unit_row.numel()
+    first = torch.cumsum(nsl, 0) - nsl
+    k = torch.arange(nunits, device=dev) - first[unit_row.long()]
+    s = nsl[unit_row.long()]
+    q0 = k * 8 // s
+    q1 = (k + 1) * 8 // s
+    unit_q = (q0 | (q1 << 4)).to(torch.uint8)
+    hist = torch.bincount(nsl, minlength=9).tolist()
+    for sl, b in ((1, 7), (2, 8), (4, 9), (8, 10)):
+        if hist[sl]:
+            info.rows_per_bin_num[b] = hist[sl]
+    info.rows_per_bin_num["ordered_units"] = nunits
+    if B_ready is not None:
+        B = B_ready()
+    splits = _splits(B) if nunits > int(hist[1]) else None
+    # lane groups from the typical segment length of a unit
+    seg = info.mean_seg if info.mean_seg > 0 else B.nnz / max(B.m, 1)
+    lg = _group_log2(seg / max(1.0, nunits / max(m - hist[0], 1)))   # B-segment length per unit
+    ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    status = torch.zeros(nunits, dtype=torch.int64, device=dev)
+    out_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
+    flags = torch.zeros(m, dtype=torch.int32, device=dev)
+    Cci = torch.empty(tot, dtype=torch.int32, device=dev)
+    Cv = torch.empty(tot, dtype=torch.float32, device=dev)
+    P = _native.ptr
+    _native.check(_native.hip().spmm_spgemm_esc_ordered(
+        P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(splits) if splits is not None else None,
+        P(unit_row), P(unit_q), nunits, B.n, lg, P(ticket), P(status), tot, P(err), P(out_nnz), P(Cci), P(Cv),
+        P(flags), _native.stream_ptr(dev)), "spgemm_esc_ordered")
+    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(out_nnz, 0, out=rowptr[1:])
+    e, nnz = torch.stack([err[0].long(), rowptr[-1]]).tolist()
+    if e & 2:
+        raise RuntimeError("spgemm ordered: output beyond the product-count bound (kernel invariant violated)")
+    if e & 1:
+        info.rows_per_bin_num["ordered_fallback"] = 1
+        return None
+    info.nnz = nnz
+    return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)
 
 
 PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper

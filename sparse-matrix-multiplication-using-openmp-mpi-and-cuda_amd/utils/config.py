@@ -35,6 +35,8 @@ class Config:
     # one-pass over row chunks, compaction overlapped on a side stream: "auto" = when the plain
     # one-pass does not fit in memory, "on" = whenever the product is large enough, "off"
     spgemm_pipeline: str = field(default_factory=lambda: _env("SPMM_SPGEMM_PIPELINE", "auto", str))
+    # one-pass numeric writing rows at final offsets (decoupled look-back, no compaction copy)
+    spgemm_ordered: str = field(default_factory=lambda: _env("SPMM_SPGEMM_ORDERED", "auto", str))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

@@ -313,3 +313,39 @@ def test_streamed_spgemm_panels_concatenate_to_full_product():
         ref = full.row_slice(lo, hi)
         assert torch.equal(C.rowptr, ref.rowptr) and torch.equal(C.col, ref.col)
         assert torch.allclose(C.val, ref.val)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["uniform1", "uniform2", "uniform4", "wide8", "skewed_fallback"])
+def test_spgemm_gpu_ordered_onepass_matches_binned(monkeypatch, case):
+    """Ordered one-pass (units in row order, final offsets from a decoupled
+    look-back, no compaction) equals the binned path bit for bit in structure;
+    rows of 1 / 2 / 4 / 8 ESC slices; a row whose products crowd one column
+    eighth overflows its unit and falls back to the binned path."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    if case == "skewed_fallback":
+        k, n = 3000, 80000
+        A = gen_csr.uniform_csr(200, k, 0.05, seed=51, device=dev)
+        B = gen_csr.uniform_csr(k, n // 8, 0.03, seed=52, device=dev)   # every column in the first eighth
+        B = CS.CSR(k, n, B.rowptr, B.col, B.val)
+    else:
+        m, k, n, d = dict(uniform1=(3000, 8000, 8000, 0.012), uniform2=(2000, 10000, 20000, 0.011),
+                          uniform4=(1500, 10000, 20000, 0.0095), wide8=(300, 20000, 20000, 0.01))[case]
+        A = gen_csr.uniform_csr(m, k, d, seed=53, device=dev)
+        B = gen_csr.uniform_csr(k, n, d, seed=54, device=dev)
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", "on")
+    monkeypatch.setattr(CONFIG, "spgemm_ordered", "on")
+    i1 = SG.SpgemmInfo()
+    C1 = SG.spgemm(A, B, i1)
+    monkeypatch.setattr(CONFIG, "spgemm_ordered", "off")
+    C2 = SG.spgemm(A, B)
+    if case == "skewed_fallback":
+        assert i1.rows_per_bin_num.get("ordered_fallback") is None   # info reset by the fallback
+    else:
+        assert "ordered_units" in i1.rows_per_bin_num
+    assert torch.equal(C1.rowptr, C2.rowptr)
+    assert torch.equal(C1.col, C2.col)
+    assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    assert C1.is_sorted()

@@ -29,7 +29,7 @@ torch.cuda.synchronize()
 nprod = SG.row_nprod(A, B)
 row_nnz = SG.symbolic(A, B, nprod, info)
 for mode in (0,):
-    for phase in ("symbolic", "numeric", "onepass"):
+    for phase in ("symbolic", "numeric", "onepass", "ordered"):
         lib.spmm_spgemm_stamps(1, None)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -38,15 +38,18 @@ for mode in (0,):
         elif phase == "numeric":
             Cm = SG.numeric(A, B, row_nnz, info, nprod)
             del Cm
-        else:
+        elif phase == "onepass":
             Cm = SG.onepass(A, B, nprod, info)
+            del Cm
+        else:   # ordered one-pass: units (row, column eighths) in row order, look-back offsets
+            Cm = SG.onepass_ordered(A, B, nprod, info)
             del Cm
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         lib.spmm_spgemm_stamps(-1, buf)
         rows = max(buf[7], 1)
-        names = ["init+staging", "inserts", "rank", "write"]
-        per = {names[i]: buf[i] / rows for i in range(4)}
+        names = ["init+staging", "inserts", "rank", "write", "count+lookback"]
+        per = {names[i]: buf[i] / rows for i in range(5)}
         tot = sum(per.values())
         print(f"mode {mode} {phase}: wall {dt * 1e3:.1f} ms, rows {buf[7]}, cycles/row " +
               ", ".join(f"{k} {v:.0f} ({v / max(tot, 1) * 100:.0f}%)" for k, v in per.items()), flush=True)
