@@ -186,14 +186,24 @@ def main() -> None:
     else:
         step, flops, extra, cfg = run_chain(comm, args)
 
-    for _ in range(args.warmup):
+    last = [time.perf_counter()]
+
+    def progress(what: str, i: int) -> None:   # long steps (R-MAT scale 24: ~25 s on one GPU) report liveness
+        now = time.perf_counter()
+        if now - last[0] > 20.0 and comm.rank == 0:
+            print(f"[bench] {what} {i + 1} done", file=sys.stderr, flush=True)
+            last[0] = now
+
+    for i in range(args.warmup):
         out = step()
         del out
+        progress("warm-up", i)
     _sync_barrier(comm)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         out = None
         out = step()
+        progress("step", i)
     del out
     _sync_barrier(comm)
     dt = comm.allreduce_max(time.perf_counter() - t0)
