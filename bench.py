@@ -62,16 +62,26 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
 
     prob = MS.UniformProblem.build(n, density, comm, seed=args.seed)
     info = SpgemmInfo()
-    C = MS.rowblock_spgemm(prob.A, prob.B, comm, info)   # first (untimed) run also counts FLOPs
+    if args.decomp == "inner":
+        # A's column panel x B's row panel per rank, sparse reduce-scatter of C
+        from spmm_amd.parallel.partition import row_panels
+
+        Ac = prob.inner_operand()
+        counts = [b - a for a, b in row_panels(n, comm.world)]
+        C = MS.innerdim_spgemm(Ac, prob.B, comm, counts, info)
+        nnz_local = C.nnz
+        step = lambda: MS.innerdim_spgemm(Ac, prob.B, comm, counts)  # noqa: E731
+    else:
+        C = MS.rowblock_spgemm(prob.A, prob.B, comm, info)   # first (untimed) run also counts FLOPs
+        nnz_local = info.nnz
+        step = lambda: MS.rowblock_spgemm(prob.A, prob.B, comm)  # noqa: E731
     flops_local = info.flops
-    nnz_local = info.nnz
     del C
-    step = lambda: MS.rowblock_spgemm(prob.A, prob.B, comm)  # noqa: E731
     total_flops = _allreduce_sum(comm, flops_local)
     total_nnz = _allreduce_sum(comm, nnz_local)
     extra = dict(nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(total_nnz))
     return step, total_flops, extra, dict(model=model, n=n, density=density, dtype_values="fp32",
-                                          global_batch=1, seq_len=n, parallelism=f"rowblock{comm.world}")
+                                          global_batch=1, seq_len=n, parallelism=f"{'innerdim' if args.decomp == 'inner' else 'rowblock'}{comm.world}")
 
 
 def run_rmat(comm, args):
@@ -160,6 +170,9 @@ def main() -> None:
     ap.add_argument("--rmat-stream", default="auto", choices=["auto", "on", "off"],
                     help="produce C in consumed row panels (auto: when its product bound does not fit)")
     ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--decomp", default="rowblock", choices=["rowblock", "inner"],
+                    help="spgemm / spgemm64k: 1D row-block with B all-gathered (default), or inner-dimension "
+                         "split with a sparse reduce-scatter of C")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (gloo on GPUs: rehearse several ranks on one card)")

@@ -575,14 +575,14 @@ __device__ __forceinline__ int64_t ord_lookback(unsigned long long* status, int6
   return pre;
 }
 
-template <int PCAP, int NT, int NP, bool ORD = false>
+template <int PCAP, int NT, int NP, bool ORD = false, int NBT = ESC_NB>
 __global__ __launch_bounds__(NT, 4) void spgemm_esc(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
     const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
     const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols, int lg,
     const int32_t* __restrict__ row_cap, int32_t* __restrict__ out_nnz, const int64_t* __restrict__ Crp,
     int32_t* __restrict__ Cci, float* __restrict__ Cv, int32_t* __restrict__ flags, EscOrd ord) {
-  constexpr int NW = NT / 64, ACAP = NT, CCAP = 2 * NT, NB = ESC_NB;
+  constexpr int NW = NT / 64, ACAP = NT, CCAP = 2 * NT, NB = NBT;
   constexpr int BPT = NB / NT;                 // buckets per thread in the scan / sort
   constexpr int QSTEP = 8 / NP;
   constexpr int D = 4;
@@ -1320,12 +1320,23 @@ SPMM_EXPORT int spmm_spgemm_esc_ordered(const int64_t* Arp, const int32_t* Aci, 
                                         const int32_t* unit_row, const uint8_t* unit_q, int64_t nunits, int ncols,
                                         int lg, uint32_t* ticket, unsigned long long* status, int64_t cap,
                                         int32_t* err, int32_t* out_nnz, int32_t* Cci, float* Cv, int32_t* flags,
-                                        void* stream) {
+                                        int pcap, void* stream) {
   if (nunits <= 0) return 0;
   if (lg < 4 || lg > 6 || nunits > 0xffffffffll) return (int)hipErrorInvalidValue;
   EscOrd o{unit_row, unit_q, ticket, status, cap, err};
-  hipLaunchKernelGGL((spgemm_esc<7680, 512, 2, true>), dim3((unsigned)nunits), dim3(512), 0, (hipStream_t)stream, Arp,
-                     Aci, Av, Brp, Bci, Bv, bsplit, nullptr, ncols, lg, nullptr, out_nnz, nullptr, Cci, Cv, flags, o);
+  // pcap 7680: 512-thread workgroups, 80 KB of LDS (2 per CU); pcap 3840:
+  // 256 threads, 40 KB (4 per CU: twice the independent units per CU to hide
+  // the staging latency and the look-back waits, same bucket density)
+  if (pcap == 7680)
+    hipLaunchKernelGGL((spgemm_esc<7680, 512, 2, true>), dim3((unsigned)nunits), dim3(512), 0, (hipStream_t)stream,
+                       Arp, Aci, Av, Brp, Bci, Bv, bsplit, nullptr, ncols, lg, nullptr, out_nnz, nullptr, Cci, Cv,
+                       flags, o);
+  else if (pcap == 3840)
+    hipLaunchKernelGGL((spgemm_esc<3840, 256, 2, true, 2048>), dim3((unsigned)nunits), dim3(256), 0,
+                       (hipStream_t)stream, Arp, Aci, Av, Brp, Bci, Bv, bsplit, nullptr, ncols, lg, nullptr, out_nnz,
+                       nullptr, Cci, Cv, flags, o);
+  else
+    return (int)hipErrorInvalidValue;
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -14,6 +14,16 @@ ranks (sparse_matrix_mult.cu:437-456) and funnels partials to rank 0
 * each rank computes its C row panel = A_panel . B with the local gfx950
   SpGEMM; C stays distributed (no reduce needed: rows are disjoint).
 
+``innerdim_spgemm`` is the other 1D decomposition (north-star "reduce-scatter
+of C"): rank r holds A's COLUMN panel r and B's row panel r (the same slice
+of the inner dimension), computes a full-height sparse partial
+C_r = A[:, K_r] . B[K_r, :], and a sparse reduce-scatter sums the partials
+into C's row panels: an all-to-all-v over RCCL moves row panel p of every
+partial to rank p, which merges the P sorted partial panels with the SpGEMM
+kernel itself (``ops.spgemm.csr_sum``: [I .. I] . [C_0; ..; C_{P-1}]).  No
+operand is replicated; traffic is the partials' nnz, so it pays when B is
+large relative to C (deep inner dimension, few products per output).
+
 ``gather_rows`` reassembles a distributed CSR on one rank (tests, output).
 """
 from __future__ import annotations
@@ -25,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops.csr import CSR
-from ..ops.spgemm import SpgemmInfo, spgemm
+from ..ops.spgemm import SpgemmInfo, csr_sum, spgemm
 from ..parallel.comm import Comm
 from ..parallel.partition import row_panels
 from ..utils.gen_csr import uniform_csr
@@ -159,6 +169,64 @@ def rowblock_spgemm(A_panel: CSR, B_panel: CSR, comm: Comm, info: Optional[Spgem
     return spgemm(A_panel, B_meta, info, B_ready=ready)
 
 
+def _alltoall_v(comm: Comm, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
+    out = torch.empty(sum(recv), dtype=x.dtype, device=x.device)
+    dist.all_to_all_single(out, x.contiguous(), recv, send)
+    return out
+
+
+def sparse_reduce_scatter(partial: CSR, comm: Comm, row_counts: List[int],
+                          info: Optional[SpgemmInfo] = None) -> CSR:
+    """Sum every rank's full-height ``partial`` (same m x n on all ranks) and
+    return this rank's row panel of the sum (panels of ``row_counts`` rows,
+    rank order).
+
+    Three all-to-all-v exchanges (RCCL over xGMI, or gloo): per-destination
+    nnz, per-row counts (fixed-size, panel r is rows of rank r), then the
+    columns and values — partial rows are contiguous in CSR, so the send
+    buffers are the partial's own arrays, no packing copy.  The received
+    panels are merged on the SpGEMM kernels (``csr_sum``)."""
+    if not comm.is_dist:
+        return partial
+    if sum(row_counts) != partial.m or len(row_counts) != comm.world:
+        raise ValueError(f"row_counts {row_counts} do not split {partial.m} rows over {comm.world} ranks")
+    wd = partial.device if comm.backend == "nccl" else torch.device("cpu")
+    W = comm.world
+    offs = [0]
+    for c in row_counts:
+        offs.append(offs[-1] + c)
+    bounds = partial.rowptr[torch.tensor(offs, device=partial.device)]
+    nnz_to = (bounds[1:] - bounds[:-1]).to(wd)
+    nnz_from = _alltoall_v(comm, nnz_to, [1] * W, [1] * W)
+    send_n, recv_n = nnz_to.tolist(), nnz_from.tolist()
+    mp = row_counts[comm.rank]
+    cnt = (partial.rowptr[1:] - partial.rowptr[:-1]).to(wd)
+    cnt_from = _alltoall_v(comm, cnt, list(row_counts), [mp] * W)
+    col = _alltoall_v(comm, partial.col.to(wd), send_n, recv_n)
+    val = _alltoall_v(comm, partial.val.float().to(wd), send_n, recv_n)
+    dev = partial.device
+    cnt_from, col, val = cnt_from.to(dev).view(W, mp), col.to(dev), val.to(dev)
+    parts, e = [], 0
+    for r in range(W):
+        rp = torch.zeros(mp + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(cnt_from[r], 0, out=rp[1:])
+        parts.append(CSR(mp, partial.n, rp, col[e:e + recv_n[r]], val[e:e + recv_n[r]]))
+        e += recv_n[r]
+    return csr_sum(parts, info)
+
+
+def innerdim_spgemm(A_colpanel: CSR, B_panel: CSR, comm: Comm, row_counts: List[int],
+                    info: Optional[SpgemmInfo] = None) -> CSR:
+    """C's row panel of this rank, where rank r holds A[:, K_r] (all rows,
+    columns re-indexed from 0) and B[K_r, :]: local full-height partial
+    product, then :func:`sparse_reduce_scatter`.  ``info`` counts the local
+    product's FLOPs (the merge's additions are not counted)."""
+    local = spgemm(A_colpanel, B_panel, info)
+    if info is not None:
+        info.partial_nnz = local.nnz
+    return sparse_reduce_scatter(local, comm, row_counts)
+
+
 STREAM_MEM_FRACTION = 0.4   # of free device memory for one panel's C bound + staging (16 B / product)
 
 
@@ -241,6 +309,14 @@ class UniformProblem:
         A = uniform_csr(n, n, density, seed=seed, device=comm.device, rows=(lo, hi))
         B = uniform_csr(n, n, density, seed=seed + 1, device=comm.device, rows=(lo, hi))
         return UniformProblem(n, density, seed, (lo, hi), A, B)
+
+    def inner_operand(self) -> CSR:
+        """A's column panel over this rank's inner-dimension slice (the rows
+        ``self.rows`` of B), for :func:`innerdim_spgemm`: generated in full
+        (chunk-seeded, so identical on every rank) and column-sliced."""
+        lo, hi = self.rows
+        A = uniform_csr(self.n, self.n, self.density, seed=self.seed, device=self.A.device)
+        return A.col_slice(lo, hi)
 
 
 def smoke(dev: torch.device) -> None:

@@ -20,7 +20,7 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from ..ops.csr import CSR, from_coo
+from ..ops.csr import CSR
 from ..ops.spmm import PanelPlan, SpmmGraph, plan_panels, spmm
 from ..parallel.comm import Comm
 from ..parallel.partition import row_panels
@@ -84,10 +84,7 @@ def _gloo_reduce_scatter(out, full, comm: Comm, mx: int) -> None:
 
 def column_panel(A: CSR, lo: int, hi: int) -> CSR:
     """Columns [lo, hi) of A, re-indexed to start at 0 (all rows kept)."""
-    r = A.row_ids()
-    sel = (A.col >= lo) & (A.col < hi)
-    return from_coo(r[sel], (A.col[sel] - lo).long(), A.val[sel], A.m, hi - lo, sum_duplicates=False,
-                    dtype=A.val.dtype)
+    return A.col_slice(lo, hi)
 
 
 def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 128, seed: int = 1,

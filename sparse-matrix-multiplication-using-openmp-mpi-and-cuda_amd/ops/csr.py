@@ -63,10 +63,25 @@ class CSR:
         rows = self.row_ids()
         return from_coo(self.col.long(), rows, self.val, self.n, self.m)
 
+    def col_slice(self, lo: int, hi: int) -> "CSR":
+        """Columns [lo, hi), re-indexed from 0; all rows kept (the column panel
+        of an inner-dimension split).  Column order inside a row is kept."""
+        sel = (self.col >= lo) & (self.col < hi)
+        cnt = torch.zeros(self.m + 1, dtype=torch.int64, device=self.device)
+        if self.nnz:
+            cnt[1:] = _row_sum(sel, self)
+        return CSR(self.m, hi - lo, torch.cumsum(cnt, 0), (self.col[sel] - lo).to(torch.int32), self.val[sel])
+
     def row_slice(self, lo: int, hi: int) -> "CSR":
         s, e = int(self.rowptr[lo]), int(self.rowptr[hi])
         return CSR(hi - lo, self.n, (self.rowptr[lo:hi + 1] - s).contiguous(), self.col[s:e].contiguous(),
                    self.val[s:e].contiguous())
+
+
+def _row_sum(mask: torch.Tensor, A: "CSR") -> torch.Tensor:
+    out = torch.zeros(A.m, dtype=torch.int64, device=A.device)
+    out.index_add_(0, A.row_ids(), mask.to(torch.int64))
+    return out
 
 
 def rowptr_from_rows(rows_sorted: torch.Tensor, m: int) -> torch.Tensor:

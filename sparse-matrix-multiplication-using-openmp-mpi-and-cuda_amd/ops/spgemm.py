@@ -47,7 +47,7 @@ _native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, 
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     C_INT, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+                     C_INT, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
@@ -78,6 +78,7 @@ class SpgemmInfo:
     rows_per_bin_sym: Dict[int, int] = field(default_factory=dict)
     rows_per_bin_num: Dict[int, int] = field(default_factory=dict)
     resorted_rows: int = 0
+    partial_nnz: int = 0      # innerdim_spgemm: nnz of this rank's full-height partial before the merge
     mean_seg: float = 0.0     # mean B-row length per A entry (products / nnz(A)); picks the LDS lane groups
 
 
@@ -317,7 +318,7 @@ def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device) -> 
     if mode == "off" or total_products == 0:
         return False
     mx = int(nprod.max())
-    if mx > int(ESC_LOAD * ESC_PCAP) * 8:
+    if mx > int(ESC_LOAD * CONFIG.spgemm_ordered_pcap) * 8:
         return False
     if mode != "on":
         nz = int((nprod > 0).sum())
@@ -342,7 +343,8 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
     dev = A.device
     m = A.m
     tot = info.flops // 2
-    caps = torch.tensor([int(ESC_LOAD * ESC_PCAP) * k for k in (1, 2, 4)], device=dev, dtype=nprod.dtype)
+    pcap = CONFIG.spgemm_ordered_pcap
+    caps = torch.tensor([int(ESC_LOAD * pcap) * k for k in (1, 2, 4)], device=dev, dtype=nprod.dtype)
     nsl = torch.pow(2, torch.bucketize(nprod, caps)).to(torch.int64)      # 1, 2, 4, 8 slices
     nsl = torch.where(nprod > 0, nsl, torch.zeros_like(nsl))
     rows = torch.arange(m, device=dev, dtype=torch.int32)
@@ -376,7 +378,7 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
     _native.check(_native.hip().spmm_spgemm_esc_ordered(
         P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(splits) if splits is not None else None,
         P(unit_row), P(unit_q), nunits, B.n, lg, P(ticket), P(status), tot, P(err), P(out_nnz), P(Cci), P(Cv),
-        P(flags), _native.stream_ptr(dev)), "spgemm_esc_ordered")
+        P(flags), pcap, _native.stream_ptr(dev)), "spgemm_esc_ordered")
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     torch.cumsum(out_nnz, 0, out=rowptr[1:])
     e, nnz = torch.stack([err[0].long(), rowptr[-1]]).tolist()
@@ -629,3 +631,35 @@ def _spgemm_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:
                                     P(rowptr), P(col), P(val), 0)
     info.nnz = nnz
     return CSR(A.m, B.n, rowptr, col, val)
+
+
+def csr_sum(parts, info: Optional[SpgemmInfo] = None) -> CSR:
+    """Sum of same-shape CSR matrices, on the SpGEMM kernels: the sum of
+    P_0 .. P_{s-1} (each m x n) is S . V with V = [P_0; ..; P_{s-1}] stacked
+    by rows (s*m x n) and S = [I I .. I] (m x s*m), so row i of the result
+    merges row i of every part.  The number of intermediate products is the
+    total nnz of the parts; every product is one exact fp32 ``1 * v``, so the
+    result equals a fp32 sum of the parts (up to summation order).  The ESC /
+    hash accumulators sort and fold duplicates, which is exactly the sparse
+    merge that a reduce-scatter of sparse partials needs (there is no sparse
+    ``ncclSum``)."""
+    parts = list(parts)
+    if not parts:
+        raise ValueError("csr_sum needs at least one part")
+    m, n, dev = parts[0].m, parts[0].n, parts[0].device
+    for p in parts:
+        if (p.m, p.n) != (m, n):
+            raise ValueError(f"csr_sum: shape {(p.m, p.n)} != {(m, n)}")
+    s = len(parts)
+    if s == 1:
+        return parts[0]
+    counts = torch.cat([p.rowptr[1:] - p.rowptr[:-1] for p in parts])
+    vrp = torch.zeros(s * m + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(counts, 0, out=vrp[1:])
+    V = CSR(s * m, n, vrp, torch.cat([p.col for p in parts]),
+            torch.cat([p.val.float() for p in parts]))
+    srp = torch.arange(m + 1, dtype=torch.int64, device=dev) * s
+    scol = (torch.arange(s, dtype=torch.int32, device=dev).view(1, s) * m
+            + torch.arange(m, dtype=torch.int32, device=dev).view(m, 1)).reshape(-1)
+    S = CSR(m, s * m, srp, scol.contiguous(), torch.ones(m * s, dtype=torch.float32, device=dev))
+    return spgemm(S, V, info)

@@ -106,6 +106,59 @@ def test_rowblock_spgemm_gloo(tmp_path, world):
     check(C, A, B)
 
 
+def test_col_slice_and_csr_sum():
+    A = gen_csr.uniform_csr(90, 120, 0.08, seed=3)
+    Ad = A.to_dense()
+    for lo, hi in [(0, 40), (40, 120), (7, 8), (50, 50)]:
+        P = A.col_slice(lo, hi)
+        assert P.m == 90 and P.n == hi - lo and P.is_sorted()
+        assert torch.equal(P.to_dense(), Ad[:, lo:hi])
+    parts = [gen_csr.uniform_csr(90, 120, 0.05, seed=s) for s in range(5)] + [gen_csr.uniform_csr(90, 120, 0.0, seed=9)]
+    C = SG.csr_sum(parts)
+    ref = sum(p.to_dense() for p in parts)
+    assert C.is_sorted() and torch.allclose(C.to_dense(), ref, atol=1e-6)
+    assert C.nnz == int((ref != 0).sum())
+
+
+def _inner_worker(rank, world, port, n, d, tmp):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.parallel import comm as CM
+    from spmm_amd.parallel.partition import row_panels
+
+    comm = CM.init(backend="gloo", device="cpu", timeout_s=120)
+    try:
+        prob = MS.UniformProblem.build(n, d, comm, seed=7)
+        counts = [b - a for a, b in row_panels(n, world)]
+        info = SG.SpgemmInfo()
+        Cp = MS.innerdim_spgemm(prob.inner_operand(), prob.B, comm, counts, info)
+        assert Cp.m == counts[rank] and Cp.is_sorted() and info.partial_nnz > 0
+        C = MS.gather_rows(Cp, comm)
+        if rank == 0:
+            torch.save({"rp": C.rowptr, "col": C.col, "val": C.val}, os.path.join(tmp, "C.pt"))
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_innerdim_spgemm_gloo(tmp_path, world):
+    """Inner-dimension split (A column panel x B row panel per rank) + sparse
+    reduce-scatter (all-to-all-v + SpGEMM-kernel merge) equals A . B."""
+    n, d = 500, 0.03
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_inner_worker, args=(world, port, n, d, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = torch.load(os.path.join(tmp_path, "C.pt"), weights_only=True)
+    A = gen_csr.uniform_csr(n, n, d, seed=7)
+    B = gen_csr.uniform_csr(n, n, d, seed=8)
+    C = CS.CSR(n, n, got["rp"], got["col"], got["val"])
+    check(C, A, B)
+
+
 # ----------------------------------------------------------------- GPU ----
 
 @pytest.mark.gpu
@@ -349,3 +402,43 @@ def test_spgemm_gpu_ordered_onepass_matches_binned(monkeypatch, case):
     assert torch.equal(C1.col, C2.col)
     assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
     assert C1.is_sorted()
+
+
+@pytest.mark.gpu
+def test_csr_sum_gpu_vs_dense():
+    """Sparse sum of partials on the gfx950 SpGEMM kernels (selector-matrix
+    product) vs a dense fp32 sum."""
+    dev = torch.device("cuda", 0)
+    parts = [gen_csr.uniform_csr(3000, 5000, 0.004 * (s + 1), seed=s, device=dev) for s in range(6)]
+    C = SG.csr_sum(parts)
+    ref = sum(p.to_dense() for p in parts)
+    assert C.is_sorted()
+    assert torch.allclose(C.to_dense(), ref, atol=1e-5)
+    assert C.nnz == int((sum((p.to_dense() != 0).float() for p in parts) != 0).sum())
+
+
+@pytest.mark.gpu
+def test_innerdim_spgemm_rccl_one_rank(monkeypatch):
+    """Inner-dimension SpGEMM through the RCCL all-to-all-v path (one-rank
+    group) equals the local product."""
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.parallel import comm as CM
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    for k, v in dict(SPMM_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                     WORLD_SIZE="1", LOCAL_RANK="0").items():
+        monkeypatch.setenv(k, v)
+    comm = CM.init(backend="nccl", device="cuda")
+    try:
+        prob = MS.UniformProblem.build(40000, 5e-4, comm, seed=5)
+        info = SG.SpgemmInfo()
+        C1 = MS.innerdim_spgemm(prob.inner_operand(), prob.B, comm, [40000], info)
+        C2 = SG.spgemm(prob.A, prob.B)
+        assert info.flops > 0
+        assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+        assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    finally:
+        comm.close()
