@@ -9,7 +9,12 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import ctypes as C
+
 import torch
+
+from .. import _native
+from .._native import c_vp
 
 
 @dataclass
@@ -60,6 +65,10 @@ class CSR:
         return bool((code[1:] > code[:-1]).all())
 
     def transpose(self) -> "CSR":
+        """A^T in canonical CSR: the gfx950 kernels of csr_transpose.hip on
+        a GPU (``transpose_gpu``), a device sort otherwise."""
+        if self.device.type == "cuda":
+            return transpose_gpu(self)
         rows = self.row_ids()
         return from_coo(self.col.long(), rows, self.val, self.n, self.m)
 
@@ -76,6 +85,43 @@ class CSR:
         s, e = int(self.rowptr[lo]), int(self.rowptr[hi])
         return CSR(hi - lo, self.n, (self.rowptr[lo:hi + 1] - s).contiguous(), self.col[s:e].contiguous(),
                    self.val[s:e].contiguous())
+
+
+_native.register_hip("spmm_csr_col_count", c_vp, C.c_int64, c_vp, c_vp)
+_native.register_hip("spmm_csr_t_scatter", c_vp, c_vp, C.c_int64, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_csr_t_sort", C.c_int, c_vp, c_vp, C.c_int64, c_vp, c_vp)
+T_SORT_LDS = 2048   # csr_transpose.hip kSortLds
+
+
+def transpose_gpu(A: "CSR") -> "CSR":
+    """Column histogram -> scan -> atomic-cursor scatter of source indices ->
+    per-segment sort (wave bitonic <= 64, LDS bitonic <= 2048, device radix
+    sort for the few longer hub segments) -> gathers.  Requires A's columns
+    sorted inside rows only for the output to be canonical (ascending source
+    index is ascending row)."""
+    lib = _native.hip()
+    P, dev = _native.ptr, A.device
+    st = _native.stream_ptr(dev)
+    cnt = torch.zeros(A.n, dtype=torch.int64, device=dev)
+    _native.check(lib.spmm_csr_col_count(P(A.col), A.nnz, P(cnt), st), "csr_col_count")
+    trp = torch.zeros(A.n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt, 0, out=trp[1:])
+    cursor = trp[:-1].clone()
+    src = torch.empty(A.nnz, dtype=torch.int64, device=dev)
+    _native.check(lib.spmm_csr_t_scatter(P(A.rowptr), P(A.col), A.m, P(cursor), P(src), st), "csr_t_scatter")
+    short = torch.nonzero((cnt > 1) & (cnt <= 64)).view(-1)
+    mid = torch.nonzero((cnt > 64) & (cnt <= T_SORT_LDS)).view(-1)
+    long_ = torch.nonzero(cnt > T_SORT_LDS).view(-1)
+    _native.check(lib.spmm_csr_t_sort(0, P(trp), P(short), short.numel(), P(src), st), "csr_t_sort")
+    _native.check(lib.spmm_csr_t_sort(1, P(trp), P(mid), mid.numel(), P(src), st), "csr_t_sort")
+    if long_.numel():
+        lens = cnt[long_]
+        seg = torch.repeat_interleave(torch.arange(long_.numel(), device=dev), lens)
+        starts = torch.repeat_interleave(trp[long_], lens)
+        idx = starts + (torch.arange(seg.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens))
+        keyed = torch.sort(seg * (A.nnz + 1) + src[idx]).values
+        src[idx] = keyed - seg * (A.nnz + 1)
+    return CSR(A.n, A.m, trp, A.row_ids()[src].to(torch.int32), A.val[src])
 
 
 def _row_sum(mask: torch.Tensor, A: "CSR") -> torch.Tensor:

@@ -442,3 +442,21 @@ def test_innerdim_spgemm_rccl_one_rank(monkeypatch):
         assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
     finally:
         comm.close()
+
+
+@pytest.mark.gpu
+def test_csr_transpose_gpu_all_segment_classes():
+    """gfx950 transpose (histogram, atomic scatter, wave / LDS bitonic and
+    radix sorted segments) equals the CPU sort-based transpose, incl. a hub
+    column longer than the LDS sort and R-MAT power-law columns."""
+    dev = torch.device("cuda", 0)
+    rows = torch.cat([torch.arange(6000), torch.arange(0, 6000, 37), torch.arange(100, 1900, 3), torch.arange(50)])
+    cols = torch.cat([torch.full((6000,), 7), torch.full((163,), 11), torch.full((600,), 900), torch.arange(50) * 19])
+    vals = torch.randn(rows.numel())
+    hub = CS.from_coo(rows, cols, vals, 6000, 1000)
+    for A in (hub, gen_csr.uniform_csr(3000, 2500, 0.01, seed=3), gen_csr.rmat_csr(14, 16, seed=2)):
+        Tc = A.transpose()
+        Tg = A.to(dev).transpose()
+        assert Tg.m == A.n and Tg.n == A.m
+        assert torch.equal(Tg.rowptr.cpu(), Tc.rowptr) and torch.equal(Tg.col.cpu(), Tc.col)
+        assert torch.equal(Tg.val.cpu(), Tc.val)
