@@ -30,6 +30,10 @@ constexpr int EMPTY = -1;
 // the workgroup barriers that delimit it.  Read with spmm_spgemm_stamps().
 __device__ int g_stamp_on = 0;
 __device__ unsigned long long g_stamps[8];
+// Diagnostic only (never set by the library): the ordered ESC publishes its
+// prefix without waiting for predecessors (wrong offsets) — an upper bound on
+// what any look-back redesign could gain.  tools/lookback_bound.py.
+__device__ int g_nowait = 0;
 #define SPMM_STAMP(i)                                                              \
   do {                                                                             \
     if (stamp_on && threadIdx.x == 0) {                                            \
@@ -542,9 +546,9 @@ struct EscOrd {
 // window slides back only while all 64 are counts without a prefix.
 __device__ __forceinline__ int64_t ord_lookback(unsigned long long* status, int64_t u, int64_t count, int lane) {
   constexpr unsigned long long AGG = 1ull << 62, INC = 2ull << 62, VM = (1ull << 62) - 1;
-  if (u == 0) {
+  if (u == 0 || g_nowait) {
     if (lane == 0)
-      __hip_atomic_store(&status[0], INC | (unsigned long long)count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&status[u], INC | (unsigned long long)count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
   if (lane == 0)
@@ -1399,15 +1403,16 @@ SPMM_EXPORT int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch) {
   return 0;
 }
 
-// Diagnostics: enable/reset (on >= 0) or read the phase-cycle accumulators of
+// Diagnostics: enable/reset (on >= 0; bit 0 stamps, bit 1 g_nowait) or read the phase-cycle accumulators of
 // spgemm_lds: [0] init+A staging, [1] product inserts, [2] rank computation,
 // [3] output writes, [7] rows.
 SPMM_EXPORT int spmm_spgemm_stamps(int on, unsigned long long* out8) {
   if (on >= 0) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int st = on & 1;
+    const int st = on & 1, nw = (on >> 1) & 1;
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z);
     if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_on), &st, sizeof st);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_nowait), &nw, sizeof nw);
     return (int)e;
   }
   hipError_t e = hipDeviceSynchronize();
