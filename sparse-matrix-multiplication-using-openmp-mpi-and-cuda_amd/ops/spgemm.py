@@ -243,7 +243,16 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     A = A if A.val.dtype == torch.float32 else A.with_values(A.val.float())
     B = B if B.val.dtype == torch.float32 else B.with_values(B.val.float())
     nprod = row_nprod(A, B)
-    tot, mx = torch.stack([nprod.sum(), nprod.max() if A.m else nprod.sum()]).tolist()
+    # every host decision below (limits, mode, ordered-unit split) from ONE
+    # device->host read: each sync drains the stream and exposes Python
+    # launch latency, which matters for the small configs and for 8-way
+    # row panels (~20 ms steps)
+    nsl = _ordered_slices(nprod)
+    stats = torch.cat([torch.stack([nprod.sum(), nprod.max() if A.m else nprod.sum(), (nprod > 0).sum(),
+                                    ((nprod > 0) & (nprod <= ESC_MIN)).sum()]),
+                       torch.bincount(nsl, minlength=9)]).tolist()
+    tot, mx = stats[0], stats[1]
+    pre = dict(max=mx, nonempty=stats[2], light=stats[3], hist=stats[4:], nsl=nsl)
     if mx >= 1 << 31:   # per-row capacities and counts are int32 in the kernels
         raise ValueError(f"a row of A.B has {mx} intermediate products (limit 2^31 - 1)")
     info.flops = 2 * tot
@@ -257,8 +266,8 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
                 cached.append(fetch())
             return cached[0]
     mode = _onepass_mode(info.flops // 2, A.device)
-    if mode is not None and _ordered_ok(nprod, info.flops // 2, A.device):
-        C_ = onepass_ordered(A, B, nprod, info, B_ready)
+    if mode is not None and _ordered_ok(nprod, info.flops // 2, A.device, pre):
+        C_ = onepass_ordered(A, B, nprod, info, B_ready, pre)
         if C_ is not None:
             return C_
         info.rows_per_bin_num = {}
@@ -310,19 +319,32 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None)
 ORDERED_MAX_LIGHT = 0.05           # ordered mode: at most this share of non-empty rows below the ESC bins
 
 
-def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device) -> bool:
+def _ordered_slices(nprod: torch.Tensor) -> torch.Tensor:
+    """Units per row of the ordered one-pass: 1 / 2 / 4 / 8 column ranges by
+    product count (0 for empty rows)."""
+    caps = torch.tensor([int(ESC_LOAD * CONFIG.spgemm_ordered_pcap) * k for k in (1, 2, 4)], device=nprod.device,
+                        dtype=nprod.dtype)
+    nsl = torch.pow(2, torch.bucketize(nprod, caps)).to(torch.int64)
+    return torch.where(nprod > 0, nsl, torch.zeros_like(nsl))
+
+
+def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device, pre: Optional[dict] = None) -> bool:
     """Ordered one-pass: every non-empty row fits the bucketed-ESC kernel
     (no HBM long rows), few rows would be better served by the small LDS
-    tables, and C fits at its product-count bound."""
+    tables, and C fits at its product-count bound.  ``pre``: the row
+    statistics already read back by ``spgemm`` (max / nonempty / light)."""
     mode = CONFIG.spgemm_ordered
     if mode == "off" or total_products == 0:
         return False
-    mx = int(nprod.max())
+    mx = pre["max"] if pre is not None else int(nprod.max())
     if mx > int(ESC_LOAD * CONFIG.spgemm_ordered_pcap) * 8:
         return False
     if mode != "on":
-        nz = int((nprod > 0).sum())
-        light = int(((nprod > 0) & (nprod <= ESC_MIN)).sum())
+        if pre is not None:
+            nz, light = pre["nonempty"], pre["light"]
+        else:
+            nz = int((nprod > 0).sum())
+            light = int(((nprod > 0) & (nprod <= ESC_MIN)).sum())
         if light > ORDERED_MAX_LIGHT * nz:
             return False
         free, _ = torch.cuda.mem_get_info(dev)
@@ -332,7 +354,8 @@ def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device) -> 
     return True
 
 
-def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None) -> Optional[CSR]:
+def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None,
+                    pre: Optional[dict] = None) -> Optional[CSR]:
     """One-pass numeric that writes every row at its FINAL offset: rows are
     split into units (row, column-eighth range) of the bucketed-ESC kernel
     (1 / 2 / 4 / 8 per row by product count), walked in row order, and each
@@ -344,19 +367,20 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
     m = A.m
     tot = info.flops // 2
     pcap = CONFIG.spgemm_ordered_pcap
-    caps = torch.tensor([int(ESC_LOAD * pcap) * k for k in (1, 2, 4)], device=dev, dtype=nprod.dtype)
-    nsl = torch.pow(2, torch.bucketize(nprod, caps)).to(torch.int64)      # 1, 2, 4, 8 slices
-    nsl = torch.where(nprod > 0, nsl, torch.zeros_like(nsl))
+    if pre is not None:
+        nsl, hist = pre["nsl"], pre["hist"]
+    else:
+        nsl = _ordered_slices(nprod)
+        hist = torch.bincount(nsl, minlength=9).tolist()
+    nunits = sum(k * hist[k] for k in (1, 2, 4, 8))
     rows = torch.arange(m, device=dev, dtype=torch.int32)
-    unit_row = torch.repeat_interleave(rows, nsl)
-    nunits = unit_row.numel()
+    unit_row = torch.repeat_interleave(rows, nsl, output_size=nunits)
     first = torch.cumsum(nsl, 0) - nsl
     k = torch.arange(nunits, device=dev) - first[unit_row.long()]
     s = nsl[unit_row.long()]
     q0 = k * 8 // s
     q1 = (k + 1) * 8 // s
     unit_q = (q0 | (q1 << 4)).to(torch.uint8)
-    hist = torch.bincount(nsl, minlength=9).tolist()
     for sl, b in ((1, 7), (2, 8), (4, 9), (8, 10)):
         if hist[sl]:
             info.rows_per_bin_num[b] = hist[sl]
@@ -381,14 +405,16 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
         P(flags), pcap, _native.stream_ptr(dev)), "spgemm_esc_ordered")
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     torch.cumsum(out_nnz, 0, out=rowptr[1:])
-    e, nnz = torch.stack([err[0].long(), rowptr[-1]]).tolist()
+    # one read-back: error bits, nnz, and the flag summaries _finish needs
+    e, nnz, f4, f1 = torch.stack([err[0].long(), rowptr[-1], ((flags & 4) != 0).sum(),
+                                  ((flags & 1) != 0).sum()]).tolist()
     if e & 2:
         raise RuntimeError("spgemm ordered: output beyond the product-count bound (kernel invariant violated)")
     if e & 1:
         info.rows_per_bin_num["ordered_fallback"] = 1
         return None
     info.nnz = nnz
-    return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)
+    return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info, (f4, f1))
 
 
 PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper
@@ -499,9 +525,13 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
     return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)
 
 
-def _finish(C_: CSR, flags: torch.Tensor, info: SpgemmInfo) -> CSR:
-    if bool(((flags & 4) != 0).any()):
+def _finish(C_: CSR, flags: torch.Tensor, info: SpgemmInfo, counts=None) -> CSR:
+    """``counts``: (rows flagged 4, rows flagged 1) when already read back."""
+    f4, f1 = counts if counts is not None else (None, None)
+    if f4 if f4 is not None else bool(((flags & 4) != 0).any()):
         raise RuntimeError("spgemm numeric: output position out of range (kernel invariant violated)")
+    if f1 == 0:
+        return C_
     bad = ((flags & 1) != 0).nonzero().flatten()
     if bad.numel():
         info.resorted_rows = int(bad.numel())
