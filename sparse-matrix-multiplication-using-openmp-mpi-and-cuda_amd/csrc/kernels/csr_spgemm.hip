@@ -1205,6 +1205,97 @@ __global__ __launch_bounds__(256) void spgemm_row_nprod(const int64_t* __restric
   if (lane == 0) nprod[row] = s;
 }
 
+// Dispatcher plan in one pass over A (replaces ~40 small PyTorch launches per
+// SpGEMM call): nprod[i] as above, the ordered one-pass unit count nsl[i]
+// (0 for an empty row, else 1 / 2 / 4 / 8 by the caps, torch.bucketize
+// semantics: nprod <= cap1 -> 1), and per-workgroup partial statistics
+// part[blockIdx][8] = {sum, max, nonempty, light (0 < nprod <= esc_min),
+// #nsl==1, #nsl==2, #nsl==4, #nsl==8}, folded by spgemm_plan_finish.
+constexpr int kPlanStats = 8;
+constexpr int kPlanBlocks = 1024;
+
+__global__ __launch_bounds__(256) void spgemm_row_plan(const int64_t* __restrict__ Arp,
+                                                       const int32_t* __restrict__ Aci,
+                                                       const int64_t* __restrict__ Brp, int64_t m, int64_t cap1,
+                                                       int64_t cap2, int64_t cap4, int64_t esc_min,
+                                                       int64_t* __restrict__ nprod, int64_t* __restrict__ nsl,
+                                                       int64_t* __restrict__ part) {
+  __shared__ int64_t red[4][kPlanStats];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t acc[kPlanStats] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < m; row += (int64_t)gridDim.x * 4) {
+    int64_t s = 0;
+    for (int64_t e = Arp[row] + lane; e < Arp[row + 1]; e += 64) {
+      const int j = Aci[e];
+      s += Brp[j + 1] - Brp[j];
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);   // every lane holds the row total
+    const int k = s == 0 ? 0 : s <= cap1 ? 1 : s <= cap2 ? 2 : s <= cap4 ? 4 : 8;
+    if (lane == 0) {
+      nprod[row] = s;
+      nsl[row] = k;
+    }
+    acc[0] += s;
+    acc[1] = s > acc[1] ? s : acc[1];
+    acc[2] += s > 0;
+    acc[3] += (s > 0) & (s <= esc_min);
+    acc[4] += k == 1;
+    acc[5] += k == 2;
+    acc[6] += k == 4;
+    acc[7] += k == 8;
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < kPlanStats; ++i) red[wave][i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < kPlanStats) {
+    const int i = threadIdx.x;
+    int64_t v = red[0][i];
+    for (int w = 1; w < 4; ++w) v = i == 1 ? (red[w][i] > v ? red[w][i] : v) : v + red[w][i];
+    part[(int64_t)blockIdx.x * kPlanStats + i] = v;
+  }
+}
+
+// stats[i] = fold of part[0..nb)[i] (max for i == 1, sum otherwise); one workgroup.
+__global__ __launch_bounds__(256) void spgemm_plan_finish(const int64_t* __restrict__ part, int nb,
+                                                          int64_t* __restrict__ stats) {
+  __shared__ int64_t red[256];
+  const int i = threadIdx.x & (kPlanStats - 1), r0 = threadIdx.x / kPlanStats;
+  int64_t v = 0;
+  for (int r = r0; r < nb; r += 256 / kPlanStats) {
+    const int64_t x = part[(int64_t)r * kPlanStats + i];
+    v = i == 1 ? (x > v ? x : v) : v + x;
+  }
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int h = 128; h >= kPlanStats; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      const int64_t x = red[threadIdx.x + h];
+      red[threadIdx.x] = i == 1 ? (x > red[threadIdx.x] ? x : red[threadIdx.x]) : red[threadIdx.x] + x;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < kPlanStats) stats[threadIdx.x] = red[threadIdx.x];
+}
+
+// Ordered one-pass units from the inclusive scan of nsl: row i owns units
+// [incl[i] - nsl[i], incl[i]); unit k of s covers column eighths
+// [k * 8 / s, (k + 1) * 8 / s), stored as q0 | q1 << 4.
+__global__ __launch_bounds__(256) void spgemm_ordered_units(const int64_t* __restrict__ nsl,
+                                                            const int64_t* __restrict__ incl, int64_t m,
+                                                            int32_t* __restrict__ unit_row,
+                                                            uint8_t* __restrict__ unit_q) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= m) return;
+  const int s = (int)nsl[row];
+  const int64_t first = incl[row] - s;
+  for (int k = 0; k < s; ++k) {
+    unit_row[first + k] = (int32_t)row;
+    unit_q[first + k] = (uint8_t)((k * 8 / s) | (((k + 1) * 8 / s) << 4));
+  }
+}
+
 template <int S, int NT, int NP>
 int launch_sym(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, const int32_t* Bci, const int64_t* bsplit,
                const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz, int32_t* flags,
@@ -1247,6 +1338,31 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
   if (m <= 0) return 0;
   hipLaunchKernelGGL(spgemm_row_nprod, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Arp, Aci,
                      Brp, m, nprod);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// nprod / nsl: [m]; part: [1024 * 8] scratch; stats: [8] (see spgemm_row_plan).
+SPMM_EXPORT int spmm_spgemm_row_plan(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, int64_t m,
+                                     int64_t cap1, int64_t cap2, int64_t cap4, int64_t esc_min, int64_t* nprod,
+                                     int64_t* nsl, int64_t* part, int64_t* stats, void* stream) {
+  if (m < 0 || !(cap1 <= cap2 && cap2 <= cap4)) return (int)hipErrorInvalidValue;
+  const int64_t want = (m + 3) / 4;
+  const int nb = (int)(want < kPlanBlocks ? (want > 0 ? want : 1) : kPlanBlocks);
+  hipLaunchKernelGGL(spgemm_row_plan, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, Arp, Aci, Brp, m, cap1,
+                     cap2, cap4, esc_min, nprod, nsl, part);
+  SPMM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(spgemm_plan_finish, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nb, stats);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// unit_row / unit_q: [incl[m - 1]] (the host sizes them from the plan's stats).
+SPMM_EXPORT int spmm_spgemm_ordered_units(const int64_t* nsl, const int64_t* incl, int64_t m, int32_t* unit_row,
+                                          uint8_t* unit_q, void* stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(spgemm_ordered_units, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, nsl,
+                     incl, m, unit_row, unit_q);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -37,6 +37,9 @@ C_I64 = C.c_int64
 C_INT = C.c_int
 
 _native.register_hip("spmm_spgemm_row_nprod", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_row_plan", c_vp, c_vp, c_vp, C_I64, C_I64, C_I64, C_I64, C_I64, c_vp, c_vp, c_vp,
+                     c_vp, c_vp)
+_native.register_hip("spmm_spgemm_ordered_units", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_row_splits", c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
@@ -107,6 +110,27 @@ def _group(bins: torch.Tensor, nbins: int):
             groups.append((b, off, cnt))
         off += cnt
     return order, groups
+
+
+_PLAN_BLOCKS = 1024   # csr_spgemm.hip kPlanBlocks
+
+
+def row_plan(A: CSR, B: CSR):
+    """Device row plan (``spgemm_row_plan`` + ``spgemm_plan_finish``): per-row
+    product counts, ordered one-pass unit counts (``_ordered_slices``), and an
+    int64[8] of {sum, max, non-empty rows, light rows, #rows with 1 / 2 / 4 / 8
+    units}.  GPU only."""
+    dev = A.device
+    nprod = torch.empty(A.m, dtype=torch.int64, device=dev)
+    nsl = torch.empty(A.m, dtype=torch.int64, device=dev)
+    part = torch.empty(_PLAN_BLOCKS * 8 + 8, dtype=torch.int64, device=dev)
+    stats = part[_PLAN_BLOCKS * 8:]
+    c1 = int(ESC_LOAD * CONFIG.spgemm_ordered_pcap)
+    P = _native.ptr
+    _native.check(_native.hip().spmm_spgemm_row_plan(P(A.rowptr), P(A.col), P(B.rowptr), A.m, c1, 2 * c1, 4 * c1,
+                                                      ESC_MIN, P(nprod), P(nsl), P(part), P(stats),
+                                                      _native.stream_ptr(dev)), "spgemm_row_plan")
+    return nprod, nsl, stats
 
 
 def row_nprod(A: CSR, B: CSR) -> torch.Tensor:
@@ -242,17 +266,13 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
         return _spgemm_cpu(A, B_ready() if B_ready is not None else B, info)
     A = A if A.val.dtype == torch.float32 else A.with_values(A.val.float())
     B = B if B.val.dtype == torch.float32 else B.with_values(B.val.float())
-    nprod = row_nprod(A, B)
     # every host decision below (limits, mode, ordered-unit split) from ONE
-    # device->host read: each sync drains the stream and exposes Python
-    # launch latency, which matters for the small configs and for 8-way
-    # row panels (~20 ms steps)
-    nsl = _ordered_slices(nprod)
-    stats = torch.cat([torch.stack([nprod.sum(), nprod.max() if A.m else nprod.sum(), (nprod > 0).sum(),
-                                    ((nprod > 0) & (nprod <= ESC_MIN)).sum()]),
-                       torch.bincount(nsl, minlength=9)]).tolist()
-    tot, mx = stats[0], stats[1]
-    pre = dict(max=mx, nonempty=stats[2], light=stats[3], hist=stats[4:], nsl=nsl)
+    # device->host read of the row plan (two kernels): each sync drains the
+    # stream and exposes Python launch latency, which matters for the small
+    # configs and for 8-way row panels (~20 ms steps)
+    nprod, nsl, st = row_plan(A, B)
+    tot, mx, nz, light, h1, h2, h4, h8 = st.tolist()
+    pre = dict(max=mx, nonempty=nz, light=light, hist=[A.m - nz, h1, h2, 0, h4, 0, 0, 0, h8], nsl=nsl)
     if mx >= 1 << 31:   # per-row capacities and counts are int32 in the kernels
         raise ValueError(f"a row of A.B has {mx} intermediate products (limit 2^31 - 1)")
     info.flops = 2 * tot
@@ -373,14 +393,13 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
         nsl = _ordered_slices(nprod)
         hist = torch.bincount(nsl, minlength=9).tolist()
     nunits = sum(k * hist[k] for k in (1, 2, 4, 8))
-    rows = torch.arange(m, device=dev, dtype=torch.int32)
-    unit_row = torch.repeat_interleave(rows, nsl, output_size=nunits)
-    first = torch.cumsum(nsl, 0) - nsl
-    k = torch.arange(nunits, device=dev) - first[unit_row.long()]
-    s = nsl[unit_row.long()]
-    q0 = k * 8 // s
-    q1 = (k + 1) * 8 // s
-    unit_q = (q0 | (q1 << 4)).to(torch.uint8)
+    unit_row = torch.empty(nunits, dtype=torch.int32, device=dev)
+    unit_q = torch.empty(nunits, dtype=torch.uint8, device=dev)
+    incl = torch.cumsum(nsl, 0)
+    _native.check(_native.hip().spmm_spgemm_ordered_units(_native.ptr(nsl), _native.ptr(incl), m, _native.ptr(unit_row),
+                                                          _native.ptr(unit_q), _native.stream_ptr(dev)),
+                  "spgemm_ordered_units")
+    del incl
     for sl, b in ((1, 7), (2, 8), (4, 9), (8, 10)):
         if hist[sl]:
             info.rows_per_bin_num[b] = hist[sl]
@@ -391,11 +410,9 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
     # lane groups from the typical segment length of a unit
     seg = info.mean_seg if info.mean_seg > 0 else B.nnz / max(B.m, 1)
     lg = _group_log2(seg / max(1.0, nunits / max(m - hist[0], 1)))   # B-segment length per unit
-    ticket = torch.zeros(1, dtype=torch.int32, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    z = torch.zeros(2 + 2 * m, dtype=torch.int32, device=dev)   # one fill for the four int32 zero arrays
+    ticket, err, out_nnz, flags = z[0:1], z[1:2], z[2:2 + m], z[2 + m:]
     status = torch.zeros(nunits, dtype=torch.int64, device=dev)
-    out_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
-    flags = torch.zeros(m, dtype=torch.int32, device=dev)
     Cci = torch.empty(tot, dtype=torch.int32, device=dev)
     Cv = torch.empty(tot, dtype=torch.float32, device=dev)
     P = _native.ptr

@@ -460,3 +460,41 @@ def test_csr_transpose_gpu_all_segment_classes():
         assert Tg.m == A.n and Tg.n == A.m
         assert torch.equal(Tg.rowptr.cpu(), Tc.rowptr) and torch.equal(Tg.col.cpu(), Tc.col)
         assert torch.equal(Tg.val.cpu(), Tc.val)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n,d", [(0, 10, 10, 0.1), (1, 50, 50, 0.2), (5000, 3000, 4000, 0.004),
+                                     (700, 20000, 20000, 0.012)])
+def test_spgemm_row_plan_matches_torch(m, k, n, d):
+    """spgemm_row_plan + spgemm_plan_finish (one launch pair, one read-back)
+    against the PyTorch computation it replaces: per-row product counts, the
+    ordered unit counts, and the folded statistics; spgemm_ordered_units
+    against repeat_interleave."""
+    from spmm_amd import _native
+
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, k, d, seed=61, device=dev)
+    B = gen_csr.uniform_csr(k, n, d, seed=62, device=dev)
+    nprod, nsl, st = SG.row_plan(A, B)
+    ref = SG.row_nprod(A, B)
+    assert torch.equal(nprod, ref)
+    assert torch.equal(nsl, SG._ordered_slices(ref))
+    tot, mx, nz, light, h1, h2, h4, h8 = st.tolist()
+    assert tot == int(ref.sum()) and mx == (int(ref.max()) if m else 0)
+    assert nz == int((ref > 0).sum()) and light == int(((ref > 0) & (ref <= SG.ESC_MIN)).sum())
+    hist = torch.bincount(nsl.cpu(), minlength=9).tolist()
+    assert [h1, h2, h4, h8] == [hist[1], hist[2], hist[4], hist[8]]
+    if m == 0:
+        return
+    nunits = int(nsl.sum())
+    unit_row = torch.empty(nunits, dtype=torch.int32, device=dev)
+    unit_q = torch.empty(nunits, dtype=torch.uint8, device=dev)
+    incl = torch.cumsum(nsl, 0)
+    P = _native.ptr
+    _native.check(_native.hip().spmm_spgemm_ordered_units(P(nsl), P(incl), m, P(unit_row), P(unit_q),
+                                                          _native.stream_ptr(dev)), "spgemm_ordered_units")
+    rows = torch.repeat_interleave(torch.arange(m, device=dev, dtype=torch.int32), nsl)
+    assert torch.equal(unit_row, rows)
+    kk = torch.arange(nunits, device=dev) - (incl - nsl)[rows.long()]
+    s = nsl[rows.long()]
+    assert torch.equal(unit_q, ((kk * 8 // s) | (((kk + 1) * 8 // s) << 4)).to(torch.uint8))
