@@ -144,7 +144,28 @@ def row_nprod(A: CSR, B: CSR) -> torch.Tensor:
     return nprod
 
 
-def _onepass_mode(total_products: int, dev: torch.device, allow_pipeline: bool = True) -> Optional[str]:
+class _FreeMem:
+    """Device bytes free to this process, asked lazily: the driver's free
+    memory (hipMemGetInfo, ~2 us) answers most questions; the caching
+    allocator's spare (reserved - allocated: ~70 us, it builds the full
+    allocator statistics) is added only when the driver figure alone is too
+    small, e.g. when an earlier product's C is still cached in the pool."""
+
+    def __init__(self, dev: torch.device):
+        self.dev = dev
+        self.driver = torch.cuda.mem_get_info(dev)[0]
+        self.spare = None
+
+    def fits(self, nbytes: float, frac: float = 0.8) -> bool:
+        if nbytes <= frac * self.driver:
+            return True
+        if self.spare is None:
+            self.spare = torch.cuda.memory_reserved(self.dev) - torch.cuda.memory_allocated(self.dev)
+        return nbytes <= frac * (self.driver + self.spare)
+
+
+def _onepass_mode(total_products: int, dev: torch.device, allow_pipeline: bool = True,
+                  pre_free: Optional[_FreeMem] = None) -> Optional[str]:
     """"plain": a product-count-sized staging buffer next to C (fastest);
     "pipelined": C at its product-count bound plus two chunk-sized staging
     buffers (~half the memory, ~3 % slower: the overlapped compaction and
@@ -157,11 +178,10 @@ def _onepass_mode(total_products: int, dev: torch.device, allow_pipeline: bool =
         return "pipelined"
     if mode == "on":
         return "plain"
-    free, _ = torch.cuda.mem_get_info(dev)
-    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)   # the caching allocator's spare
-    if 2 * total_products * 8 <= 0.8 * free:
+    free = pre_free if pre_free is not None else _FreeMem(dev)
+    if free.fits(2 * total_products * 8):
         return "plain"
-    if pipe_ok and (total_products + 2 * PIPE_CHUNK_PRODUCTS) * 8 <= 0.8 * free:
+    if pipe_ok and free.fits((total_products + 2 * PIPE_CHUNK_PRODUCTS) * 8):
         return "pipelined"
     return None
 
@@ -285,7 +305,9 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
             if not cached:
                 cached.append(fetch())
             return cached[0]
-    mode = _onepass_mode(info.flops // 2, A.device)
+    if CONFIG.spgemm_onepass == "auto" or CONFIG.spgemm_ordered == "auto":
+        pre["free"] = _FreeMem(A.device)
+    mode = _onepass_mode(info.flops // 2, A.device, pre_free=pre.get("free"))
     if mode is not None and _ordered_ok(nprod, info.flops // 2, A.device, pre):
         C_ = onepass_ordered(A, B, nprod, info, B_ready, pre)
         if C_ is not None:
@@ -367,9 +389,8 @@ def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device, pre
             light = int(((nprod > 0) & (nprod <= ESC_MIN)).sum())
         if light > ORDERED_MAX_LIGHT * nz:
             return False
-        free, _ = torch.cuda.mem_get_info(dev)
-        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-        if total_products * 8 > 0.8 * free:
+        free = pre["free"] if pre is not None and pre.get("free") is not None else _FreeMem(dev)
+        if not free.fits(total_products * 8):
             return False
     return True
 
