@@ -498,3 +498,16 @@ def test_spgemm_row_plan_matches_torch(m, k, n, d):
     kk = torch.arange(nunits, device=dev) - (incl - nsl)[rows.long()]
     s = nsl[rows.long()]
     assert torch.equal(unit_q, ((kk * 8 // s) | (((kk + 1) * 8 // s) << 4)).to(torch.uint8))
+
+
+def test_free_mem_asks_allocator_only_when_needed(monkeypatch):
+    """The dispatcher's free-memory check reads the caching allocator's
+    statistics (slow) only when the driver's free figure alone is too small."""
+    calls = []
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (1000, 4000))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda dev=None: calls.append("r") or 3000)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda dev=None: calls.append("a") or 1000)
+    f = SG._FreeMem(torch.device("cpu"))
+    assert f.fits(800) and not calls             # 800 <= 0.8 * 1000
+    assert f.fits(2000) and calls == ["r", "a"]  # 2000 <= 0.8 * (1000 + 2000)
+    assert not f.fits(2500) and calls == ["r", "a"]   # spare cached
