@@ -934,23 +934,23 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
 
 // Eighth split points of every B row (rows column-sorted): bsplit[j*7 + q-1] =
 // first index of row j whose column >= floor(q * ncols / 8), q = 1..7.
+// Eight lanes per row, lane q searches split q: seven short independent
+// binary searches instead of one thread chaining all seven (the searches
+// are latency bound: ~log2(row length) dependent loads each).
 __global__ __launch_bounds__(256) void spgemm_row_splits(const int64_t* __restrict__ Brp,
                                                          const int32_t* __restrict__ Bci, int64_t mb, int ncols,
                                                          int64_t* __restrict__ bsplit) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= mb) return;
-  const int64_t lo0 = Brp[j], hi0 = Brp[j + 1];
-  int64_t lo = lo0;
-#pragma unroll
-  for (int q = 1; q <= 7; ++q) {
-    const int bound = (int)(((int64_t)q * ncols) >> 3);
-    int64_t hi = hi0;   // first index with col >= bound (search starts at the previous split)
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (Bci[mid] < bound) lo = mid + 1; else hi = mid;
-    }
-    bsplit[j * 7 + q - 1] = lo;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t j = t >> 3;
+  const int q = (int)(t & 7);
+  if (j >= mb || q == 0) return;
+  const int bound = (int)(((int64_t)q * ncols) >> 3);
+  int64_t lo = Brp[j], hi = Brp[j + 1];   // first index with col >= bound
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (Bci[mid] < bound) lo = mid + 1; else hi = mid;
   }
+  bsplit[j * 7 + q - 1] = lo;
 }
 
 // One-pass mode: rows were written at their product-count offsets (src_off);
@@ -1379,8 +1379,9 @@ SPMM_EXPORT int spmm_spgemm_compact(const int64_t* src_off, const int64_t* dst_o
 SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int ncols,
                                        int64_t* bsplit, void* stream) {
   if (mb <= 0) return 0;
-  hipLaunchKernelGGL(spgemm_row_splits, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Brp,
-                     Bci, mb, ncols, bsplit);
+  if (mb > (1ll << 34)) return (int)hipErrorInvalidValue;   // grid of 8 lanes per row
+  hipLaunchKernelGGL(spgemm_row_splits, dim3((unsigned)((mb * 8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     Brp, Bci, mb, ncols, bsplit);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

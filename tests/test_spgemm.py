@@ -511,3 +511,20 @@ def test_free_mem_asks_allocator_only_when_needed(monkeypatch):
     assert f.fits(800) and not calls             # 800 <= 0.8 * 1000
     assert f.fits(2000) and calls == ["r", "a"]  # 2000 <= 0.8 * (1000 + 2000)
     assert not f.fits(2500) and calls == ["r", "a"]   # spare cached
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d", [(3000, 0.02), (70000, 0.0015)])
+def test_spgemm_row_splits_match_searchsorted(n, d):
+    """Eighth split points of every B row (8 lanes per row, one binary search
+    per lane) against torch.searchsorted on each row."""
+    dev = torch.device("cuda")
+    B = gen_csr.uniform_csr(n, n, d, seed=81, device=dev)
+    B = CS.CSR(B.m, B.n, B.rowptr, B.col, B.val)
+    sp = SG._splits(B).view(B.m, 7).cpu()
+    rp, col = B.rowptr.cpu(), B.col.cpu()
+    bounds = torch.tensor([(q * B.n) >> 3 for q in range(1, 8)], dtype=torch.int32)
+    for j in list(range(min(B.m, 300))) + [B.m - 1]:
+        lo, hi = int(rp[j]), int(rp[j + 1])
+        ref = lo + torch.searchsorted(col[lo:hi].contiguous(), bounds)
+        assert torch.equal(sp[j], ref.to(torch.int64)), j
