@@ -1209,9 +1209,11 @@ __global__ __launch_bounds__(256) void spgemm_row_nprod(const int64_t* __restric
 // SpGEMM call): nprod[i] as above, the ordered one-pass unit count nsl[i]
 // (0 for an empty row, else 1 / 2 / 4 / 8 by the caps, torch.bucketize
 // semantics: nprod <= cap1 -> 1), and per-workgroup partial statistics
-// part[blockIdx][8] = {sum, max, nonempty, light (0 < nprod <= esc_min),
-// #nsl==1, #nsl==2, #nsl==4, #nsl==8}, folded by spgemm_plan_finish.
-constexpr int kPlanStats = 8;
+// part[blockIdx][16] = {sum, max, nonempty, light (0 < nprod <= esc_min),
+// #nsl==1, #nsl==2, #nsl==4, #nsl==8, max nnz of an A row, 0 x 7}, folded by
+// spgemm_plan_finish (max for slots 1 and 8, sum otherwise).
+constexpr int kPlanStats = 16;
+__device__ __forceinline__ bool plan_is_max(int i) { return i == 1 || i == 8; }
 constexpr int kPlanBlocks = 1024;
 
 __global__ __launch_bounds__(256) void spgemm_row_plan(const int64_t* __restrict__ Arp,
@@ -1222,7 +1224,7 @@ __global__ __launch_bounds__(256) void spgemm_row_plan(const int64_t* __restrict
                                                        int64_t* __restrict__ part) {
   __shared__ int64_t red[4][kPlanStats];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t acc[kPlanStats] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t acc[kPlanStats] = {};
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < m; row += (int64_t)gridDim.x * 4) {
     int64_t s = 0;
     for (int64_t e = Arp[row] + lane; e < Arp[row + 1]; e += 64) {
@@ -1244,6 +1246,8 @@ __global__ __launch_bounds__(256) void spgemm_row_plan(const int64_t* __restrict
     acc[5] += k == 2;
     acc[6] += k == 4;
     acc[7] += k == 8;
+    const int64_t na = Arp[row + 1] - Arp[row];
+    acc[8] = na > acc[8] ? na : acc[8];
   }
   if (lane == 0)
 #pragma unroll
@@ -1252,7 +1256,7 @@ __global__ __launch_bounds__(256) void spgemm_row_plan(const int64_t* __restrict
   if (threadIdx.x < kPlanStats) {
     const int i = threadIdx.x;
     int64_t v = red[0][i];
-    for (int w = 1; w < 4; ++w) v = i == 1 ? (red[w][i] > v ? red[w][i] : v) : v + red[w][i];
+    for (int w = 1; w < 4; ++w) v = plan_is_max(i) ? (red[w][i] > v ? red[w][i] : v) : v + red[w][i];
     part[(int64_t)blockIdx.x * kPlanStats + i] = v;
   }
 }
@@ -1265,14 +1269,14 @@ __global__ __launch_bounds__(256) void spgemm_plan_finish(const int64_t* __restr
   int64_t v = 0;
   for (int r = r0; r < nb; r += 256 / kPlanStats) {
     const int64_t x = part[(int64_t)r * kPlanStats + i];
-    v = i == 1 ? (x > v ? x : v) : v + x;
+    v = plan_is_max(i) ? (x > v ? x : v) : v + x;
   }
   red[threadIdx.x] = v;
   __syncthreads();
   for (int h = 128; h >= kPlanStats; h >>= 1) {
     if ((int)threadIdx.x < h) {
       const int64_t x = red[threadIdx.x + h];
-      red[threadIdx.x] = i == 1 ? (x > red[threadIdx.x] ? x : red[threadIdx.x]) : red[threadIdx.x] + x;
+      red[threadIdx.x] = plan_is_max(i) ? (x > red[threadIdx.x] ? x : red[threadIdx.x]) : red[threadIdx.x] + x;
     }
     __syncthreads();
   }
@@ -1342,7 +1346,7 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
   return 0;
 }
 
-// nprod / nsl: [m]; part: [1024 * 8] scratch; stats: [8] (see spgemm_row_plan).
+// nprod / nsl: [m]; part: [1024 * 16] scratch; stats: [16] (see spgemm_row_plan).
 SPMM_EXPORT int spmm_spgemm_row_plan(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, int64_t m,
                                      int64_t cap1, int64_t cap2, int64_t cap4, int64_t esc_min, int64_t* nprod,
                                      int64_t* nsl, int64_t* part, int64_t* stats, void* stream) {

@@ -52,6 +52,11 @@ _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
+_native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
+                     c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -113,18 +118,19 @@ def _group(bins: torch.Tensor, nbins: int):
 
 
 _PLAN_BLOCKS = 1024   # csr_spgemm.hip kPlanBlocks
+_PLAN_STATS = 16      # csr_spgemm.hip kPlanStats
 
 
 def row_plan(A: CSR, B: CSR):
     """Device row plan (``spgemm_row_plan`` + ``spgemm_plan_finish``): per-row
     product counts, ordered one-pass unit counts (``_ordered_slices``), and an
-    int64[8] of {sum, max, non-empty rows, light rows, #rows with 1 / 2 / 4 / 8
-    units}.  GPU only."""
+    int64[16] of {sum, max, non-empty rows, light rows, #rows with 1 / 2 / 4 / 8
+    units, max nnz of an A row, 0 ...}.  GPU only."""
     dev = A.device
     nprod = torch.empty(A.m, dtype=torch.int64, device=dev)
     nsl = torch.empty(A.m, dtype=torch.int64, device=dev)
-    part = torch.empty(_PLAN_BLOCKS * 8 + 8, dtype=torch.int64, device=dev)
-    stats = part[_PLAN_BLOCKS * 8:]
+    part = torch.empty((_PLAN_BLOCKS + 1) * _PLAN_STATS, dtype=torch.int64, device=dev)
+    stats = part[_PLAN_BLOCKS * _PLAN_STATS:]
     c1 = int(ESC_LOAD * CONFIG.spgemm_ordered_pcap)
     P = _native.ptr
     _native.check(_native.hip().spmm_spgemm_row_plan(P(A.rowptr), P(A.col), P(B.rowptr), A.m, c1, 2 * c1, 4 * c1,
@@ -291,8 +297,8 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     # stream and exposes Python launch latency, which matters for the small
     # configs and for 8-way row panels (~20 ms steps)
     nprod, nsl, st = row_plan(A, B)
-    tot, mx, nz, light, h1, h2, h4, h8 = st.tolist()
-    pre = dict(max=mx, nonempty=nz, light=light, hist=[A.m - nz, h1, h2, 0, h4, 0, 0, 0, h8], nsl=nsl)
+    tot, mx, nz, light, h1, h2, h4, h8, amax = st.tolist()[:9]
+    pre = dict(max=mx, nonempty=nz, light=light, hist=[A.m - nz, h1, h2, 0, h4, 0, 0, 0, h8], nsl=nsl, amax=amax)
     if mx >= 1 << 31:   # per-row capacities and counts are int32 in the kernels
         raise ValueError(f"a row of A.B has {mx} intermediate products (limit 2^31 - 1)")
     info.flops = 2 * tot
@@ -305,6 +311,11 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
             if not cached:
                 cached.append(fetch())
             return cached[0]
+    if _bitmap_ok(A, B, info.flops // 2, pre):
+        C_ = onepass_bitmap(A, B, info, B_ready, pre)
+        if C_ is not None:
+            return C_
+        info.rows_per_bin_num = {}
     if CONFIG.spgemm_onepass == "auto" or CONFIG.spgemm_ordered == "auto":
         pre["free"] = _FreeMem(A.device)
     mode = _onepass_mode(info.flops // 2, A.device, pre_free=pre.get("free"))
@@ -453,6 +464,113 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
         return None
     info.nnz = nnz
     return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info, (f4, f1))
+
+
+_BM_CFGS = {}
+BM_FILL = 0.7              # mean products per window <= BM_FILL * fast capacity
+
+
+def _bm_config(cfg: int):
+    """(log2 window, windows per count unit, fast-kernel product capacity,
+    register rounds, longest stageable A row) of bitmap configuration ``cfg``."""
+    if cfg not in _BM_CFGS:
+        v = [C.c_int() for _ in range(5)]
+        _native.check(_native.hip().spmm_spgemm_bm_config(cfg, *[C.byref(x) for x in v]), "spgemm_bm_config")
+        _BM_CFGS[cfg] = tuple(x.value for x in v)
+    return _BM_CFGS[cfg]
+
+
+def _bm_pick(mean_row_products: float, ncols: int) -> Optional[int]:
+    """The configuration with the widest window whose mean products per window
+    fit BM_FILL of its fast capacity (widest = fewest units per row)."""
+    best = None
+    for cfg in (0, 2, 1):   # widest window first
+        lgw, _, pcap, _, _ = _bm_config(cfg)
+        W = 1 << lgw
+        per_window = mean_row_products * min(W, ncols) / max(ncols, 1)
+        if per_window <= BM_FILL * pcap:
+            best = cfg
+            break
+    return best
+
+
+def _bitmap_ok(A: CSR, B: CSR, total_products: int, pre: dict) -> bool:
+    """Bitmap-rank path: uint32 B indices, every A row stageable by the reload
+    kernel, row products not far above the mean (the windows are sized from
+    the mean; a skewed matrix, e.g. R-MAT, takes the binned path)."""
+    mode = CONFIG.spgemm_bitmap
+    if mode == "off" or total_products == 0 or B.nnz >= (1 << 31) or B.n >= (1 << 30):
+        return False
+    nz = max(pre["nonempty"], 1)
+    mean = total_products / nz
+    cfg = CONFIG.spgemm_bitmap_cfg if CONFIG.spgemm_bitmap_cfg >= 0 else _bm_pick(mean, B.n)
+    if cfg is None:
+        cfg = 1 if mode == "on" else None
+    if cfg is None or pre.get("amax", 1 << 30) > _bm_config(cfg)[4]:
+        return False
+    if mode == "on":
+        return True
+    if pre["max"] > 4 * mean or nz < 0.5 * A.m:
+        return False
+    return _FreeMem(A.device).fits(total_products * 8 + A.m * 64)
+
+
+def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional[dict] = None) -> Optional[CSR]:
+    """Bitmap-rank SpGEMM (csr_spgemm_bitmap.hip): a count kernel gives the
+    exact nnz of every (row, column window) unit, one scan gives every unit's
+    final offset, and the numeric kernel writes each unit there once (no
+    look-back, no staging buffer, no compaction).  Returns None when a unit
+    does not fit even the reload kernel; the caller then runs the binned
+    path."""
+    dev = A.device
+    m = A.m
+    tot = info.flops // 2
+    nz = max(pre["nonempty"], 1) if pre is not None else max(m, 1)
+    cfg = CONFIG.spgemm_bitmap_cfg if CONFIG.spgemm_bitmap_cfg >= 0 else _bm_pick(tot / nz, B.n)
+    if cfg is None:
+        cfg = 1
+    lgw, nsub, pcap, rounds, _ = _bm_config(cfg)
+    nwin = max(1, -(-B.n // (1 << lgw)))
+    if B_ready is not None:
+        B = B_ready()
+    lib = _native.hip()
+    P = _native.ptr
+    st = _native.stream_ptr(dev)
+    ws = torch.empty(B.m * (nwin + 1), dtype=torch.int32, device=dev)
+    _native.check(lib.spmm_spgemm_bm_splits(P(B.rowptr), P(B.col), B.m, lgw, nwin, P(ws), st), "spgemm_bm_splits")
+    seg = info.mean_seg if info.mean_seg > 0 else B.nnz / max(B.m, 1)
+    lg_count = _group_log2(seg * min(nsub, nwin) / nwin)
+    lg_num = 4 if seg / nwin < 48 else (5 if seg / nwin < 96 else 6)
+    nunits = m * nwin
+    z = torch.zeros(2, dtype=torch.int32, device=dev)   # err, deferred count
+    err, novf = z[0:1], z[1:2]
+    ucnt = torch.empty(nunits, dtype=torch.int32, device=dev)
+    _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, lg_count, P(ucnt),
+                                           P(err), st), "spgemm_bm_count")
+    uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
+    uoff[0] = 0
+    torch.cumsum(ucnt, 0, out=uoff[1:])
+    del ucnt
+    nnz = int(uoff[-1])
+    info.nnz = nnz
+    Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
+    Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
+    ovf_cap = min(nunits, 1 << 20)
+    ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
+    _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m, nwin,
+                                             lg_num, P(uoff), P(Cci), P(Cv), P(ovf), P(novf), ovf_cap, P(err), st),
+                  "spgemm_bm_numeric")
+    e, deferred = z.tolist()
+    info.rows_per_bin_num["bitmap_units"] = nunits
+    info.rows_per_bin_num["bitmap_cfg"] = cfg
+    info.rows_per_bin_num["bitmap_deferred"] = deferred
+    if e & 2:
+        raise RuntimeError("spgemm bitmap: numeric and count kernels disagree (kernel invariant violated)")
+    if e & 5:
+        info.rows_per_bin_num["bitmap_fallback"] = 1
+        return None
+    rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
+    return CSR(m, B.n, rowptr, Cci, Cv)
 
 
 PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper

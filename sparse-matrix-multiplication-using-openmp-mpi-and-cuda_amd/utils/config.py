@@ -39,6 +39,11 @@ class Config:
     spgemm_ordered: str = field(default_factory=lambda: _env("SPMM_SPGEMM_ORDERED", "auto", str))
     # products per ordered unit: 7680 (512-thread workgroups, 2 per CU) or 3840 (256 threads, 4 per CU)
     spgemm_ordered_pcap: int = field(default_factory=lambda: _env("SPMM_SPGEMM_ORDERED_PCAP", 7680, int))
+    # bitmap-rank SpGEMM (count kernel + numeric kernel, exact offsets, no look-back):
+    # "auto" = when every row's columns look uniform enough for its windows, "on", "off"
+    spgemm_bitmap: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP", "auto", str))
+    # its window configuration (csr_spgemm_bitmap.hip kCfgs), -1 = chosen from the row statistics
+    spgemm_bitmap_cfg: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CFG", -1, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

@@ -479,8 +479,9 @@ def test_spgemm_row_plan_matches_torch(m, k, n, d):
     ref = SG.row_nprod(A, B)
     assert torch.equal(nprod, ref)
     assert torch.equal(nsl, SG._ordered_slices(ref))
-    tot, mx, nz, light, h1, h2, h4, h8 = st.tolist()
+    tot, mx, nz, light, h1, h2, h4, h8, amax = st.tolist()[:9]
     assert tot == int(ref.sum()) and mx == (int(ref.max()) if m else 0)
+    assert amax == (int((A.rowptr[1:] - A.rowptr[:-1]).max()) if m else 0)
     assert nz == int((ref > 0).sum()) and light == int(((ref > 0) & (ref <= SG.ESC_MIN)).sum())
     hist = torch.bincount(nsl.cpu(), minlength=9).tolist()
     assert [h1, h2, h4, h8] == [hist[1], hist[2], hist[4], hist[8]]
@@ -528,3 +529,115 @@ def test_spgemm_row_splits_match_searchsorted(n, d):
         lo, hi = int(rp[j]), int(rp[j + 1])
         ref = lo + torch.searchsorted(col[lo:hi].contiguous(), bounds)
         assert torch.equal(sp[j], ref.to(torch.int64)), j
+
+
+def _bitmap_vs_binned(monkeypatch, A, B, cfg):
+    from spmm_amd.utils.config import CONFIG
+
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap", "on")
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_cfg", cfg)
+    i1 = SG.SpgemmInfo()
+    C1 = SG.spgemm(A, B, i1)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap", "off")
+    C2 = SG.spgemm(A, B)
+    assert torch.equal(C1.rowptr, C2.rowptr)
+    assert torch.equal(C1.col, C2.col)
+    assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    assert C1.is_sorted()
+    return i1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,m,k,n,da,db", [(0, 2000, 20000, 300000, 0.002, 2.7e-4),
+                                             (1, 3000, 10000, 65536, 0.006, 0.001),
+                                             (2, 2500, 9000, 200001, 0.006, 5e-4), (1, 700, 3000, 1000, 0.01, 0.01),
+                                             (0, 500, 400, 50, 0.2, 0.2)])
+def test_spgemm_gpu_bitmap_matches_binned(monkeypatch, cfg, m, k, n, da, db):
+    """Bitmap-rank path (count kernel -> unit offsets -> numeric kernel) equals
+    the binned path bit for bit in structure, for every window configuration,
+    ragged last windows (n not a multiple of the window) and n below one
+    window."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, k, da, seed=91, device=dev)
+    B = gen_csr.uniform_csr(k, n, db, seed=92, device=dev)
+    info = _bitmap_vs_binned(monkeypatch, A, B, cfg)
+    assert info.rows_per_bin_num["bitmap_cfg"] == cfg and "bitmap_fallback" not in info.rows_per_bin_num
+
+
+@pytest.mark.gpu
+def test_spgemm_gpu_bitmap_deferred_units_and_fallback(monkeypatch):
+    """Rows too long for the fast kernel (A rows > 256 entries, windows above
+    its product capacity) are deferred to the reload kernel; a unit beyond the
+    reload budget (> 12288 products in one window) sends the whole product to
+    the binned path; empty rows give empty units."""
+    dev = torch.device("cuda")
+    k, n = 6000, 300000
+    base = gen_csr.uniform_csr(1500, k, 0.01, seed=93)
+    rows = [base.row_ids(), torch.full((400,), 3), torch.full((300,), 1000)]
+    cols = [base.col.long(), torch.randperm(k)[:400], torch.randperm(k)[:300]]
+    keep = (rows[0] != 3) & (rows[0] != 1000) & (rows[0] != 7)   # row 7 empty
+    A = CS.from_coo(torch.cat([rows[0][keep]] + rows[1:]), torch.cat([cols[0][keep]] + cols[1:]),
+                    torch.rand(int(keep.sum()) + 700) - 0.5, 1500, k).to(dev)
+    B = gen_csr.uniform_csr(k, n, 2e-4, seed=94, device=dev)
+    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    assert info.rows_per_bin_num["bitmap_deferred"] >= 6   # rows 3 and 1000 (> 256 entries) in their 3 windows
+    # one window crowded beyond the reload capacity -> binned fallback
+    Bc = gen_csr.uniform_csr(k, 1 << 17, 0.03, seed=95)
+    Bc = CS.CSR(k, n, Bc.rowptr, Bc.col, Bc.val).to(dev)   # every column in window 0 of cfg 0
+    Ac = CS.from_coo(torch.full((900,), 5), torch.randperm(k)[:900], torch.rand(900), 64, k).to(dev)
+    info = _bitmap_vs_binned(monkeypatch, Ac, Bc, 0)
+    assert info.rows_per_bin_num.get("bitmap_fallback") is None   # info reset by the fallback
+    assert "bitmap_units" not in info.rows_per_bin_num
+
+
+def sampled_rows_check(A, B, C, nrows: int, seed: int = 0) -> float:
+    """Gustavson in fp64 on the CPU for ``nrows`` random rows of C = A.B:
+    asserts the exact column structure of each row, returns the max relative
+    value error (|got - ref| / (|ref| + 1e-6))."""
+    g = torch.Generator().manual_seed(seed)
+    rows = torch.randint(0, A.m, (nrows,), generator=g).unique()
+    Arp, Aci, Av = A.rowptr.cpu(), A.col.cpu().long(), A.val.cpu().double()
+    Brp, Bci, Bv = B.rowptr.cpu(), B.col.cpu().long(), B.val.cpu().double()
+    Crp = C.rowptr.cpu()
+    worst = 0.0
+    for i in rows.tolist():
+        s, e = int(Arp[i]), int(Arp[i + 1])
+        js, avs = Aci[s:e], Av[s:e]
+        lens = Brp[js + 1] - Brp[js]
+        idx = torch.repeat_interleave(Brp[js], lens) + (torch.arange(int(lens.sum())) -
+                                                         torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens))
+        cols, prods = Bci[idx], Bv[idx] * torch.repeat_interleave(avs, lens)
+        uc, inv = torch.unique(cols, return_inverse=True)
+        ref = torch.zeros(uc.numel(), dtype=torch.float64).index_add_(0, inv, prods)
+        cs, ce = int(Crp[i]), int(Crp[i + 1])
+        got_c = C.col[cs:ce].cpu().long()
+        got_v = C.val[cs:ce].cpu().double()
+        assert torch.equal(got_c, uc), f"row {i}: column structure differs"
+        if uc.numel():
+            worst = max(worst, float(((got_v - ref).abs() / (ref.abs() + 1e-6)).max()))
+    return worst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,ordered", [(65536, 1e-3, False), (65536, 1e-3, True), (1 << 20, 1e-4, False)])
+def test_spgemm_bench_scale_sampled_rows(monkeypatch, n, d, ordered):
+    """BASELINE configs 2 and 4 at full size, on the path the bench takes
+    (bitmap-rank; ordered one-pass with ``ordered``): 4096 random rows against
+    fp64 Gustavson on the CPU (structure exact, values to fp32 accumulation
+    error), and the total nnz against the two-phase symbolic count."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(n, n, d, seed=1, device=dev)
+    B = gen_csr.uniform_csr(n, n, d, seed=2, device=dev)
+    if ordered:
+        monkeypatch.setattr(CONFIG, "spgemm_bitmap", "off")
+        monkeypatch.setattr(CONFIG, "spgemm_ordered", "on")
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, B, info)
+    assert ("ordered_units" if ordered else "bitmap_units") in info.rows_per_bin_num
+    assert C.rowptr[-1] == C.nnz == info.nnz
+    err = sampled_rows_check(A, B, C, 4096)
+    assert err < 1e-4, err
+    row_nnz = SG.symbolic(A, B, SG.row_nprod(A, B), SG.SpgemmInfo())
+    assert torch.equal((C.rowptr[1:] - C.rowptr[:-1]).to(torch.int32), row_nnz)
