@@ -52,19 +52,21 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("native build failed: " + " ".join(cmd[:4]) + " ...")
 
 
-def build_hip(force: bool = False, verbose: bool = False) -> str:
+def build_hip(force: bool = False, verbose: bool = False, out: str = HIP_LIB, extra=()) -> str:
+    """``out`` / ``extra``: a diagnostic variant (e.g. ``-DSPMM_BM_STAMPS``)
+    built next to the real library; load it with ``SPMM_HIP_LIB=<path>``."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.hpp"))
-    if force or _stale(HIP_LIB, deps):
-        os.makedirs(LIB_DIR, exist_ok=True)
-        tmp = HIP_LIB + ".tmp"
+    if force or _stale(out, deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        tmp = out + ".tmp"
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-fvisibility=hidden", "-munsafe-fp-atomics", "-o", tmp] + srcs
+               "-fvisibility=hidden", "-munsafe-fp-atomics", *extra, "-o", tmp] + srcs
         if verbose:
             print(" ".join(cmd))
         _run(cmd)
-        os.replace(tmp, HIP_LIB)
-    return HIP_LIB
+        os.replace(tmp, out)
+    return out
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:

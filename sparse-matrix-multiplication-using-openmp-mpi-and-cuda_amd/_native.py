@@ -89,9 +89,12 @@ def hip():
             if _hip is None:
                 import torch  # noqa: F401  (bind to torch's HIP runtime first)
 
-                if not os.path.exists(_build.HIP_LIB) or os.environ.get("SPMM_REBUILD"):
-                    _build_locked("hip")
-                lib = C.CDLL(_build.HIP_LIB)
+                path = os.environ.get("SPMM_HIP_LIB")   # a diagnostic build (tools/bm_stamps.py)
+                if not path:
+                    if not os.path.exists(_build.HIP_LIB) or os.environ.get("SPMM_REBUILD"):
+                        _build_locked("hip")
+                    path = _build.HIP_LIB
+                lib = C.CDLL(path)
                 _sig(lib, "spmm_bsr_u64_numeric", C.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int,
                      C.c_int64, c_vp)
                 _sig(lib, "spmm_bsr_u64_nonzero", C.c_int, c_vp, C.c_int, C.c_int64, c_vp, c_vp)

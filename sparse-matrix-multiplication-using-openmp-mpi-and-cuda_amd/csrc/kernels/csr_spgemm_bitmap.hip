@@ -67,6 +67,32 @@ __device__ __forceinline__ int bm_scan(int v, int* wsum, int* total) {
   return pre + x - v;
 }
 
+// Two block-wide exclusive scans with one barrier (wsum holds 2 * NW ints).
+template <int NT>
+__device__ __forceinline__ void bm_scan2(int a, int b, int* wsum, int& pa, int& pb, int& ta, int& tb) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int xa = bm_wave_incl(a), xb = bm_wave_incl(b);
+  if (lane == 63) {
+    wsum[w] = xa;
+    wsum[NW + w] = xb;
+  }
+  __syncthreads();
+  int qa = 0, qb = 0;
+  ta = 0;
+  tb = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int sa = wsum[i], sb = wsum[NW + i];
+    qa += (i < w) ? sa : 0;
+    qb += (i < w) ? sb : 0;
+    ta += sa;
+    tb += sb;
+  }
+  pa = qa + xa - a;
+  pb = qb + xb - b;
+}
+
 __device__ __forceinline__ int bm_wave_sum(int x) {
   return __builtin_amdgcn_readlane(bm_wave_incl(x), 63);
 }
@@ -76,6 +102,36 @@ __device__ __forceinline__ int64_t bm_rfl64(int64_t x) {
   const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+
+// Diagnostic phase stamps, compiled in only with -DSPMM_BM_STAMPS (the
+// accumulators cost registers): thread 0 of every workgroup adds the
+// shader-clock cycles of each phase of a unit, measured between the barriers
+// that delimit it, in registers, flushed once at the end; [7] counts units.
+__device__ int g_bm_stamp_on = 0;
+__device__ unsigned long long g_bm_stamps[8];
+#ifdef SPMM_BM_STAMPS
+#define BM_STAMP_DECL                                                              \
+  const int stamp_on = g_bm_stamp_on;                                              \
+  unsigned long long t_prev = stamp_on ? __builtin_amdgcn_s_memtime() : 0ull;      \
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define BM_STAMP(i)                                                                \
+  do {                                                                             \
+    if (stamp_on) {                                                                \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
+      st_acc[i] += _t - t_prev;                                                    \
+      t_prev = _t;                                                                 \
+    }                                                                              \
+  } while (0)
+#define BM_STAMP_UNIT() st_acc[7] += 1
+#define BM_STAMP_FLUSH()                                                           \
+  if (stamp_on && threadIdx.x == 0)                                                \
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_bm_stamps[i], st_acc[i])
+#else
+#define BM_STAMP_DECL
+#define BM_STAMP(i) do {} while (0)
+#define BM_STAMP_UNIT() do {} while (0)
+#define BM_STAMP_FLUSH() do {} while (0)
+#endif
 
 // One instantiation's geometry.  MODE 0: count (NSUB windows per unit);
 // 1: numeric, products held in R register rounds; 2: numeric reload
@@ -111,6 +167,7 @@ struct BmArgs {
   int32_t* ovf;            // numeric: deferred units
   uint32_t* novf;          //          and their count
   int64_t ovf_cap;
+  int64_t cap;             // numeric: entries allocated for C (a unit outside it is an error, never a write)
   int32_t* err;            // bit 0: a deferred unit exceeds the reload budget (host falls back)
                            // bit 1: count / numeric disagree (kernel invariant)
                            // bit 2: deferred list full (host falls back)
@@ -132,7 +189,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned long long items[VALUES ? PCAP : 1];
   using Desc = typename std::conditional<VALUES, uint4, uint2>::type;
   __shared__ __attribute__((aligned(16))) Desc desc[CCAP];
-  __shared__ int wsum[NW];
+  __shared__ int wsum[2 * NW];
   __shared__ int scnt[NSUB];
   __shared__ int sdup;
 
@@ -152,6 +209,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   // first LDS read after them for a full memory latency.
   int vz;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  BM_STAMP_DECL
 
   // bitmap clear: 16-byte stores, consecutive lanes on consecutive slots (conflict-free)
   auto clear_bm = [&]() {
@@ -172,103 +230,120 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   const int64_t NG = gridDim.x;
   const int64_t me = (MODE != 2 && NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8
                                                 : (int64_t)blockIdx.x;
-  // (row, window) of consecutive slots by carries, not divisions
-  const int64_t step_row = NG / nsw;
-  const int step_q = (int)(NG - step_row * nsw);
 
   // ---- software pipeline over this workgroup's units ----------------------
-  // Unit k+2: row pointer loads (s1) at the top of unit k.  Unit k+1: its A
-  // entries and output offsets (s2) at the top of unit k, its window bounds
-  // (s3) after unit k's first B pass.  So unit k+1's staging finds every
-  // input in registers; each link of the Arp -> Aci -> ws chain has a whole
-  // phase to land.
-  struct Head {   // wave-uniform identity of a unit
-    int64_t slot, u, row;
-    int qi;       // unit index inside its row
+  // Three units ahead, every load issued unconditionally at the top of an
+  // iteration (one control path, so no conservative waits): at the top of
+  // unit k, the window bounds and output offsets of unit k+1 (needs k+1's A
+  // columns, loaded one iteration earlier), the A entries of unit k+2 (needs
+  // its row pointers, one iteration earlier) and the row pointers of unit
+  // k+3.  Unit k's staging then finds its inputs in registers.
+  struct Head {   // wave-uniform identity of a unit (m * nwin < 2^31, checked by the host)
+    int slot, u, row, qi;   // qi: unit index inside its row
   };
   auto first_head = [&](int64_t slot) {
-    Head h{slot, 0, 0, 0};
+    Head h{(int)(slot < nunits ? slot : nunits), 0, 0, 0};
     if (slot < nunits) {
-      h.u = MODE == 2 ? (int64_t)p.ovf[slot] : slot;
-      h.row = h.u / nsw;
-      h.qi = (int)(h.u - h.row * nsw);
+      h.u = MODE == 2 ? p.ovf[slot] : (int)slot;
+      h.row = (int)(h.u / nsw);
+      h.qi = (int)(h.u - (int64_t)h.row * nsw);
     }
     return h;
   };
+  const int step_q = (int)(NG % nsw), step_row = (int)(NG / nsw);
   auto next_head = [&](const Head& h) {
-    if constexpr (MODE == 2) return first_head(h.slot + NG);
-    Head n{h.slot + NG, h.u + NG, h.row + step_row, h.qi + step_q};
-    if (n.qi >= nsw) {
-      n.qi -= (int)nsw;
-      ++n.row;
+    if constexpr (MODE == 2) {
+      return first_head((int64_t)h.slot + NG);
+    } else {
+      Head n{h.slot, h.u, h.row, h.qi};
+      if ((int64_t)h.slot + NG >= nunits) {
+        n.slot = (int)nunits;
+        return n;
+      }
+      n.slot = (int)(h.slot + NG);
+      n.u = (int)(h.u + NG);
+      n.row = h.row + step_row;
+      n.qi = h.qi + step_q;
+      if (n.qi >= nsw) {
+        n.qi -= (int)nsw;
+        ++n.row;
+      }
+      return n;
     }
-    return n;
   };
-  Head h1 = first_head(me);
-  Head h2 = next_head(h1);   // units k+1 and k+2
+  auto live = [&](const Head& h) { return (int64_t)h.slot < nunits; };
   auto q0_of = [&](const Head& h) { return h.qi * (MODE == 0 ? NSUB : 1); };
   auto q1_of = [&](const Head& h) { return MODE == 0 ? min(h.qi * NSUB + NSUB, nwin) : h.qi + 1; };
-  int64_t r1a = 0, r1b = 0, r2a = 0, r2b = 0;   // Arp[row], Arp[row + 1] (vector registers)
-  int64_t o1a = 0, o1b = 0;                     // uoff[u], uoff[u + 1] of unit k+1
-  int j1 = 0;
-  float av1 = 0.f;
-  uint32_t b01 = 0, b11 = 0;
-  auto s1 = [&](const Head& h, int64_t& ra, int64_t& rb) {
-    if (h.slot < nunits) {
-      ra = p.Arp[h.row + vz];
-      rb = p.Arp[h.row + 1 + vz];
+  Head h0 = first_head(me);
+  Head h1 = next_head(h0), h2 = next_head(h1), h3 = next_head(h2);
+  // row start / length of A (vector registers; nnz(A) < 2^31, checked by the host)
+  int ra0 = 0, rb0 = 0, ra1 = 0, rb1 = 0, ra2 = 0, rb2 = 0, ra3 = 0, rb3 = 0;
+  int jj1 = 0, jj2 = 0;                   // A columns of units k+1 (landed) and k+2 (in flight)
+  float av0 = 0.f, av1 = 0.f, av2 = 0.f;  // A values of units k, k+1, k+2
+  uint32_t b00 = 0, b10 = 0, b01 = 0, b11 = 0;   // window bounds of units k and k+1
+  int64_t oa0 = 0, oa1 = 0;   // uoff of units k and k+1, and the low words of the next entry
+  int ob0 = 0, ob1 = 0;
+  auto ld_arp = [&](const Head& h, int& ra, int& rb) {
+    if (live(h)) {
+      ra = (int)p.Arp[h.row + vz];
+      rb = (int)p.Arp[h.row + 1 + vz];
     }
   };
-  auto s2 = [&]() {
-    if (h1.slot < nunits) {
-      const int64_t a0 = bm_rfl64(r1a), na = bm_rfl64(r1b) - a0;
+  auto ld_entries = [&](const Head& h, int ra, int rb, int& j, float& av) {
+    if (live(h)) {
+      const int a0 = __builtin_amdgcn_readfirstlane(ra), na = __builtin_amdgcn_readfirstlane(rb) - a0;
       if (tid < na) {
-        j1 = p.Aci[a0 + tid];
-        if constexpr (VALUES) av1 = p.Av[a0 + tid];
+        j = p.Aci[a0 + tid];
+        if constexpr (VALUES) av = p.Av[a0 + tid];
+      }
+    }
+  };
+  auto ld_bounds = [&](const Head& h, int ra, int rb, int j, uint32_t& b0, uint32_t& b1, int64_t& oa, int& ob) {
+    if (live(h)) {
+      const int na = __builtin_amdgcn_readfirstlane(rb) - __builtin_amdgcn_readfirstlane(ra);
+      if (tid < na) {
+        const uint32_t* wr = p.ws + (int64_t)j * nw1;
+        b0 = wr[q0_of(h)];
+        b1 = wr[q1_of(h)];
       }
       if constexpr (VALUES) {
-        o1a = p.uoff[h1.u + vz];
-        o1b = p.uoff[h1.u + 1 + vz];
+        oa = p.uoff[h.u + vz];
+        ob = (int)p.uoff[h.u + 1 + vz];   // low word: the unit's count is (ob - oa) mod 2^32
       }
     }
   };
-  auto s3 = [&]() {
-    if (h1.slot < nunits) {
-      const int64_t a0 = bm_rfl64(r1a), na = bm_rfl64(r1b) - a0;
-      if (tid < na) {
-        const uint32_t* wr = p.ws + (int64_t)j1 * nw1;
-        b01 = wr[q0_of(h1)];
-        b11 = wr[q1_of(h1)];
-      }
-    }
-  };
-  s1(h1, r1a, r1b);
-  s1(h2, r2a, r2b);
-  s2();
-  s3();
+  // prologue: units 0, 1, 2 staged to the depth the loop expects
+  ld_arp(h0, ra0, rb0);
+  ld_arp(h1, ra1, rb1);
+  ld_arp(h2, ra2, rb2);
+  ld_entries(h0, ra0, rb0, jj1, av0);
+  ld_bounds(h0, ra0, rb0, jj1, b00, b10, oa0, ob0);
+  ld_entries(h1, ra1, rb1, jj1, av1);
+  ld_entries(h2, ra2, rb2, jj2, av2);
+  ld_arp(h3, ra3, rb3);
   __syncthreads();
 
-  // Products of chunk rounds [i0, i0 + RR) of this lane group: one 16-byte
-  // descriptor read (a broadcast inside the group) and the B loads of the
-  // rounds that exist (wave-uniform guards), every load before any use.
+  // Products of chunk rounds [i0, i0 + RR) of this lane group: descriptor
+  // reads for every round (LDS broadcasts, clamped index: all in flight
+  // together), B loads only for rounds that exist (wave-uniform guards),
+  // every load before any use.
   int c[RR];
   float v[RR];
   auto fetch = [&](int i0, int nr, int TC, int clo) {
+    Desc ds[RR];
+#pragma unroll
+    for (int d = 0; d < RR; ++d) {
+      const int t = gid + (i0 + d) * ngrp;
+      ds[d] = desc[t < TC ? t : TC - 1];
+    }
     uint32_t f[RR];
-    float a[RR];
     uint32_t okm = 0;
 #pragma unroll
     for (int d = 0; d < RR; ++d) {
-      f[d] = 0;
-      a[d] = 0.f;
-      if (i0 + d < nr) {   // wave-uniform
-        const int t = gid + (i0 + d) * ngrp;
-        const Desc ds = desc[t < TC ? t : TC - 1];
-        const bool ok = (t < TC) & ((uint32_t)gl < ds.y);
-        okm |= (ok ? 1u : 0u) << d;
-        f[d] = ds.x + (ok ? (uint32_t)gl : 0u);
-        if constexpr (VALUES) a[d] = __uint_as_float(reinterpret_cast<const uint4&>(ds).z);
-      }
+      const int t = gid + (i0 + d) * ngrp;
+      const bool ok = (t < TC) & ((uint32_t)gl < ds[d].y);
+      okm |= (ok ? 1u : 0u) << d;
+      f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
     }
     int x[RR];
     float b[RR];
@@ -284,7 +359,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 #pragma unroll
     for (int d = 0; d < RR; ++d) {
       c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
-      if constexpr (VALUES) v[d] = a[d] * b[d];
+      if constexpr (VALUES) v[d] = __uint_as_float(reinterpret_cast<const uint4&>(ds[d]).z) * b[d];
     }
   };
   // OR the columns into the bitmap.  Numeric mode keeps the old words: a
@@ -309,19 +384,31 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
     return dupm;
   };
 
-  while (h1.slot < nunits) {
-    // ---- take unit k from the pipeline registers; start k+1 / k+2 loads ----
-    const Head h = h1;
-    const int64_t a0 = bm_rfl64(r1a), na = bm_rfl64(r1b) - a0;
-    const int64_t off = bm_rfl64(o1a), want = bm_rfl64(o1b) - off;
-    const float av0 = av1;
-    const uint32_t b00 = b01, b10 = b11;
-    h1 = h2;
-    r1a = r2a;
-    r1b = r2b;
-    h2 = next_head(h2);
-    s1(h2, r2a, r2b);
-    s2();
+  while (live(h0)) {
+    // ---- unit k = h0: inputs in registers; issue the loads of k+1..k+3 ----
+    const Head h = h0;
+    const int64_t a0 = __builtin_amdgcn_readfirstlane(ra0);
+    const int64_t na = __builtin_amdgcn_readfirstlane(rb0) - (int)a0;
+    const int64_t off = bm_rfl64(oa0);
+    const int want = __builtin_amdgcn_readfirstlane(ob0) - (int)(uint32_t)off;
+    const float avk = av0;
+    const uint32_t bk0 = b00, bk1 = b10;
+    {
+      const Head h4 = next_head(h3);
+      int ra4 = 0, rb4 = 0;
+      int jj3 = 0;
+      float av3 = 0.f;
+      ld_bounds(h1, ra1, rb1, jj1, b01, b11, oa1, ob1);
+      ld_entries(h3, ra3, rb3, jj3, av3);
+      ld_arp(h4, ra4, rb4);
+      // rotate the pipeline registers
+      h0 = h1; h1 = h2; h2 = h3; h3 = h4;
+      ra0 = ra1; rb0 = rb1; ra1 = ra2; rb1 = rb2; ra2 = ra3; rb2 = rb3; ra3 = ra4; rb3 = rb4;
+      av0 = av1; av1 = av2; av2 = av3;
+      jj1 = jj2; jj2 = jj3;
+      b00 = b01; b10 = b11;
+      oa0 = oa1; ob0 = ob1;
+    }
     const int64_t row = h.row;
     const int q0 = q0_of(h), q1 = q1_of(h);
     const int clo = q0 << LGW;
@@ -335,8 +422,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         uint32_t b0 = 0;
         if (tid < nb) {
           if (bat == 0) {   // from the pipeline registers
-            b0 = b00;
-            len = (int)(b10 - b00);
+            b0 = bk0;
+            len = (int)(bk1 - bk0);
           } else {
             const uint32_t* wr = p.ws + (int64_t)p.Aci[a0 + bat + tid] * nw1;
             b0 = wr[q0];
@@ -344,10 +431,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
           }
           nch = (len + Gl - 1) >> lg;
         }
-        int TCall, Pb;
-        const int pre = bm_scan<NT>(nch, wsum, &TCall);
-        __syncthreads();
-        bm_scan<NT>(len, wsum, &Pb);
+        int pre, plen, TCall, Pb;
+        bm_scan2<NT>(nch, len, wsum, pre, plen, TCall, Pb);
         P += Pb;
         for (int cb = 0; cb < TCall; cb += CCAP) {
           const int TC = TCall - cb < CCAP ? TCall - cb : CCAP;
@@ -368,7 +453,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
           __syncthreads();   // descriptors consumed before they are rewritten
         }
       }
-      s3();
+      BM_STAMP(5);
       if (P == 0) {   // uniform
         if (tid < q1 - q0) p.ucnt[row * nwin + q0 + tid] = 0;
         continue;
@@ -387,64 +472,56 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       }
       clear_bm();
       __syncthreads();   // cleared before the next unit's ORs
+      BM_STAMP(6);
     } else {
       // ---- numeric staging: the whole row in one batch, from registers -----
       int len = 0, nch = 0;
       if (tid < na && tid < NT) {
-        len = (int)(b10 - b00);
+        len = (int)(bk1 - bk0);
         nch = (len + Gl - 1) >> lg;
       }
-      // one scan of (products, chunks): len < 2^16 is checked below through P
-      const bool big = len >= 65536;
-      int both;
-      const int pk = bm_scan<NT>(big ? 0 : ((len << 16) | nch), wsum, &both);
-      const int pre = pk & 0xffff;
-      const int TC = both & 0xffff;
-      const int P = (int)((uint32_t)both >> 16);
-      const bool any_big = __syncthreads_or(big);
-      if (P == 0 && !any_big) {   // uniform; the count kernel wrote 0 for this unit
-        s3();
-        continue;
-      }
-      const bool too_big = any_big || na > NT || P > PCAP || TC > CCAP || (MODE == 1 && TC > R * ngrp);
+      int pre, plen, TC, P;
+      bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+      if (P == 0) continue;   // uniform; the count kernel wrote 0 for this unit
+      const bool too_big = na > NT || P > PCAP || TC > CCAP || (MODE == 1 && TC > R * ngrp);
       if (too_big) {   // uniform
         if (tid == 0) {
           if (MODE == 1) {
             const uint32_t at = atomicAdd(p.novf, 1u);
-            if ((int64_t)at < p.ovf_cap) p.ovf[at] = (int32_t)h.u;
+            if ((int64_t)at < p.ovf_cap) p.ovf[at] = h.u;
             else atomicOr(p.err, 4);
           } else {
             atomicOr(p.err, 1);
           }
         }
-        s3();
+        __syncthreads();   // wsum reads done before the next unit's scan
         continue;
       }
       for (int kk = 0; kk < nch; ++kk) {
         const int rem = len - (kk << lg);
         Desc dd{};
-        dd.x = b00 + ((uint32_t)kk << lg);
+        dd.x = bk0 + ((uint32_t)kk << lg);
         dd.y = (uint32_t)(rem < Gl ? rem : Gl);
-        reinterpret_cast<uint4&>(dd).z = __float_as_uint(av0);
+        reinterpret_cast<uint4&>(dd).z = __float_as_uint(avk);
         desc[pre + kk] = dd;
       }
       __syncthreads();
+      BM_STAMP(0);
       // ---- pass 1: products into registers, columns into the bitmap -------
       const int nr = (TC + ngrp - 1) / ngrp;
       uint32_t dupm = 0;
       if constexpr (MODE == 1) {
         fetch(0, nr, TC, clo);
-        s3();
         dupm = or_all();
       } else {
         for (int i0 = 0; i0 < nr; i0 += RR) {
           fetch(i0, nr, TC, clo);
           or_all();
         }
-        s3();
       }
       if (dupm) sdup = 1;
       __syncthreads();
+      BM_STAMP(1);
       // ---- rank prefix per 64-bit word: wave w owns words [w*WPW, (w+1)*WPW)
       int run[WPT];
       int wtot = 0;
@@ -469,6 +546,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
       if (tid == 0) sdup = 0;
       __syncthreads();
+      BM_STAMP(2);
       // ---- pass 2: rank -> slot; owners store (column, value), duplicates
       // add their value after a barrier (bit set by an earlier product)
       auto rank = [&](int cc) {
@@ -512,11 +590,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         }
       }
       __syncthreads();
+      BM_STAMP(3);
       // ---- the unit's slots to C at its final offset; clear the bitmap -----
       int lim = total;
-      if (want != total) {   // count and numeric disagree: never write outside the unit
+      if (want != total || off < 0 || off + total > p.cap) {   // never write outside the unit or C
         if (tid == 0) atomicOr(p.err, 2);
-        lim = total < want ? total : (int)want;
+        lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : (int)want);
       }
       for (int i = tid; i < lim; i += NT) {
         const unsigned long long it = items[i];
@@ -525,8 +604,321 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       }
       clear_bm();
       __syncthreads();   // cleared (and items read) before the next unit's pass 1
+      BM_STAMP(4);
+      BM_STAMP_UNIT();
     }
   }
+  BM_STAMP_FLUSH();
+}
+
+// ---- row-major numeric kernel (nwin <= 8) ---------------------------------
+// A workgroup takes whole rows (row k*gridDim + perm(g)) and runs their
+// windows back to back, so the A row and all its window bounds are loaded
+// ONCE per row, one row ahead: the A entries of row k+1 and the row pointers
+// of row k+2 before row k's first B pass, the packed bounds and output
+// offsets of row k+1 before row k's last B pass.  They are copied into the
+// current-row registers right after that last pass has waited for its B
+// loads, when every one of them has landed (a copy of a register whose load
+// is still in flight would stall the wave for the whole memory latency).
+// Per window the staging is register arithmetic + one scan.
+// ws8[j] = {first index of B row j, 16-bit lengths of windows 0..7} (uint4 x 2).
+struct BmRowArgs {
+  BmArgs a;
+  const uint4* ws8;
+};
+
+template <int LGW, int NT, int PCAP, int R, int CCAP>
+__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
+  const BmArgs& p = ra.a;
+  constexpr int NW = NT / 64;
+  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  constexpr int RR = R;
+  static_assert(WPW % 64 == 0 && PCAP < 65536, "geometry");
+
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
+  __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
+  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];   // chunk: {first B index, valid lanes}
+  __shared__ float dval[CCAP];                                 //        a(i, j)
+  __shared__ int wsum[2 * NW];
+  __shared__ int sdup;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = p.lg;
+  const int Gl = 1 << lg;
+  const int ngrp = NW << (6 - lg);
+  const int gid = (w << (6 - lg)) + (lane >> lg);
+  const int gl = lane & (Gl - 1);
+  const int nwin = p.nwin;
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  BM_STAMP_DECL
+
+  auto clear_bm = [&]() {
+    for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+  };
+  clear_bm();
+  if (tid == 0) sdup = 0;
+
+  const int64_t NG = gridDim.x;
+  const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+  const int64_t m = p.m;
+
+  // row pipeline registers
+  int64_t row = me;               // current row
+  int ca0 = 0, cna = 0;           // its A row (scalars after the copy)
+  float cav = 0.f;                // its A value (thread = entry)
+  uint4 cwa = make_uint4(0, 0, 0, 0);   // its packed window bounds
+  uint32_t cwb = 0;
+  int64_t cuo = 0;                // lane q: uoff[row * nwin + q], q <= nwin
+  int n1a = 0, n1b = 0;           // Arp of row + NG (vector, landed one row early)
+  int n2a = 0, n2b = 0;           // Arp of row + 2 NG (in flight)
+  int njj = 0;                    // A columns of row + NG
+  float nav = 0.f;
+  uint4 nwa = make_uint4(0, 0, 0, 0);
+  uint32_t nwb = 0;
+  int64_t nuo = 0;
+
+  auto ld_arp = [&](int64_t r, int& a, int& b) {
+    if (r < m) {
+      a = (int)p.Arp[r + vz];
+      b = (int)p.Arp[r + 1 + vz];
+    }
+  };
+  auto ld_entries = [&](int64_t r, int a, int b) {   // A entries of row r into njj / nav
+    if (r < m) {
+      const int a0 = __builtin_amdgcn_readfirstlane(a), na = __builtin_amdgcn_readfirstlane(b) - a0;
+      if (tid < na) {
+        njj = p.Aci[a0 + tid];
+        nav = p.Av[a0 + tid];
+      }
+    }
+  };
+  auto ld_bounds = [&](int64_t r, int a, int b) {    // packed bounds + offsets of row r
+    if (r < m) {
+      const int na = __builtin_amdgcn_readfirstlane(b) - __builtin_amdgcn_readfirstlane(a);
+      if (tid < na) {
+        nwa = ra.ws8[2 * (int64_t)njj];
+        nwb = ra.ws8[2 * (int64_t)njj + 1].x;
+      }
+      if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
+    }
+  };
+  auto take_next = [&]() {   // next row -> current row (call only when its loads have landed)
+    ca0 = __builtin_amdgcn_readfirstlane(n1a);
+    cna = __builtin_amdgcn_readfirstlane(n1b) - ca0;
+    cav = nav;
+    cwa = nwa;
+    cwb = nwb;
+    cuo = nuo;
+    n1a = n2a;
+    n1b = n2b;
+  };
+  // prologue: row me in the current registers, Arp of row me + NG loaded
+  ld_arp(row, n1a, n1b);
+  ld_entries(row, n1a, n1b);
+  ld_bounds(row, n1a, n1b);
+  ld_arp(row + NG, n2a, n2b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  take_next();
+  __syncthreads();
+
+  int c[RR];
+  float v[RR];
+  for (; row < m; row += NG) {
+    const int na = cna;
+    uint32_t bq = cwa.x;   // first B index of window q of this thread's entry
+    for (int q = 0; q < nwin; ++q) {
+      const bool last = q == nwin - 1;
+      // ---- pipeline hooks (every path) ---------------------------------
+      if (q == 0) {
+        ld_entries(row + NG, n1a, n1b);
+        ld_arp(row + 2 * NG, n2a, n2b);
+      }
+      if (last) ld_bounds(row + NG, n1a, n1b);
+      // ---- staging from registers ---------------------------------------
+      const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
+      int len = 0, nch = 0;
+      if (tid < na && tid < NT) {
+        len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
+        nch = (len + Gl - 1) >> lg;
+      }
+      const uint32_t b0 = bq;
+      bq += (uint32_t)len;
+      const int clo = q << LGW;
+      const int u = (int)(row * nwin + q);
+      // (both halves zero-extended: offsets pass 2^31 on the 1M product)
+      const int64_t off =
+          (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)cuo >> 32), q) << 32) |
+                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cuo, q));
+      const int want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
+      int pre, plen, TC, P;
+      bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+      const bool too_big = na > NT || P > PCAP || TC > CCAP || TC > R * ngrp;
+      if (P == 0 || too_big) {   // uniform
+        if (too_big && P != 0 && tid == 0) {
+          const uint32_t at = atomicAdd(p.novf, 1u);
+          if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
+          else atomicOr(p.err, 4);
+        }
+        if (last) take_next();   // (rare: waits for the next row's loads here)
+        __syncthreads();         // wsum reads done before the next scan
+        continue;
+      }
+      for (int kk = 0; kk < nch; ++kk) {
+        const int rem = len - (kk << lg);
+        desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
+        dval[pre + kk] = cav;
+      }
+      __syncthreads();
+      BM_STAMP(0);
+      // ---- pass 1 ----------------------------------------------------------
+      const int nr = (TC + ngrp - 1) / ngrp;
+      {
+        uint2 ds[RR];
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          const int t = gid + d * ngrp;
+          ds[d] = desc[t < TC ? t : TC - 1];
+        }
+        uint32_t f[RR];
+        uint32_t okm = 0;
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          const int t = gid + d * ngrp;
+          const bool ok = (t < TC) & ((uint32_t)gl < ds[d].y);
+          okm |= (ok ? 1u : 0u) << d;
+          f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
+        }
+        int x[RR];
+        float b[RR];
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          x[d] = 0;
+          b[d] = 0.f;
+          if (d < nr) {   // wave-uniform
+            x[d] = p.Bci[f[d]];
+            b[d] = p.Bv[f[d]];
+          }
+        }
+        // A values while the B loads are in flight
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          const int t = gid + d * ngrp;
+          v[d] = dval[t < TC ? t : TC - 1];
+        }
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
+          v[d] *= b[d];
+        }
+      }
+      uint32_t dupm = 0;
+      {
+        uint32_t old[RR];
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          old[d] = 0u;
+          if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
+        }
+#pragma unroll
+        for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
+      }
+      // this unit's B loads have landed, and with them every older load:
+      // the next row's registers are ready to be taken
+      if (last) take_next();
+      if (dupm) sdup = 1;
+      __syncthreads();
+      BM_STAMP(1);
+      // ---- rank prefix per 64-bit word ---------------------------------
+      int run[WPT];
+      int wtot = 0;
+#pragma unroll
+      for (int kk = 0; kk < WPT; ++kk) {
+        const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
+        const int incl = bm_wave_incl(cnt);
+        run[kk] = wtot + incl - cnt;
+        wtot += __builtin_amdgcn_readlane(incl, 63);
+      }
+      const int any_dup = sdup;
+      if (lane == 0) wsum[w] = wtot;
+      __syncthreads();
+      int base = 0, total = 0;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const int sw = wsum[i];
+        base += (i < w) ? sw : 0;
+        total += sw;
+      }
+#pragma unroll
+      for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
+      if (tid == 0) sdup = 0;
+      __syncthreads();
+      BM_STAMP(2);
+      // ---- pass 2 --------------------------------------------------------
+      auto rank = [&](int cc) {
+        const int wd = cc >> 6;
+        return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
+      };
+#pragma unroll
+      for (int d0 = 0; d0 < RR; d0 += 4) {
+        int r[4];
+#pragma unroll
+        for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
+#pragma unroll
+        for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) {
+          const int d = d0 + dd;
+          if (c[d] >= 0 && !((dupm >> d) & 1u))
+            items[r[dd]] = ((unsigned long long)__float_as_uint(v[d]) << 32) | (uint32_t)(c[d] + clo);
+        }
+      }
+      if (any_dup) {   // uniform
+        __syncthreads();
+#pragma unroll
+        for (int d = 0; d < RR; ++d)
+          if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+      }
+      __syncthreads();
+      BM_STAMP(3);
+      // ---- write-out -----------------------------------------------------
+      int lim = total;
+      if (want != total || off < 0 || off + total > p.cap) {   // never write outside the unit or C
+        if (tid == 0) atomicOr(p.err, 2);
+        lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : want);
+      }
+      for (int i = tid; i < lim; i += NT) {
+        const unsigned long long it = items[i];
+        p.Cci[off + i] = (int32_t)(uint32_t)it;
+        p.Cv[off + i] = __uint_as_float((uint32_t)(it >> 32));
+      }
+      clear_bm();
+      __syncthreads();
+      BM_STAMP(4);
+      BM_STAMP_UNIT();
+    }
+  }
+  BM_STAMP_FLUSH();
+}
+
+// ws8[j] from ws (nwin <= 8): first index + 16-bit window lengths; err bit 3
+// if a window segment of some B row is 65536 entries or longer.
+__global__ __launch_bounds__(256) void bm_pack_ws8(const uint32_t* __restrict__ ws, int64_t mb, int nwin,
+                                                   uint4* __restrict__ ws8, int32_t* __restrict__ err) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= mb) return;
+  const uint32_t* wr = ws + j * (nwin + 1);
+  uint32_t l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool bad = false;
+  for (int q = 0; q < nwin; ++q) {
+    const uint32_t d = wr[q + 1] - wr[q];
+    bad |= d > 0xffffu;
+    l[q] = d & 0xffffu;
+  }
+  if (bad) atomicOr(err, 8);
+  ws8[2 * j] = make_uint4(wr[0], l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16));
+  ws8[2 * j + 1] = make_uint4(l[6] | (l[7] << 16), 0u, 0u, 0u);
 }
 
 // ws[j * (nwin + 1) + q] = first index of B row j whose column >= q * 2^lgw
@@ -604,6 +996,28 @@ int bm_count(int64_t work, const BmArgs& a, hipStream_t s) {
   return launch_bm(BmKernels<C>::count, BmKernels<C>::kCountNT, work, a, s);
 }
 
+// row-major fast kernel of configuration C (same geometry as its fast kernel)
+template <int C>
+struct BmRowKernel {
+  static constexpr BmCfg K = kCfgs[C];
+  static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;   // (the pipeline registers cost 2 rounds)
+  static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
+};
+
+template <int C>
+int bm_numeric_rows(const BmRowArgs& ra, hipStream_t s) {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, BmRowKernel<C>::k, kFastNT, 0) != hipSuccess || per <= 0)
+    per = 1;
+  int64_t g = (int64_t)per * ncu;
+  if (ra.a.m < g) g = ra.a.m;
+  hipLaunchKernelGGL(BmRowKernel<C>::k, dim3((unsigned)g), dim3(kFastNT), 0, s, ra);
+  SPMM_LAUNCH_CHECK();
+  return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
+}
+
 template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, hipStream_t s) {
   const int rc = launch_bm(BmKernels<C>::fast, kFastNT, work, a, s);
@@ -643,7 +1057,7 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
                                      void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
-  BmArgs a{Arp, Aci, nullptr, ws, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+  BmArgs a{Arp, Aci, nullptr, ws, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0,
            err};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * ((nwin + kCfgs[cfg].nsub_count - 1) / kCfgs[cfg].nsub_count);
@@ -658,16 +1072,63 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
 // units it deferred (novf must be zero; ovf has room for ovf_cap units).
 SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                        const uint32_t* ws, const int32_t* Bci, const float* Bv, int64_t m, int nwin,
-                                       int lg, const int64_t* uoff, int32_t* Cci, float* Cv, int32_t* ovf,
-                                       uint32_t* novf, int64_t ovf_cap, int32_t* err, void* stream) {
+                                       int lg, const int64_t* uoff, int64_t cap, int32_t* Cci, float* Cv,
+                                       int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
-  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, err};
+  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, err};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * nwin;
   switch (cfg) {
     case 0: return bm_numeric<0>(work, a, s);
     case 1: return bm_numeric<1>(work, a, s);
     default: return bm_numeric<2>(work, a, s);
+  }
+}
+
+// Diagnostics: on >= 0 resets the stamp accumulators and enables (1) or
+// disables (0) them; on < 0 synchronises and reads the eight accumulators:
+// numeric [0] staging [1] pass 1 [2] rank scan [3] pass 2 [4] write-out,
+// count [5] staging + ORs [6] popcount + clear, [7] numeric units.
+SPMM_EXPORT int spmm_spgemm_bm_stamps(int on, unsigned long long* out8) {
+  if (on >= 0) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_bm_stamps), z, sizeof z);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_bm_stamp_on), &on, sizeof on);
+    return (int)e;
+  }
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_bm_stamps), 8 * sizeof(unsigned long long));
+  return (int)e;
+}
+
+// ws8 for the row-major numeric kernel (nwin <= 8); err bit 3: a window
+// segment too long for 16 bits (use spmm_spgemm_bm_numeric instead).
+SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin, void* ws8, int32_t* err,
+                                        void* stream) {
+  if (mb <= 0) return 0;
+  if (nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bm_pack_ws8, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, mb, nwin,
+                     (uint4*)ws8, err);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Row-major numeric (nwin <= 8, ws8 from spmm_spgemm_bm_pack_ws8), then the
+// reload kernel over the deferred units; same contract as spmm_spgemm_bm_numeric.
+SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                                            const void* ws8, const uint32_t* ws, const int32_t* Bci, const float* Bv,
+                                            int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap,
+                                            int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
+                                            int32_t* err, void* stream) {
+  if (m <= 0) return 0;
+  if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
+  BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, err},
+               (const uint4*)ws8};
+  hipStream_t s = (hipStream_t)stream;
+  switch (cfg) {
+    case 0: return bm_numeric_rows<0>(ra, s);
+    case 1: return bm_numeric_rows<1>(ra, s);
+    default: return bm_numeric_rows<2>(ra, s);
   }
 }

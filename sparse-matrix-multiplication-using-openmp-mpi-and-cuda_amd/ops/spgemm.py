@@ -53,10 +53,14 @@ _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_
                      C_INT, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_stamps", C_INT, c_vp)
+_native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
+                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
-                     c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
+                     C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -499,7 +503,7 @@ def _bitmap_ok(A: CSR, B: CSR, total_products: int, pre: dict) -> bool:
     kernel, row products not far above the mean (the windows are sized from
     the mean; a skewed matrix, e.g. R-MAT, takes the binned path)."""
     mode = CONFIG.spgemm_bitmap
-    if mode == "off" or total_products == 0 or B.nnz >= (1 << 31) or B.n >= (1 << 30):
+    if mode == "off" or total_products == 0 or B.nnz >= (1 << 31) or B.n >= (1 << 30) or A.nnz >= (1 << 31):
         return False
     nz = max(pre["nonempty"], 1)
     mean = total_products / nz
@@ -531,6 +535,8 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         cfg = 1
     lgw, nsub, pcap, rounds, _ = _bm_config(cfg)
     nwin = max(1, -(-B.n // (1 << lgw)))
+    if m * nwin >= (1 << 31):
+        return None
     if B_ready is not None:
         B = B_ready()
     lib = _native.hip()
@@ -547,19 +553,31 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     ucnt = torch.empty(nunits, dtype=torch.int32, device=dev)
     _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, lg_count, P(ucnt),
                                            P(err), st), "spgemm_bm_count")
+    ws8 = None
+    if nwin <= 8 and CONFIG.spgemm_bitmap_rows != "off":
+        ws8 = torch.empty(B.m * 8, dtype=torch.int32, device=dev)
+        _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err), st), "spgemm_bm_pack_ws8")
     uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
     uoff[0] = 0
     torch.cumsum(ucnt, 0, out=uoff[1:])
     del ucnt
-    nnz = int(uoff[-1])
+    nnz, e0 = torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
+    err.zero_()
     info.nnz = nnz
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
-    _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m, nwin,
-                                             lg_num, P(uoff), P(Cci), P(Cv), P(ovf), P(novf), ovf_cap, P(err), st),
-                  "spgemm_bm_numeric")
+    rows_mode = CONFIG.spgemm_bitmap_rows
+    if rows_mode != "off" and nwin <= 8 and (rows_mode == "on" or cfg == 0) and not (e0 & 8):
+        _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
+                                                      P(B.val), m, nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
+                                                      P(novf), ovf_cap, P(err), st), "spgemm_bm_numeric_rows")
+        info.rows_per_bin_num["bitmap_rows"] = 1
+    else:
+        _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
+                                                 nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap,
+                                                 P(err), st), "spgemm_bm_numeric")
     e, deferred = z.tolist()
     info.rows_per_bin_num["bitmap_units"] = nunits
     info.rows_per_bin_num["bitmap_cfg"] = cfg

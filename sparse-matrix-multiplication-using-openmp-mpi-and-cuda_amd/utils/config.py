@@ -44,6 +44,9 @@ class Config:
     spgemm_bitmap: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP", "auto", str))
     # its window configuration (csr_spgemm_bitmap.hip kCfgs), -1 = chosen from the row statistics
     spgemm_bitmap_cfg: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CFG", -1, int))
+    # row-major numeric kernel of the bitmap path (a row's windows back to back, <= 8 windows):
+    # "auto" = for the widest-window configuration, "on", "off"
+    spgemm_bitmap_rows: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_ROWS", "auto", str))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

@@ -1,0 +1,50 @@
+"""Shader-clock phase stamps of the bitmap-rank SpGEMM kernels (diagnostic build
+path: the stamps are off in normal runs).  usage: python tools/bm_stamps.py [n] [density] [cfg]"""
+import ctypes as C
+import sys
+import time
+
+sys.path.insert(0, ".")
+import os  # noqa: E402
+
+# the stamps are compiled in only in a diagnostic variant of the library
+from spmm_amd import _build  # noqa: E402
+
+os.environ["SPMM_HIP_LIB"] = _build.build_hip(out=os.path.join(_build.LIB_DIR, "diag", "libspmm_hip_stamps.so"),
+                                              extra=["-DSPMM_BM_STAMPS"])
+import torch  # noqa: E402
+
+import spmm_amd  # noqa: E402,F401
+from spmm_amd import _native  # noqa: E402
+from spmm_amd.ops import spgemm as SG  # noqa: E402
+from spmm_amd.utils import gen_csr  # noqa: E402
+from spmm_amd.utils.config import CONFIG  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+d = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-4
+if len(sys.argv) > 3:
+    CONFIG.spgemm_bitmap_cfg = int(sys.argv[3])
+dev = torch.device("cuda")
+A = gen_csr.uniform_csr(n, n, d, seed=1, device=dev)
+B = gen_csr.uniform_csr(n, n, d, seed=2, device=dev)
+lib = _native.hip()
+SG.spgemm(A, B)
+torch.cuda.synchronize()
+t = time.perf_counter()
+SG.spgemm(A, B)
+torch.cuda.synchronize()
+plain = time.perf_counter() - t
+lib.spmm_spgemm_bm_stamps(1, None)
+info = SG.SpgemmInfo()
+SG.spgemm(A, B, info)
+out = (C.c_ulonglong * 8)()
+lib.spmm_spgemm_bm_stamps(-1, out)
+lib.spmm_spgemm_bm_stamps(0, None)
+st = list(out)
+units = max(st[7], 1)
+names = ["num staging", "num pass1", "num scan", "num pass2", "num writeout", "count stage+OR", "count pop+clear"]
+tot = sum(st[:5])
+print(f"n={n} d={d} plain step {plain * 1e3:.2f} ms  info={info.rows_per_bin_num}")
+for i, nm in enumerate(names):
+    share = f"{100 * st[i] / tot:5.1f} %" if i < 5 and tot else ""
+    print(f"{nm:18s} {st[i] / units:10.0f} cycles/unit {share}")
