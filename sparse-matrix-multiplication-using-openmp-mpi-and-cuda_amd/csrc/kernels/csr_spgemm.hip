@@ -1383,7 +1383,8 @@ SPMM_EXPORT int spmm_spgemm_compact(const int64_t* src_off, const int64_t* dst_o
 SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int ncols,
                                        int64_t* bsplit, void* stream) {
   if (mb <= 0) return 0;
-  if (mb > (1ll << 34)) return (int)hipErrorInvalidValue;   // grid of 8 lanes per row
+  // 8 lanes per row, one grid: gridDim.x * 256 work-items must stay below 2^32
+  if (mb > ((int64_t)UINT32_MAX - 255) / 8) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(spgemm_row_splits, dim3((unsigned)((mb * 8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      Brp, Bci, mb, ncols, bsplit);
   SPMM_LAUNCH_CHECK();

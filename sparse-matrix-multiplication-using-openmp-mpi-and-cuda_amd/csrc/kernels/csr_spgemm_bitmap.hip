@@ -902,6 +902,170 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   BM_STAMP_FLUSH();
 }
 
+// ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
+// The count kernel of the same row pipeline: one window's bitmap (16 KB at
+// W = 2^17) per workgroup, so eight 256-thread workgroups share a CU and
+// hide each other's B-load latency (the 8-window, 128 KB-bitmap count kernel
+// runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
+// wave's own bitmap rows, clear of the same rows, one barrier.
+template <int LGW, int NT, int RR, int CCAP>
+__global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {
+  const BmArgs& p = ra.a;
+  constexpr int NW = NT / 64;
+  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  static_assert(WPW % 64 == 0, "geometry");
+
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
+  __shared__ int wsum[2 * NW];
+  __shared__ int csum[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = p.lg;
+  const int Gl = 1 << lg;
+  const int ngrp = NW << (6 - lg);
+  const int gid = (w << (6 - lg)) + (lane >> lg);
+  const int gl = lane & (Gl - 1);
+  const int nwin = p.nwin;
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  if (*p.err & 8) return;   // ws8 lengths truncated: the host re-counts with spgemm_bm (uniform exit)
+
+  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+
+  const int64_t NG = gridDim.x;
+  const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+  const int64_t m = p.m;
+  int64_t row = me;
+  int cna = 0;
+  uint4 cwa = make_uint4(0, 0, 0, 0);
+  uint32_t cwb = 0;
+  int n1a = 0, n1b = 0, n2a = 0, n2b = 0, njj = 0;
+  uint4 nwa = make_uint4(0, 0, 0, 0);
+  uint32_t nwb = 0;
+  auto ld_arp = [&](int64_t r, int& a, int& b) {
+    if (r < m) {
+      a = (int)p.Arp[r + vz];
+      b = (int)p.Arp[r + 1 + vz];
+    }
+  };
+  auto ld_entries = [&](int64_t r) {
+    if (r < m) {
+      const int a0 = __builtin_amdgcn_readfirstlane(n1a), na = __builtin_amdgcn_readfirstlane(n1b) - a0;
+      if (tid < na) njj = p.Aci[a0 + tid];
+    }
+  };
+  auto ld_bounds = [&](int64_t r) {
+    if (r < m) {
+      const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
+      if (tid < na) {
+        nwa = ra.ws8[2 * (int64_t)njj];
+        nwb = ra.ws8[2 * (int64_t)njj + 1].x;
+      }
+    }
+  };
+  auto take_next = [&]() {
+    cna = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
+    cwa = nwa;
+    cwb = nwb;
+    n1a = n2a;
+    n1b = n2b;
+  };
+  ld_arp(row, n1a, n1b);
+  ld_entries(row);
+  ld_bounds(row);
+  ld_arp(row + NG, n2a, n2b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  take_next();
+  __syncthreads();
+
+  for (; row < m; row += NG) {
+    const int na = cna;
+    uint32_t bq = cwa.x;
+    for (int q = 0; q < nwin; ++q) {
+      const bool last = q == nwin - 1;
+      if (q == 0) {
+        ld_entries(row + NG);
+        ld_arp(row + 2 * NG, n2a, n2b);
+      }
+      if (last) ld_bounds(row + NG);
+      const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
+      int len = 0, nch = 0;
+      if (tid < na && tid < NT) {
+        len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
+        nch = (len + Gl - 1) >> lg;
+      }
+      const uint32_t b0 = bq;
+      bq += (uint32_t)len;
+      const int clo = q << LGW;
+      const int64_t u = row * nwin + q;
+      int pre, plen, TC, P;
+      bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+      for (int cb = 0; cb < TC; cb += CCAP) {
+        const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
+        const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
+        for (int kk = k0; kk < k1; ++kk) {
+          const int rem = len - (kk << lg);
+          desc[pre + kk - cb] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
+        }
+        __syncthreads();
+        const int nr = (TCb + ngrp - 1) / ngrp;
+        for (int i0 = 0; i0 < nr; i0 += RR) {
+          uint2 ds[RR];
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            const int t = gid + (i0 + d) * ngrp;
+            ds[d] = desc[t < TCb ? t : TCb - 1];
+          }
+          int x[RR];
+          uint32_t okm = 0;
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            const int t = gid + (i0 + d) * ngrp;
+            const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
+            okm |= (ok ? 1u : 0u) << d;
+            x[d] = 0;
+            if (i0 + d < nr) x[d] = p.Bci[ds[d].x + (ok ? (uint32_t)gl : 0u)];   // wave-uniform guard
+          }
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            if ((okm >> d) & 1u) {
+              const int cc = x[d] - clo;
+              atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+            }
+          }
+        }
+        __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
+      }
+      if (last) take_next();   // after this unit's B loads: every older load has landed
+      if (P == 0) {   // uniform: nothing was ORed
+        if (tid == 0) p.ucnt[u] = 0;
+        __syncthreads();   // wsum reads done before the next scan
+        continue;
+      }
+      // popcount of this wave's bitmap rows, clearing them as they are read
+      int cnt = 0;
+#pragma unroll
+      for (int kk = 0; kk < WPT; ++kk) {
+        const int wd = w * WPW + kk * 64 + lane;
+        cnt += __popcll(bm[wd]);
+        bm[wd] = 0ull;
+      }
+      cnt = bm_wave_sum(cnt);
+      if (lane == 0) csum[w] = cnt;
+      __syncthreads();
+      if (tid == 0) {
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) t += csum[i];
+        p.ucnt[u] = t;
+      }
+    }
+  }
+}
+
 // ws8[j] from ws (nwin <= 8): first index + 16-bit window lengths; err bit 3
 // if a window segment of some B row is 65536 entries or longer.
 __global__ __launch_bounds__(256) void bm_pack_ws8(const uint32_t* __restrict__ ws, int64_t mb, int nwin,
@@ -1003,6 +1167,25 @@ struct BmRowKernel {
   static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;   // (the pipeline registers cost 2 rounds)
   static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
 };
+
+template <int C>
+struct BmRowCountKernel {
+  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, kFastNT, 8, 256>;
+};
+
+template <int C>
+int bm_count_rows(const BmRowArgs& ra, hipStream_t s) {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, BmRowCountKernel<C>::k, kFastNT, 0) != hipSuccess || per <= 0)
+    per = 1;
+  int64_t g = (int64_t)per * ncu;
+  if (ra.a.m < g) g = ra.a.m;
+  hipLaunchKernelGGL(BmRowCountKernel<C>::k, dim3((unsigned)g), dim3(kFastNT), 0, s, ra);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
 
 template <int C>
 int bm_numeric_rows(const BmRowArgs& ra, hipStream_t s) {
@@ -1130,5 +1313,24 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
     case 0: return bm_numeric_rows<0>(ra, s);
     case 1: return bm_numeric_rows<1>(ra, s);
     default: return bm_numeric_rows<2>(ra, s);
+  }
+}
+
+// Row-major count (nwin <= 8, every A row <= 256 entries, ws8 packed): same
+// output as spmm_spgemm_bm_count.  Returns without counting when err bit 3
+// is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
+SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
+                                          const int32_t* Bci, int64_t m, int nwin, int lg, int32_t* ucnt,
+                                          int32_t* err, void* stream) {
+  if (m <= 0) return 0;
+  if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
+  BmRowArgs ra{BmArgs{Arp, Aci, nullptr, nullptr, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, 0, 0, err},
+               (const uint4*)ws8};
+  hipStream_t s = (hipStream_t)stream;
+  switch (cfg) {
+    case 0: return bm_count_rows<0>(ra, s);
+    case 1: return bm_count_rows<1>(ra, s);
+    default: return bm_count_rows<2>(ra, s);
   }
 }

@@ -734,9 +734,13 @@ int run(const Options& o, int rank, int world, double t_start) {
     Range r("prune + write");
     const double t2 = now_s();
     Mat final_;
-    if (gpu) {
+    if (N <= 0) {
+      final_.k = k;   // empty chain: an empty product (0 x 0, no tiles), not a dereference of nothing
+    } else if (gpu) {
+      A4_CHECK(gm.has_value(), "rank 0 holds no partial product");
       final_ = dev_download(dev_prune(std::move(*gm), s), s);
     } else {
+      A4_CHECK(cpart.has_value(), "rank 0 holds no partial product");
       final_ = cpu_prune(std::move(*cpart));
     }
     if (o.dump) dump("result", final_);

@@ -55,6 +55,7 @@ _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
@@ -551,25 +552,40 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     z = torch.zeros(2, dtype=torch.int32, device=dev)   # err, deferred count
     err, novf = z[0:1], z[1:2]
     ucnt = torch.empty(nunits, dtype=torch.int32, device=dev)
-    _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, lg_count, P(ucnt),
-                                           P(err), st), "spgemm_bm_count")
+    # row-major kernels (a row's windows back to back): <= 8 windows, packed
+    # 16-bit window lengths (ws8); the count kernel also needs A rows <= 256
+    rows_mode = CONFIG.spgemm_bitmap_rows
     ws8 = None
-    if nwin <= 8 and CONFIG.spgemm_bitmap_rows != "off":
+    if nwin <= 8 and rows_mode != "off":
         ws8 = torch.empty(B.m * 8, dtype=torch.int32, device=dev)
         _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err), st), "spgemm_bm_pack_ws8")
-    uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
-    uoff[0] = 0
-    torch.cumsum(ucnt, 0, out=uoff[1:])
+    count_rows = ws8 is not None and pre is not None and pre.get("amax", 1 << 30) <= 256
+
+    def count(use_rows: bool):
+        if use_rows:
+            _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8), P(B.col), m, nwin,
+                                                        lg_num, P(ucnt), P(err), st), "spgemm_bm_count_rows")
+        else:
+            _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, lg_count,
+                                                   P(ucnt), P(err), st), "spgemm_bm_count")
+        uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
+        uoff[0] = 0
+        torch.cumsum(ucnt, 0, out=uoff[1:])
+        return uoff, torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
+
+    uoff, (nnz, e0) = count(count_rows)
+    if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
+        ws8 = None
+        if count_rows:
+            uoff, (nnz, e0) = count(False)
     del ucnt
-    nnz, e0 = torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
     err.zero_()
     info.nnz = nnz
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
-    rows_mode = CONFIG.spgemm_bitmap_rows
-    if rows_mode != "off" and nwin <= 8 and (rows_mode == "on" or cfg == 0) and not (e0 & 8):
+    if ws8 is not None and (rows_mode == "on" or cfg == 0):
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), m, nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
                                                       P(novf), ovf_cap, P(err), st), "spgemm_bm_numeric_rows")

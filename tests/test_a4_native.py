@@ -79,6 +79,19 @@ def test_a4_missing_size_file(tmp_path, a4_bin):
     assert "Cannot open size file!" in r.stderr
 
 
+@pytest.mark.parametrize("p", [1, 3])
+def test_a4_empty_chain_writes_empty_matrix(tmp_path, a4_bin, p):
+    """A size file with N = 0: rank 0 writes an empty product instead of
+    dereferencing a partial that was never built."""
+    folder = tmp_path / "in"
+    folder.mkdir()
+    (folder / "size").write_text("0 2\n")
+    out = str(tmp_path / "matrix")
+    r = _run(a4_bin, p, str(folder), "--device", "cpu", "--out", out)
+    assert open(out).read() == "0 0\n0\n"
+    assert len(re.findall(r"time taken [0-9.e+-]+ seconds", r.stdout)) == p
+
+
 def test_a4_checkpoint_resume_and_metrics(tmp_path, a4_bin):
     mats, folder = _chain(tmp_path, 8, seed=3)
     ck = str(tmp_path / "ck")
