@@ -168,6 +168,7 @@ struct BmArgs {
   uint32_t* novf;          //          and their count
   int64_t ovf_cap;
   int64_t cap;             // numeric: entries allocated for C (a unit outside it is an error, never a write)
+  const uint2* Bcv;        // row-major numeric: B as interleaved (column, value bits), or null
   int32_t* err;            // bit 0: a deferred unit exceeds the reload budget (host falls back)
                            // bit 1: count / numeric disagree (kernel invariant)
                            // bit 2: deferred list full (host falls back)
@@ -627,7 +628,7 @@ struct BmRowArgs {
   const uint4* ws8;
 };
 
-template <int LGW, int NT, int PCAP, int R, int CCAP>
+template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
@@ -799,8 +800,14 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
           x[d] = 0;
           b[d] = 0.f;
           if (d < nr) {   // wave-uniform
-            x[d] = p.Bci[f[d]];
-            b[d] = p.Bv[f[d]];
+            if constexpr (CV) {   // one 8-byte load: a chunk's products share cache lines
+              const uint2 e = p.Bcv[f[d]];
+              x[d] = (int)e.x;
+              b[d] = __uint_as_float(e.y);
+            } else {
+              x[d] = p.Bci[f[d]];
+              b[d] = p.Bv[f[d]];
+            }
           }
         }
         // A values while the B loads are in flight
@@ -900,6 +907,351 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
     }
   }
   BM_STAMP_FLUSH();
+}
+
+// ---- software-pipelined row-major numeric kernel (4 <= nwin <= 8) ----------
+// The row-major kernel with the B loads of unit k+1 in flight during unit k:
+//   1. issue unit k's B values; OR its columns (loaded one unit ago)   (barrier)
+//   2. unit k+1's descriptor scan; unit k's wave-local rank prefixes    (barrier)
+//   3. unit k+1's descriptors; unit k's pass 2 (slot owners)           (barrier)
+//   4. ISSUE unit k+1's B columns; unit k's duplicate adds            (barrier)
+//   5. unit k's C slots out (a FIXED number of buffer stores per thread:
+//      lanes past the unit's count fall outside the buffer range and are
+//      dropped) and the bitmap clear                                   (barrier)
+// Two register sets alternate through a 2x unrolled body, so an in-flight
+// register is never copied, and the fixed store count lets the compiler wait
+// for unit k+1's loads with a counted vmcnt instead of waiting for the
+// stores too.  The row pipeline is the row-major kernel's, one window earlier.
+template <int LGW, int NT, int PCAP, int R, int CCAP>
+__global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
+  const BmArgs& p = ra.a;
+  constexpr int NW = NT / 64;
+  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  constexpr int NWO = PCAP / NT;   // write-out rounds
+  static_assert(WPW % 64 == 0 && PCAP < 65536 && PCAP % NT == 0, "geometry");
+
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
+  __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
+  __shared__ uint32_t desc[CCAP];   // chunk: first B index << 5 | (valid lanes - 1)   (B.nnz < 2^27, lanes <= 32)
+  __shared__ int64_t suo[16];       // uoff of the current row's windows
+  __shared__ float dval[2][CCAP];   // by unit parity: unit k's survive unit k+1's staging
+  __shared__ int wsum[3 * NW];
+  __shared__ int sdup;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = p.lg;
+  const int Gl = 1 << lg;
+  const int ngrp = NW << (6 - lg);
+  const int gid = (w << (6 - lg)) + (lane >> lg);
+  const int gl = lane & (Gl - 1);
+  const int nwin = p.nwin;
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+
+  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+  if (tid == 0) sdup = 0;
+
+  const int64_t NG = gridDim.x;
+  const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+  const int64_t m = p.m;
+
+  // row pipeline (see spgemm_bm_rows)
+  int cna = 0;
+  float cav = 0.f;
+  uint32_t cw1 = 0, cw2 = 0, cw3 = 0, cw4 = 0;   // packed 16-bit window lengths of the current row
+  int n1a = 0, n1b = 0, n2a = 0, n2b = 0, njj = 0;
+  float nav = 0.f;
+  uint4 nwa = make_uint4(0, 0, 0, 0);
+  uint32_t nwb = 0;
+  int64_t nuo = 0;
+  auto ld_arp = [&](int64_t r, int& a, int& b) {
+    if (r < m) {
+      a = (int)p.Arp[r + vz];
+      b = (int)p.Arp[r + 1 + vz];
+    }
+  };
+  auto ld_entries = [&](int64_t r) {
+    if (r < m) {
+      const int a0 = __builtin_amdgcn_readfirstlane(n1a), na = __builtin_amdgcn_readfirstlane(n1b) - a0;
+      if (tid < na) {
+        njj = p.Aci[a0 + tid];
+        nav = p.Av[a0 + tid];
+      }
+    }
+  };
+  auto ld_bounds = [&](int64_t r) {
+    if (r < m) {
+      const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
+      if (tid < na) {
+        nwa = ra.ws8[2 * (int64_t)njj];
+        nwb = ra.ws8[2 * (int64_t)njj + 1].x;
+      }
+      if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
+    }
+  };
+  uint32_t bq = 0;   // first B index of the next window to stage (this thread's entry)
+  // next row -> current row; the row's offsets go to LDS (read after the
+  // next barrier: every reader of the old ones has passed it)
+  auto take_next = [&]() {
+    cna = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
+    cav = nav;
+    bq = nwa.x;
+    cw1 = nwa.y;
+    cw2 = nwa.z;
+    cw3 = nwa.w;
+    cw4 = nwb;
+    if (w == 0 && lane <= nwin) suo[lane] = nuo;
+    n1a = n2a;
+    n1b = n2b;
+  };
+
+  struct U {          // wave-uniform state of a unit
+    int64_t row;
+    int q, u, clo, want, TC, nr, valid, par;
+    int64_t off;
+  };
+  auto next_unit = [&](const U& x) {
+    U y{};
+    y.row = x.q + 1 < nwin ? x.row : x.row + NG;
+    y.q = x.q + 1 < nwin ? x.q + 1 : 0;
+    y.par = x.par ^ 1;
+    return y;
+  };
+  // per-thread staging of unit y (row registers current for y.row)
+  auto stage_local = [&](const U& y, int& len, int& nch, uint32_t& b0) {
+    len = 0;
+    nch = 0;
+    b0 = bq;
+    if (y.row < m && tid < cna && tid < NT) {
+      // (select VALUES: a ternary over the captured lvalues selects their
+      // addresses and pins them to the scratch stack)
+      const uint32_t a1 = cw1, a2 = cw2, a3 = cw3, a4 = cw4;
+      const uint32_t wl = y.q < 4 ? (y.q < 2 ? a1 : a2) : (y.q < 6 ? a3 : a4);
+      len = (int)((wl >> (16 * (y.q & 1))) & 0xffffu);
+      nch = (len + Gl - 1) >> lg;
+    }
+    bq += (uint32_t)len;
+  };
+  // after the scan: descriptors, offsets, deferral
+  auto stage_finish = [&](U& y, int len, int nch, uint32_t b0, int pre, int TC, int P) {
+    y.u = (int)(y.row * nwin + y.q);
+    y.clo = y.q << LGW;
+    y.TC = TC;
+    y.nr = (TC + ngrp - 1) / ngrp;
+    y.valid = 0;
+    if (y.row >= m) return;
+    y.off = bm_rfl64(suo[y.q]);
+    y.want = (int)(bm_rfl64(suo[y.q + 1]) - y.off);
+    const bool too_big = cna > NT || P > PCAP || TC > CCAP || TC > R * ngrp;
+    if (P == 0) return;
+    if (too_big) {
+      if (tid == 0) {
+        const uint32_t at = atomicAdd(p.novf, 1u);
+        if ((int64_t)at < p.ovf_cap) p.ovf[at] = y.u;
+        else atomicOr(p.err, 4);
+      }
+      return;
+    }
+    y.valid = 1;
+    for (int kk = 0; kk < nch; ++kk) {
+      const int rem = len - (kk << lg);
+      desc[pre + kk] = ((b0 + ((uint32_t)kk << lg)) << 5) | (uint32_t)((rem < Gl ? rem : Gl) - 1);
+      dval[y.par][pre + kk] = cav;
+    }
+  };
+  // B index of round d of unit y for this lane (ok: a valid product)
+  auto addr = [&](const U& y, uint32_t (&f)[R], uint32_t& okm) {
+    okm = 0;
+#pragma unroll
+    for (int d = 0; d < R; ++d) {
+      const int t = gid + d * ngrp;
+      const uint32_t ds = desc[t < y.TC ? t : y.TC - 1];
+      const bool ok = (t < y.TC) & ((uint32_t)gl <= (ds & 31u));
+      okm |= (ok ? 1u : 0u) << d;
+      f[d] = (ds >> 5) + (ok ? (uint32_t)gl : 0u);
+    }
+  };
+  // unit y's B columns (one unit ahead) / B values (at the top of its own unit)
+  auto issue_cols = [&](const U& y, int (&cc)[R], uint32_t& okm) {
+    uint32_t f[R];
+    addr(y, f, okm);
+#pragma unroll
+    for (int d = 0; d < R; ++d) {
+      cc[d] = 0;
+      if (d < y.nr) cc[d] = p.Bci[f[d]];   // wave-uniform guard
+    }
+  };
+  auto issue_vals = [&](const U& y, float (&vv)[R]) {
+    uint32_t f[R], okm;
+    addr(y, f, okm);
+#pragma unroll
+    for (int d = 0; d < R; ++d) {
+      vv[d] = 0.f;
+      if (d < y.nr) vv[d] = p.Bv[f[d]];
+    }
+  };
+
+  // ---- prologue: the row pipeline, then stage + issue the first unit ------
+  ld_arp(me, n1a, n1b);
+  ld_entries(me);
+  ld_bounds(me);
+  ld_arp(me + NG, n2a, n2b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  take_next();
+  U X{};
+  X.row = me;
+  X.q = 0;
+  X.par = 0;
+  int cA[R], cB[R];
+  float vC[R];
+  uint32_t okA = 0, okB = 0;
+  {
+    int len, nch, pre, plen, TC, P;
+    uint32_t b0;
+    stage_local(X, len, nch, b0);
+    bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+    stage_finish(X, len, nch, b0, pre, TC, P);
+    __syncthreads();
+    okA = 0;
+    if (X.valid) issue_cols(X, cA, okA);
+  }
+
+  auto body = [&](U& X, int (&cC)[R], uint32_t okC, int (&cN)[R], uint32_t& okN) {
+    const bool lastq = X.q == nwin - 1;
+    if (X.q == 0) {
+      ld_entries(X.row + NG);
+      ld_arp(X.row + 2 * NG, n2a, n2b);
+    }
+    if (X.q == nwin - 2) ld_bounds(X.row + NG);
+    // ---- 1. unit X: its B values in flight, OR its columns ---------------
+    uint32_t dupm = 0;
+    if (X.valid) {
+      issue_vals(X, vC);   // used in pass 2, two barriers later
+      uint32_t old[R];
+#pragma unroll
+      for (int d = 0; d < R; ++d) cC[d] = ((okC >> d) & 1u) ? cC[d] - X.clo : -1;
+#pragma unroll
+      for (int d = 0; d < R; ++d) {
+        old[d] = 0u;
+        if (cC[d] >= 0) old[d] = atomicOr(bm32 + (cC[d] >> 5), 1u << (cC[d] & 31));
+      }
+#pragma unroll
+      for (int d = 0; d < R; ++d) dupm |= (cC[d] >= 0 ? (old[d] >> (cC[d] & 31)) & 1u : 0u) << d;
+    }
+    if (lastq) take_next();   // the next row's loads were issued before unit X's: landed
+    if (dupm) sdup = 1;
+    __syncthreads();   // (a) X's bitmap complete
+    // ---- 2. unit Y's staging scan; unit X's wave-local rank prefixes ---------
+    U Y = next_unit(X);
+    int len, nch;
+    uint32_t b0;
+    stage_local(Y, len, nch, b0);
+    const int xa = bm_wave_incl(nch), xb = bm_wave_incl(len);
+    int wtot = 0;
+    if (X.valid) {
+#pragma unroll
+      for (int kk = 0; kk < WPT; ++kk) {
+        const int wd = w * WPW + kk * 64 + lane;
+        const int cnt = __popcll(bm[wd]);
+        const int incl = bm_wave_incl(cnt);
+        pre16[wd] = (uint16_t)(wtot + incl - cnt);
+        wtot += __builtin_amdgcn_readlane(incl, 63);
+      }
+    }
+    if (lane == 63) {
+      wsum[w] = xa;
+      wsum[NW + w] = xb;
+    }
+    if (lane == 0) wsum[2 * NW + w] = wtot;
+    __syncthreads();   // (b) scans + X's prefixes visible
+    // ---- 3. unit Y's descriptors; unit X's pass 2 (owners) -----------------
+    int qa = 0, TC = 0, P = 0, total = 0;
+    int wt[NW];   // rank total of every wave's bitmap block (uniform)
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int sa = wsum[i], sb = wsum[NW + i], sc = __builtin_amdgcn_readfirstlane(wsum[2 * NW + i]);
+      qa += (i < w) ? sa : 0;
+      TC += sa;
+      P += sb;
+      wt[i] = sc;
+      total += sc;
+    }
+    const int any_dup = sdup;
+    stage_finish(Y, len, nch, b0, qa + xa - nch, TC, P);
+    static_assert((WPW & (WPW - 1)) == 0, "power-of-two wave blocks");
+    // (the base is a sum of compares over scalars: a select chain over an
+    // array gets folded into a dynamically indexed stack load)
+    auto rank = [&](int c) {
+      const int wd = c >> 6;
+      const int blk = wd / WPW;
+      int base = 0;
+#pragma unroll
+      for (int i = 0; i < NW - 1; ++i) base += blk > i ? wt[i] : 0;
+      return base + (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (c & 63)) - 1ull));
+    };
+    if (X.valid) {
+      // B values times a(i, j) (this unit's parity buffer survived unit Y's staging)
+#pragma unroll
+      for (int d = 0; d < R; ++d) {
+        const int t = gid + d * ngrp;
+        vC[d] *= dval[X.par][t < X.TC ? t : X.TC - 1];
+      }
+#pragma unroll
+      for (int d0 = 0; d0 < R; d0 += 4) {
+        int r[4];
+#pragma unroll
+        for (int dd = 0; dd < 4 && d0 + dd < R; ++dd) r[dd] = rank(cC[d0 + dd] >= 0 ? cC[d0 + dd] : 0);
+#pragma unroll
+        for (int dd = 0; dd < 4 && d0 + dd < R; ++dd) {
+          const int d = d0 + dd;
+          if (cC[d] >= 0 && !((dupm >> d) & 1u))
+            items[r[dd]] = ((unsigned long long)__float_as_uint(vC[d]) << 32) | (uint32_t)(cC[d] + X.clo);
+        }
+      }
+    }
+    __syncthreads();   // (c) Y's descriptors visible, X's owner slots written
+    // ---- 4. unit X's duplicates; ISSUE unit Y's B columns ------------------
+    // (the duplicates first: any wait in their code would otherwise also wait
+    // for Y's loads)
+    if (tid == 0) sdup = 0;
+    if (X.valid && any_dup) {
+#pragma unroll
+      for (int d = 0; d < R; ++d)
+        if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(cC[d])]) + 1, vC[d]);
+    }
+    okN = 0;
+    if (Y.valid) issue_cols(Y, cN, okN);
+    __syncthreads();   // (d) X's slots final
+    // ---- 5. unit X's slots to C: NWO rounds, 2 buffer stores each ---------
+    if (X.valid) {
+      int lim = total;
+      if (X.want != total || X.off < 0 || X.off + total > p.cap) {   // never write outside the unit or C
+        if (tid == 0) atomicOr(p.err, 2);
+        lim = (X.off < 0 || X.off + total > p.cap) ? 0 : (total < X.want ? total : X.want);
+      }
+      const auto rc = __builtin_amdgcn_make_buffer_rsrc(p.Cci + X.off, (short)0, lim * 4, 0x00020000);
+      const auto rv = __builtin_amdgcn_make_buffer_rsrc(p.Cv + X.off, (short)0, lim * 4, 0x00020000);
+#pragma unroll
+      for (int it = 0; it < NWO; ++it) {
+        const int i = tid + it * NT;
+        const unsigned long long x = items[i];
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, rc, i * 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(x >> 32), rv, i * 4, 0, 0);
+      }
+      for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();   // (e) bitmap clear, items read
+    X = Y;
+  };
+
+  while (X.row < m) {
+    body(X, cA, okA, cB, okB);
+    if (X.row >= m) break;
+    body(X, cB, okB, cA, okA);
+  }
 }
 
 // ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
@@ -1165,7 +1517,8 @@ template <int C>
 struct BmRowKernel {
   static constexpr BmCfg K = kCfgs[C];
   static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;   // (the pipeline registers cost 2 rounds)
-  static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
+  static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false>;
+  static constexpr auto kcv = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true>;
 };
 
 template <int C>
@@ -1188,16 +1541,32 @@ int bm_count_rows(const BmRowArgs& ra, hipStream_t s) {
 }
 
 template <int C>
-int bm_numeric_rows(const BmRowArgs& ra, hipStream_t s) {
+struct BmPipeKernel {
+  static constexpr BmCfg K = kCfgs[C];
+  static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;
+  static constexpr auto k = spgemm_bm_pipe<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
+};
+
+template <typename Kern>
+int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s) {
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, BmRowKernel<C>::k, kFastNT, 0) != hipSuccess || per <= 0)
-    per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kFastNT, 0) != hipSuccess || per <= 0) per = 1;
   int64_t g = (int64_t)per * ncu;
   if (ra.a.m < g) g = ra.a.m;
-  hipLaunchKernelGGL(BmRowKernel<C>::k, dim3((unsigned)g), dim3(kFastNT), 0, s, ra);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(kFastNT), 0, s, ra);
   SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// pipe: the software-pipelined kernel (needs nwin >= 4 for its row pipeline)
+template <int C>
+int bm_numeric_rows(const BmRowArgs& ra, int pipe, hipStream_t s) {
+  const int rc = pipe       ? launch_rows(BmPipeKernel<C>::k, ra, s)
+                 : ra.a.Bcv ? launch_rows(BmRowKernel<C>::kcv, ra, s)
+                            : launch_rows(BmRowKernel<C>::k, ra, s);
+  if (rc) return rc;
   return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
 }
 
@@ -1241,7 +1610,7 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
   BmArgs a{Arp, Aci, nullptr, ws, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0,
-           err};
+           nullptr, err};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * ((nwin + kCfgs[cfg].nsub_count - 1) / kCfgs[cfg].nsub_count);
   switch (cfg) {
@@ -1259,7 +1628,7 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_
                                        int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
-  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, err};
+  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, nullptr, err};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * nwin;
   switch (cfg) {
@@ -1299,20 +1668,24 @@ SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin
 
 // Row-major numeric (nwin <= 8, ws8 from spmm_spgemm_bm_pack_ws8), then the
 // reload kernel over the deferred units; same contract as spmm_spgemm_bm_numeric.
+// Bcv: optional [nnz(B)] (column, value bits) pairs read by the row-major kernel.
 SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                             const void* ws8, const uint32_t* ws, const int32_t* Bci, const float* Bv,
+                                            const void* Bcv,
                                             int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap,
                                             int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                                            int32_t* err, void* stream) {
+                                            int32_t* err, int pipe, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
-  BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, err},
+  if (pipe && (nwin < 4 || lg > 5)) return (int)hipErrorInvalidValue;   // (+ B.nnz < 2^27: host)
+  BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
+                      (const uint2*)Bcv, err},
                (const uint4*)ws8};
   hipStream_t s = (hipStream_t)stream;
   switch (cfg) {
-    case 0: return bm_numeric_rows<0>(ra, s);
-    case 1: return bm_numeric_rows<1>(ra, s);
-    default: return bm_numeric_rows<2>(ra, s);
+    case 0: return bm_numeric_rows<0>(ra, pipe, s);
+    case 1: return bm_numeric_rows<1>(ra, pipe, s);
+    default: return bm_numeric_rows<2>(ra, pipe, s);
   }
 }
 
@@ -1325,7 +1698,7 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   BmRowArgs ra{BmArgs{Arp, Aci, nullptr, nullptr, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr,
-                      nullptr, 0, 0, err},
+                      nullptr, 0, 0, nullptr, err},
                (const uint4*)ws8};
   hipStream_t s = (hipStream_t)stream;
   switch (cfg) {

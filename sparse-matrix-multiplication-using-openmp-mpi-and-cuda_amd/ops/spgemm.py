@@ -56,8 +56,8 @@ _native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_v
 _native.register_hip("spmm_spgemm_bm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
+                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
@@ -585,11 +585,17 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
-    if ws8 is not None and (rows_mode == "on" or cfg == 0):
+    if ws8 is not None and (rows_mode in ("on", "pipe", "nopipe") or cfg == 0):
+        pipe = rows_mode == "pipe" and nwin >= 4 and lg_num <= 5 and B.nnz < (1 << 27)
+        # the row-major kernel reads B as interleaved (column, value) pairs: one
+        # 8-byte stream per chunk instead of two 4-byte ones (fewer partial lines)
+        Bcv = None if pipe or not CONFIG.spgemm_bitmap_cv else torch.stack([B.col, B.val.view(torch.int32)], 1)
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
-                                                      P(B.val), m, nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
-                                                      P(novf), ovf_cap, P(err), st), "spgemm_bm_numeric_rows")
-        info.rows_per_bin_num["bitmap_rows"] = 1
+                                                      P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
+                                                      lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
+                                                      P(novf), ovf_cap, P(err), int(pipe), st),
+                      "spgemm_bm_numeric_rows")
+        info.rows_per_bin_num["bitmap_rows"] = 2 if pipe else 1
     else:
         _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
                                                  nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap,

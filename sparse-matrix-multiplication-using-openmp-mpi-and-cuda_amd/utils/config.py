@@ -47,6 +47,8 @@ class Config:
     # row-major numeric kernel of the bitmap path (a row's windows back to back, <= 8 windows):
     # "auto" = for the widest-window configuration, "on", "off"
     spgemm_bitmap_rows: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_ROWS", "auto", str))
+    # row-major numeric kernel reads an interleaved (column, value) copy of B (1) or the two arrays (0)
+    spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))

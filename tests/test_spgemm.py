@@ -565,6 +565,22 @@ def test_spgemm_gpu_bitmap_matches_binned(monkeypatch, cfg, m, k, n, da, db):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows", ["pipe", "nopipe", "off"])
+def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows):
+    """The three numeric kernels of the widest-window configuration on a
+    product with 5 windows per row (ragged last window): software-pipelined
+    row-major, row-major, per-unit; all equal the binned path."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(1500, 20000, 0.002, seed=95, device=dev)
+    B = gen_csr.uniform_csr(20000, 600000, 1.4e-4, seed=96, device=dev)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_rows", rows)
+    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    assert info.rows_per_bin_num.get("bitmap_rows", 0) == {"pipe": 2, "nopipe": 1, "off": 0}[rows]
+
+
+@pytest.mark.gpu
 def test_spgemm_gpu_bitmap_deferred_units_and_fallback(monkeypatch):
     """Rows too long for the fast kernel (A rows > 256 entries, windows above
     its product capacity) are deferred to the reload kernel; a unit beyond the
