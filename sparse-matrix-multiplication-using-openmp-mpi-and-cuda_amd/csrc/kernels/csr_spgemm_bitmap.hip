@@ -1260,12 +1260,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
 // hide each other's B-load latency (the 8-window, 128 KB-bitmap count kernel
 // runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
 // wave's own bitmap rows, clear of the same rows, one barrier.
-template <int LGW, int NT, int RR, int CCAP>
-__global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {
+template <int LGW, int NSUB, int NT, int RR, int CCAP>
+__global__ __launch_bounds__(NT, NSUB == 1 ? 8 : 4) void spgemm_bm_rows_count(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
-  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
-  static_assert(WPW % 64 == 0, "geometry");
+  constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  constexpr int WORDS_PER_WIN = NWORD / NSUB;
+  static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
@@ -1336,8 +1337,8 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {
   for (; row < m; row += NG) {
     const int na = cna;
     uint32_t bq = cwa.x;
-    for (int q = 0; q < nwin; ++q) {
-      const bool last = q == nwin - 1;
+    for (int q = 0; q < nwin; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
+      const bool last = q + NSUB >= nwin;
       if (q == 0) {
         ld_entries(row + NG);
         ld_arp(row + 2 * NG, n2a, n2b);
@@ -1346,7 +1347,12 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {
       const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
       int len = 0, nch = 0;
       if (tid < na && tid < NT) {
-        len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
+        if constexpr (NSUB == 1) {
+          len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
+        } else {   // q even: windows q and q + 1 share one 32-bit word of lengths
+          static_assert(NSUB == 2, "count units of one or two windows");
+          len = (int)(wl & 0xffffu) + (q + 1 < nwin ? (int)(wl >> 16) : 0);
+        }
         nch = (len + Gl - 1) >> lg;
       }
       const uint32_t b0 = bq;
@@ -1393,7 +1399,11 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {
       }
       if (last) take_next();   // after this unit's B loads: every older load has landed
       if (P == 0) {   // uniform: nothing was ORed
-        if (tid == 0) p.ucnt[u] = 0;
+        if constexpr (NSUB == 1) {
+          if (tid == 0) p.ucnt[u] = 0;
+        } else if (tid < NSUB && q + tid < nwin) {
+          p.ucnt[u + tid] = 0;
+        }
         __syncthreads();   // wsum reads done before the next scan
         continue;
       }
@@ -1408,11 +1418,19 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {
       cnt = bm_wave_sum(cnt);
       if (lane == 0) csum[w] = cnt;
       __syncthreads();
-      if (tid == 0) {
+      if constexpr (NSUB == 1) {
+        if (tid == 0) {
+          int t = 0;
+#pragma unroll
+          for (int i = 0; i < NW; ++i) t += csum[i];
+          p.ucnt[u] = t;
+        }
+      } else if (tid < NSUB && q + tid < nwin) {   // window tid of the unit: the waves whose blocks lie in it
+        constexpr int WAVES_PER_WIN = WORDS_PER_WIN / WPW;
         int t = 0;
 #pragma unroll
-        for (int i = 0; i < NW; ++i) t += csum[i];
-        p.ucnt[u] = t;
+        for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[tid * WAVES_PER_WIN + i];
+        p.ucnt[u + tid] = t;
       }
     }
   }
@@ -1521,32 +1539,6 @@ struct BmRowKernel {
   static constexpr auto kcv = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true>;
 };
 
-template <int C>
-struct BmRowCountKernel {
-  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, kFastNT, 8, 256>;
-};
-
-template <int C>
-int bm_count_rows(const BmRowArgs& ra, hipStream_t s) {
-  int dev = 0, ncu = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, BmRowCountKernel<C>::k, kFastNT, 0) != hipSuccess || per <= 0)
-    per = 1;
-  int64_t g = (int64_t)per * ncu;
-  if (ra.a.m < g) g = ra.a.m;
-  hipLaunchKernelGGL(BmRowCountKernel<C>::k, dim3((unsigned)g), dim3(kFastNT), 0, s, ra);
-  SPMM_LAUNCH_CHECK();
-  return 0;
-}
-
-template <int C>
-struct BmPipeKernel {
-  static constexpr BmCfg K = kCfgs[C];
-  static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;
-  static constexpr auto k = spgemm_bm_pipe<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
-};
-
 template <typename Kern>
 int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s) {
   int dev = 0, ncu = 0, per = 0;
@@ -1559,6 +1551,26 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s) {
   SPMM_LAUNCH_CHECK();
   return 0;
 }
+
+// count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
+// per unit (32 KB, 4 per CU: a B row's column segment read once for both)
+template <int C, int NSUB>
+struct BmRowCountKernel {
+  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kFastNT, 8, 256>;
+};
+
+template <int C>
+int bm_count_rows(const BmRowArgs& ra, int nsub, hipStream_t s) {
+  return nsub == 2 ? launch_rows(BmRowCountKernel<C, 2>::k, ra, s) : launch_rows(BmRowCountKernel<C, 1>::k, ra, s);
+}
+
+template <int C>
+struct BmPipeKernel {
+  static constexpr BmCfg K = kCfgs[C];
+  static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;
+  static constexpr auto k = spgemm_bm_pipe<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
+};
+
 
 // pipe: the software-pipelined kernel (needs nwin >= 4 for its row pipeline)
 template <int C>
@@ -1693,7 +1705,7 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
 // output as spmm_spgemm_bm_count.  Returns without counting when err bit 3
 // is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
 SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
-                                          const int32_t* Bci, int64_t m, int nwin, int lg, int32_t* ucnt,
+                                          const int32_t* Bci, int64_t m, int nwin, int lg, int nsub, int32_t* ucnt,
                                           int32_t* err, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
@@ -1702,8 +1714,8 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
                (const uint4*)ws8};
   hipStream_t s = (hipStream_t)stream;
   switch (cfg) {
-    case 0: return bm_count_rows<0>(ra, s);
-    case 1: return bm_count_rows<1>(ra, s);
-    default: return bm_count_rows<2>(ra, s);
+    case 0: return bm_count_rows<0>(ra, nsub, s);
+    case 1: return bm_count_rows<1>(ra, nsub, s);
+    default: return bm_count_rows<2>(ra, nsub, s);
   }
 }

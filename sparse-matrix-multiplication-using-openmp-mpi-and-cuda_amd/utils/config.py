@@ -49,6 +49,8 @@ class Config:
     spgemm_bitmap_rows: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_ROWS", "auto", str))
     # row-major numeric kernel reads an interleaved (column, value) copy of B (1) or the two arrays (0)
     spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
+    # windows per row-major count unit (1: 16 KB bitmaps, 8 per CU; 2: 32 KB, 4 per CU)
+    spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.15, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))
