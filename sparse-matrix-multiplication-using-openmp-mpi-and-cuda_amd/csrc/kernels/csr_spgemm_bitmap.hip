@@ -1554,9 +1554,12 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s) {
 
 // count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
 // per unit (32 KB, 4 per CU: a B row's column segment read once for both)
+#ifndef SPMM_BM_COUNT_RR   // B loads in flight per thread (diagnostic builds: tools/bm_variants.py)
+#define SPMM_BM_COUNT_RR 8
+#endif
 template <int C, int NSUB>
 struct BmRowCountKernel {
-  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kFastNT, 8, 256>;
+  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kFastNT, SPMM_BM_COUNT_RR, 256>;
 };
 
 template <int C>
