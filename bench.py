@@ -77,7 +77,7 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
         step = lambda: MS.rowblock_spgemm(prob.A, prob.B, comm)  # noqa: E731
     flops_local = info.flops
     del C
-    total_flops = _allreduce_sum(comm, flops_local)
+    total_flops = int(_allreduce_sum(comm, flops_local))
     total_nnz = _allreduce_sum(comm, nnz_local)
     extra = dict(nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(total_nnz))
     return step, total_flops, extra, dict(model=model, n=n, density=density, dtype_values="fp32",
@@ -85,27 +85,23 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
 
 
 def run_rmat(comm, args):
-    """BASELINE config 5: R-MAT A.A^T, rows split over ranks at equal
-    intermediate-product counts.  C is kept resident when its product-count
-    bound fits this GPU; otherwise (scale 24: ~10^12 products, C of several
-    TB) it is produced in row panels that are consumed and freed one at a time
-    (``streamed_spgemm``; every product is still computed)."""
+    """BASELINE config 5: R-MAT A.A^T as a distributed 1D row-block workload
+    (``models.spgemm.RmatProblem``): every rank generates its share of the
+    edge chunks, the edges are shuffled to product-balanced row panels and
+    transposed with all-to-all-v exchanges, and each step all-gathers A^T and
+    multiplies the local A panel by it.  C is kept resident when its
+    product-count bound fits this GPU; otherwise (scale 24: ~10^12 products,
+    C of several TB) it is produced in row panels that are consumed and freed
+    one at a time (``streamed_spgemm``; every product is still computed)."""
     import torch
 
     from spmm_amd.models import spgemm as MS
-    from spmm_amd.ops.spgemm import SpgemmInfo, row_nprod, spgemm
-    from spmm_amd.parallel.partition import weighted_row_panels
-    from spmm_amd.utils import gen_csr
+    from spmm_amd.ops.spgemm import SpgemmInfo, row_nprod
 
-    A = gen_csr.rmat_csr(args.scale, args.edge_factor, seed=args.seed, device=comm.device)
-    At = A.transpose()
-    nprod = row_nprod(A, At)
-    lo, hi = weighted_row_panels(torch.cumsum(nprod, 0), comm.world)[comm.rank]
-    local_products = int(nprod[lo:hi].sum())
-    del nprod
-    Ap = A.row_slice(lo, hi)
-    del A
-    torch.cuda.empty_cache() if comm.device.type == "cuda" else None
+    prob = MS.RmatProblem.build(args.scale, args.edge_factor, comm, seed=args.seed)
+    local_products = int(row_nprod(prob.A, prob.right_operand(comm)).sum())
+    if comm.device.type == "cuda":
+        torch.cuda.empty_cache()
     stream = args.rmat_stream == "on" or (args.rmat_stream == "auto" and local_products > MS.stream_budget(comm.device))
     info = SpgemmInfo()
     if stream:
@@ -114,16 +110,17 @@ def run_rmat(comm, args):
         def consume(_lo, _hi, C):   # C's row panel is complete here; count it and let it go
             nnz[0] += C.nnz
 
-        MS.streamed_spgemm(Ap, At, consume, info=info)
-        step = lambda: MS.streamed_spgemm(Ap, At, consume)  # noqa: E731
+        prob.step(comm, info, consume)
+        step = lambda: prob.step(comm, None, consume)  # noqa: E731
     else:
-        C = spgemm(Ap, At, info)
+        C = prob.step(comm, info)
         del C
-        step = lambda: spgemm(Ap, At)  # noqa: E731
+        step = lambda: prob.step(comm)  # noqa: E731
     if comm.device.type == "cuda":
         torch.cuda.empty_cache()
     par = f"rowblock{comm.world}-product-balanced" + ("-streamed-C" if stream else "")
-    return step, _allreduce_sum(comm, info.flops), dict(nnz_C=int(_allreduce_sum(comm, info.nnz)), c_streamed=stream), dict(
+    return step, int(_allreduce_sum(comm, info.flops)), dict(
+        nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(_allreduce_sum(comm, info.nnz)), c_streamed=stream), dict(
         model=f"R-MAT scale-{args.scale} A.A^T", scale=args.scale, edge_factor=args.edge_factor, global_batch=1,
         seq_len=1 << args.scale, parallelism=par)
 

@@ -37,8 +37,8 @@ import torch.distributed as dist
 from ..ops.csr import CSR
 from ..ops.spgemm import SpgemmInfo, csr_sum, spgemm
 from ..parallel.comm import Comm
-from ..parallel.partition import row_panels
-from ..utils.gen_csr import uniform_csr
+from ..parallel.partition import row_panels, weighted_row_panels
+from ..utils.gen_csr import pattern_csr, rmat_edges, rmat_nchunks, rmat_perm, uniform_csr
 
 
 def _allgather_equal(comm: Comm, t: torch.Tensor) -> torch.Tensor:
@@ -317,6 +317,108 @@ class UniformProblem:
         lo, hi = self.rows
         A = uniform_csr(self.n, self.n, self.density, seed=self.seed, device=self.A.device)
         return A.col_slice(lo, hi)
+
+
+def _allreduce_sum_(comm: Comm, t: torch.Tensor) -> torch.Tensor:
+    """In-place sum over ranks (RCCL on the device, gloo through the host)."""
+    if not comm.is_dist:
+        return t
+    if comm.backend == "nccl":
+        dist.all_reduce(t)
+        return t
+    h = t.cpu()
+    dist.all_reduce(h)
+    t.copy_(h)
+    return t
+
+
+def shuffle_pairs(comm: Comm, rows: torch.Tensor, cols: torch.Tensor, cuts: List[int]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Send every (row, col) pair to the rank that owns ``row`` (rank r owns
+    [cuts[r], cuts[r + 1])): one all-to-all-v of the counts, one of the
+    packed int64 pairs.  Returns the pairs this rank received (any order)."""
+    if not comm.is_dist:
+        return rows, cols
+    W = comm.world
+    dev = rows.device
+    inner = torch.tensor(cuts[1:-1], dtype=torch.int64, device=dev)
+    dest = torch.searchsorted(inner, rows, right=True)
+    order = torch.argsort(dest, stable=True)
+    send = torch.bincount(dest, minlength=W)
+    packed = torch.stack([rows[order], cols[order]], 1).reshape(-1)
+    del order, dest
+    wd = dev if comm.backend == "nccl" else torch.device("cpu")
+    send_w = send.to(wd)
+    recv_w = _alltoall_v(comm, send_w, [1] * W, [1] * W)
+    sn, rn = (2 * send_w).tolist(), (2 * recv_w).tolist()
+    got = _alltoall_v(comm, packed.to(wd), sn, rn).to(dev).view(-1, 2)
+    return got[:, 0].contiguous(), got[:, 1].contiguous()
+
+
+@dataclass
+class RmatProblem:
+    """BASELINE config 5 (R-MAT A.A^T) as a 1D row-block problem, built the
+    distributed way (reference: the rank-local work split and explicit
+    inter-rank transfers of sparse_matrix_mult.cu:437-553):
+
+    1. rank r generates its share of the edge chunks (chunk-seeded: the global
+       graph does not depend on P), relabelled by the common permutation;
+    2. row panels balanced on intermediate products: column degrees and the
+       per-row weight sum_{(i,j)} coldeg(j) (duplicate edges included) are
+       summed over ranks (two all-reduces of 2^scale entries);
+    3. edges go to their row owner (all-to-all-v), which builds its CSR row
+       panel A_r (duplicates merged, unit weights);
+    4. distributed transpose: every entry (i, j) of A_r goes as (j, i) to the
+       owner of row j of A^T (all-to-all-v), which builds its panel At_r;
+    5. each step all-gathers the At_r into the right operand A^T (as
+       :func:`rowblock_spgemm`) and multiplies its A_r by it."""
+
+    scale: int
+    edge_factor: int
+    seed: int
+    rows: Tuple[int, int]
+    cuts: List[int]
+    A: CSR
+    At: CSR
+
+    @staticmethod
+    def build(scale: int, edge_factor: int, comm: Comm, seed: int = 1, chunk: Optional[int] = None) -> "RmatProblem":
+        from ..utils import gen_csr
+
+        chunk = chunk or gen_csr.RMAT_CHUNK_EDGES
+        dev = comm.device
+        n = 1 << scale
+        k0, k1 = row_panels(rmat_nchunks(scale, edge_factor, chunk), comm.world)[comm.rank]
+        perm = rmat_perm(scale, seed, dev)
+        s, d, _ = rmat_edges(scale, edge_factor, seed=seed, device=dev, chunk=chunk, chunks=(k0, k1), perm=perm)
+        del perm
+        coldeg = _allreduce_sum_(comm, torch.bincount(d, minlength=n))
+        w = _allreduce_sum_(comm, torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, s, coldeg[d]))
+        del coldeg
+        panels = weighted_row_panels(torch.cumsum(w, 0), comm.world)
+        del w
+        cuts = [lo for lo, _ in panels] + [n]
+        lo, hi = panels[comm.rank]
+        rs, cs = shuffle_pairs(comm, s, d, cuts)
+        del s, d
+        A = pattern_csr(rs, cs, hi - lo, n, row0=lo)
+        del rs, cs
+        tj, ti = shuffle_pairs(comm, A.col.long(), A.row_ids() + lo, cuts)   # (j, i) to the owner of j
+        At = pattern_csr(tj, ti, hi - lo, n, row0=lo)
+        return RmatProblem(scale, edge_factor, seed, (lo, hi), cuts, A, At)
+
+    def right_operand(self, comm: Comm) -> CSR:
+        """A^T on every rank: the all-gather of the At_r panels."""
+        return allgather_operand(self.At, comm)
+
+    def step(self, comm: Comm, info: Optional[SpgemmInfo] = None,
+             consume: Optional[Callable[[int, int, CSR], None]] = None) -> Optional[CSR]:
+        """One product: C_r = A_r . A^T with A^T all-gathered inside the step.
+        Resident (returns C_r, the gather overlapping the row planning) or,
+        with ``consume``, streamed in row panels (returns None)."""
+        if consume is None:
+            return rowblock_spgemm(self.A, self.At, comm, info)
+        streamed_spgemm(self.A, self.right_operand(comm), consume, info=info)
+        return None
 
 
 def smoke(dev: torch.device) -> None:

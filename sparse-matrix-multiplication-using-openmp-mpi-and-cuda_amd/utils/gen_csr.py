@@ -12,7 +12,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ..ops.csr import CSR, from_coo, rowptr_from_rows
+from ..ops.csr import CSR, rowptr_from_rows
 
 CHUNK_ROWS = 65536
 
@@ -73,16 +73,37 @@ def uniform_csr(m: int, n: int, density: float, seed: int = 0, device="cpu", row
     return CSR(hi - lo, n, rowptr_from_rows(r, hi - lo), c, v)
 
 
+RMAT_CHUNK_EDGES = 1 << 22
+
+
+def rmat_nchunks(scale: int, edge_factor: int = 16, chunk: int = RMAT_CHUNK_EDGES) -> int:
+    return (edge_factor * (1 << scale) + chunk - 1) // chunk
+
+
+def rmat_perm(scale: int, seed: int = 0, device="cpu") -> torch.Tensor:
+    """The vertex relabelling of the R-MAT graph (same on every rank: one
+    fixed-seed generator)."""
+    return torch.randperm(1 << scale, generator=_gen(device, seed * 7919 + scale), device=device)
+
+
 def rmat_edges(scale: int, edge_factor: int = 16, a: float = 0.57, b: float = 0.19, c: float = 0.19,
-               seed: int = 0, device="cpu", permute: bool = True, chunk: int = 1 << 24):
-    """Graph500-style R-MAT edge list (src, dst) int64, 2^scale vertices."""
+               seed: int = 0, device="cpu", permute: bool = True, chunk: int = RMAT_CHUNK_EDGES,
+               chunks: Optional[Tuple[int, int]] = None, perm: Optional[torch.Tensor] = None):
+    """Graph500-style R-MAT edge list (src, dst) int64, 2^scale vertices.
+
+    The edges come in chunks of ``chunk`` with a generator seeded per chunk,
+    so ``chunks=(k0, k1)`` yields exactly those chunks of the global list:
+    P ranks that each generate a share of the chunks hold, together, the same
+    graph as one rank that generates all of them (any P, strong scaling)."""
     n = 1 << scale
     ne = edge_factor * n
-    g = _gen(device, seed * 7919 + scale)
+    nck = (ne + chunk - 1) // chunk
+    k0, k1 = chunks if chunks is not None else (0, nck)
     srcs, dsts = [], []
     ab, abc = a + b, a + b + c
-    for off in range(0, ne, chunk):
-        e = min(chunk, ne - off)
+    for k in range(max(k0, 0), min(k1, nck)):
+        g = _gen(device, (seed * 7919 + scale) * 1000003 + k + 1)
+        e = min(chunk, ne - k * chunk)
         s = torch.zeros(e, dtype=torch.int64, device=device)
         d = torch.zeros(e, dtype=torch.int64, device=device)
         for lvl in range(scale):
@@ -93,21 +114,25 @@ def rmat_edges(scale: int, edge_factor: int = 16, a: float = 0.57, b: float = 0.
             d |= db.to(torch.int64) << lvl
         srcs.append(s)
         dsts.append(d)
-    s = torch.cat(srcs)
-    d = torch.cat(dsts)
+    s = torch.cat(srcs) if srcs else torch.empty(0, dtype=torch.int64, device=device)
+    d = torch.cat(dsts) if dsts else torch.empty(0, dtype=torch.int64, device=device)
     if permute:
-        perm = torch.randperm(n, generator=g, device=device)
+        perm = perm if perm is not None else rmat_perm(scale, seed, device)
         s, d = perm[s], perm[d]
     return s, d, n
 
 
-def rmat_csr(scale: int, edge_factor: int = 16, seed: int = 0, device="cpu", dtype=torch.float32) -> CSR:
+def pattern_csr(s: torch.Tensor, d: torch.Tensor, m: int, n: int, row0: int = 0, dtype=torch.float32) -> CSR:
+    """Rows row0 .. row0 + m of the 0/1 pattern of the edges (s, d) (every s
+    in that range), duplicates merged, unit values."""
+    code = torch.unique((s - row0) * n + d)   # sorted, unique
+    r = torch.div(code, n, rounding_mode="floor")
+    col = (code - r * n).to(torch.int32)
+    return CSR(m, n, rowptr_from_rows(r, m), col, torch.ones(col.numel(), dtype=dtype, device=s.device))
+
+
+def rmat_csr(scale: int, edge_factor: int = 16, seed: int = 0, device="cpu", dtype=torch.float32,
+             chunk: int = RMAT_CHUNK_EDGES) -> CSR:
     """R-MAT adjacency matrix (duplicates merged, unit weights)."""
-    s, d, n = rmat_edges(scale, edge_factor, seed=seed, device=device)
-    M = from_coo(s, d, None, n, n, sum_duplicates=False, dtype=dtype)
-    # merge duplicates by dropping repeats (pattern graph)
-    code = M.row_ids() * n + M.col.long()
-    keep = torch.ones(code.shape[0], dtype=torch.bool, device=code.device)
-    keep[1:] = code[1:] != code[:-1]
-    r = M.row_ids()[keep]
-    return CSR(n, n, rowptr_from_rows(r, n), M.col[keep].contiguous(), M.val[keep].contiguous())
+    s, d, n = rmat_edges(scale, edge_factor, seed=seed, device=device, chunk=chunk)
+    return pattern_csr(s, d, n, n, dtype=dtype)

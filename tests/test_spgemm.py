@@ -660,3 +660,100 @@ def test_spgemm_bench_scale_sampled_rows(monkeypatch, n, d, ordered):
     assert err < 1e-6, err
     row_nnz = SG.symbolic(A, B, SG.row_nprod(A, B), SG.SpgemmInfo())
     assert torch.equal((C.rowptr[1:] - C.rowptr[:-1]).to(torch.int32), row_nnz)
+
+
+def _rmat_worker(rank, world, port, scale, ef, chunk, stream, tmp):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.parallel import comm as CM
+
+    comm = CM.init(backend="gloo", device="cpu", timeout_s=120)
+    try:
+        prob = MS.RmatProblem.build(scale, ef, comm, seed=5, chunk=chunk)
+        info = SG.SpgemmInfo()
+        if stream:
+            got = []
+            MS.streamed_spgemm(prob.A, prob.right_operand(comm), lambda lo, hi, C: got.append(C), budget=3000,
+                               info=info)
+            Cp = got[0] if len(got) == 1 else CS.CSR(prob.A.m, prob.A.n, *_cat_panels(got))
+        else:
+            Cp = prob.step(comm, info)
+        Ag = MS.gather_rows(prob.A, comm)
+        Atg = MS.gather_rows(prob.At, comm)
+        Cg = MS.gather_rows(Cp, comm)
+        flops = torch.tensor([info.flops], dtype=torch.int64)
+        if comm.is_dist:
+            torch.distributed.all_reduce(flops)
+        if rank == 0:
+            torch.save({"A": (Ag.rowptr, Ag.col), "At": (Atg.rowptr, Atg.col), "C": (Cg.rowptr, Cg.col, Cg.val),
+                        "flops": int(flops), "cuts": prob.cuts}, os.path.join(tmp, "rmat.pt"))
+    finally:
+        comm.close()
+
+
+def _cat_panels(panels):
+    rp = [torch.zeros(1, dtype=torch.int64)]
+    base = 0
+    for C in panels:
+        rp.append(C.rowptr[1:] + base)
+        base += C.nnz
+    return torch.cat(rp), torch.cat([C.col for C in panels]), torch.cat([C.val for C in panels])
+
+
+@pytest.mark.parametrize("world,stream", [(1, False), (4, False), (7, True), (8, False)])
+def test_rmat_distributed_gloo(tmp_path, world, stream):
+    """BASELINE config 5 the distributed way (chunked generation per rank,
+    product-balanced panels, all-to-all-v row shuffle, all-to-all-v
+    transpose, all-gathered A^T): at world 1, 4, 7 and 8 (7: streamed C
+    panels, uneven panels) the gathered A, A^T and C = A.A^T equal the
+    single-process product of the same graph, and the FLOPs summed over ranks
+    are the same."""
+    scale, ef, chunk = 9, 8, 256   # 16 edge chunks over the ranks
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_rmat_worker, args=(world, port, scale, ef, chunk, stream, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = torch.load(os.path.join(tmp_path, "rmat.pt"), weights_only=True)
+    n = 1 << scale
+    A = gen_csr.rmat_csr(scale, ef, seed=5, chunk=chunk)
+    assert torch.equal(got["A"][0], A.rowptr) and torch.equal(got["A"][1], A.col)
+    At = A.transpose()
+    assert torch.equal(got["At"][0], At.rowptr) and torch.equal(got["At"][1], At.col)
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, At, info)
+    assert got["flops"] == info.flops
+    assert torch.equal(got["C"][0], C.rowptr) and torch.equal(got["C"][1], C.col)
+    assert torch.allclose(got["C"][2], C.val)
+    cuts = got["cuts"]
+    assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == n and cuts == sorted(cuts)
+
+
+@pytest.mark.gpu
+def test_spgemm_gpu_rmat18_streamed_panels_match_resident():
+    """R-MAT scale-18 A.A^T streamed in row panels (a budget that forces
+    several panels, hub rows included) vs the resident product: every panel
+    equals the same rows of C (structure exact, values to fp32 rounding:
+    unit weights, so entries are exact integer counts)."""
+    from spmm_amd.models import spgemm as MS
+
+    dev = torch.device("cuda")
+    A = gen_csr.rmat_csr(18, 16, seed=4, device=dev)
+    At = A.transpose()
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, At, info)
+    budget = info.flops // 2 // 6 + 1
+    seen = []
+
+    def consume(lo, hi, Cp):
+        ref = C.row_slice(lo, hi)
+        assert Cp.m == hi - lo and torch.equal(Cp.rowptr, ref.rowptr) and torch.equal(Cp.col, ref.col), (lo, hi)
+        assert torch.equal(Cp.val, ref.val), (lo, hi)
+        seen.append((lo, hi))
+
+    sinfo = MS.streamed_spgemm(A, At, consume, budget=budget)
+    assert len(seen) >= 4 and seen[0][0] == 0 and seen[-1][1] == A.m
+    assert all(a[1] == b[0] for a, b in zip(seen, seen[1:]))
+    assert sinfo.flops == info.flops and sinfo.nnz == info.nnz == C.nnz
