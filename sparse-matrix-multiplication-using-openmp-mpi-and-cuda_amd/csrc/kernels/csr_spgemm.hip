@@ -990,8 +990,15 @@ __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict_
 //          column order over the chunk's region, count in rt_nnz
 //   place  chunk results copied to their final CSR positions
 // Traffic per product: 4 + 8 B of B reads, 8 B scratch write + 8 B read.
+#ifndef SPMM_LONG_EPW                   // (diagnostic builds: tools/bm_variants.py)
+#define SPMM_LONG_EPW 64
+#endif
+#ifndef SPMM_LONG_DLOADS
+#define SPMM_LONG_DLOADS 4
+#endif
 constexpr int LONG_NT = 512;
-constexpr int LONG_EPW = 64;            // A entries per routing workgroup
+constexpr int LONG_EPW = SPMM_LONG_EPW; // A entries per routing workgroup
+constexpr int LONG_DL = SPMM_LONG_DLOADS;   // scratch loads in flight per lane (long_dense)
 constexpr int LONG_LGW = 14;            // W = 16384 columns per chunk
 constexpr int LONG_W = 1 << LONG_LGW;
 constexpr int LONG_MAXCH = 4096;        // chunks per row (ncols <= 2^26)
@@ -1081,7 +1088,7 @@ template <bool VALUES>
 __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restrict__ rt_off,
                                                          const int64_t* __restrict__ rt_cnt, int64_t nrt, int nch,
                                                          unsigned long long* __restrict__ scratch,
-                                                         int64_t* __restrict__ rt_nnz) {
+                                                         int64_t* __restrict__ rt_nnz, int64_t small) {
   __shared__ float vals[VALUES ? LONG_W : 1];
   __shared__ uint32_t bits[LONG_W / 32];
   __shared__ int wsum[LONG_NT / 64];
@@ -1091,12 +1098,14 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
   bits[tid] = 0u;
   if constexpr (VALUES)
     for (int i = tid; i < LONG_W / 4; i += LONG_NT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // items of <= small products belong to long_rank (it runs first and writes their counts)
+  auto count_of = [&](int64_t r) { const int64_t c = rt_cnt[r]; return c <= small ? int64_t(0) : c; };
   int64_t rt = blockIdx.x;
   int64_t n = 0, base = 0;
-  if (rt < nrt) { n = rt_cnt[rt]; base = rt_off[rt]; }
-  unsigned long long x[4];
+  if (rt < nrt) { n = count_of(rt); base = rt_off[rt]; }
+  unsigned long long x[LONG_DL];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < LONG_DL; ++u) {
     const int64_t i = tid + u * LONG_NT;
     x[u] = i < n ? scratch[base + i] : ~0ull;
   }
@@ -1104,12 +1113,12 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
   while (rt < nrt) {
     const int64_t rt2 = rt + gridDim.x;
     if (n == 0) {   // uniform over the workgroup: no LDS state touched
-      if (tid == 0) rt_nnz[rt] = 0;
+      if (tid == 0 && small < 0) rt_nnz[rt] = 0;
       rt = rt2;
       n = 0;
-      if (rt < nrt) { n = rt_cnt[rt]; base = rt_off[rt]; }
+      if (rt < nrt) { n = count_of(rt); base = rt_off[rt]; }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < LONG_DL; ++u) {
         const int64_t i = tid + u * LONG_NT;
         x[u] = i < n ? scratch[base + i] : ~0ull;
       }
@@ -1118,24 +1127,24 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
     const int c0 = (int)(rt % nch) << LONG_LGW;
     for (int64_t i0 = tid;;) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < LONG_DL; ++u) {
         if (x[u] == ~0ull) continue;
         const int c = (int)(uint32_t)x[u] - c0;
         atomicOr(&bits[c >> 5], 1u << (c & 31));
         if constexpr (VALUES) atomicAdd(&vals[c], __uint_as_float((uint32_t)(x[u] >> 32)));
       }
-      i0 += 4 * LONG_NT;
+      i0 += LONG_DL * LONG_NT;
       if (i0 >= n) break;
-      // 4 scratch loads in flight per lane before the LDS updates
+      // LONG_DL scratch loads in flight per lane before the LDS updates
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < LONG_DL; ++u) {
         const int64_t i = i0 + u * LONG_NT;
         x[u] = i < n ? scratch[base + i] : ~0ull;
       }
     }
     __syncthreads();
     int64_t n2 = 0, base2 = 0;
-    if (rt2 < nrt) { n2 = rt_cnt[rt2]; base2 = rt_off[rt2]; }
+    if (rt2 < nrt) { n2 = count_of(rt2); base2 = rt_off[rt2]; }
     // one occupancy word per thread: its columns in order; the write-back
     // clears what it reads
     const uint32_t word = bits[tid];
@@ -1162,12 +1171,122 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
     }
     if (tid == 0) rt_nnz[rt] = total;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < LONG_DL; ++u) {
       const int64_t i = tid + u * LONG_NT;
       x[u] = i < n2 ? scratch[base2 + i] : ~0ull;
     }
     rt = rt2; n = n2; base = base2;
     __syncthreads();   // write-back clears and wsum reads done before the next item's atomics / wsum writes
+  }
+}
+
+// Wave-per-item long rows: most (row, chunk) items of an R-MAT hub row hold
+// a few hundred products, where long_dense's fixed per-item cost (three
+// workgroup barriers, a 512-word scan and write-back by 512 threads) dominates.
+// Here ONE WAVE owns an item of <= LR_CAP products and runs the bitmap-rank
+// scheme of csr_spgemm_bitmap.hip on it with no workgroup barrier:
+//   load the item's (column | a*b) words into registers (16 per lane);
+//   OR each column into the wave's 2 KB chunk bitmap (ds_or_rtn: the return
+//   marks duplicates); 16-bit rank prefix per 64-bit word (4 DPP scans);
+//   slot = prefix + popcount of the bits below; owners store their item,
+//   duplicates add after; write-back over the item's own scratch region
+//   (all its words are in registers by then), count to rt_nnz; the wave clears
+//   its bitmap and takes the next item (rt += waves in the grid).
+// LDS ops of one wave complete in issue order, so the phases only need the
+// compiler not to move LDS accesses across them (wave-scope fences).
+constexpr int LR_R = 16, LR_CAP = LR_R * 64, LR_WAVES = 4;
+constexpr int LR_WORDS = LONG_W / 64;   // 64-bit bitmap words per chunk
+static_assert(LR_WORDS % 64 == 0, "whole bitmap rows per lane");
+
+__device__ __forceinline__ void lr_wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool VALUES>
+__global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int64_t* __restrict__ rt_off,
+                                                           const int64_t* __restrict__ rt_cnt, int64_t nrt, int nch,
+                                                           unsigned long long* __restrict__ scratch,
+                                                           int64_t* __restrict__ rt_nnz) {
+  __shared__ __attribute__((aligned(16))) unsigned long long bm_all[LR_WAVES][LR_WORDS];
+  __shared__ __attribute__((aligned(16))) uint16_t pre_all[LR_WAVES][LR_WORDS];
+  __shared__ __attribute__((aligned(16))) unsigned long long it_all[VALUES ? LR_WAVES : 1][VALUES ? LR_CAP : 1];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  unsigned long long* const bm = bm_all[w];
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  uint16_t* const pre = pre_all[w];
+  unsigned long long* const it = it_all[VALUES ? w : 0];
+#pragma unroll
+  for (int k = 0; k < LR_WORDS / 64; ++k) bm[k * 64 + lane] = 0ull;
+  lr_wave_fence();
+  const int64_t nwv = (int64_t)gridDim.x * LR_WAVES;
+  for (int64_t rt = (int64_t)blockIdx.x * LR_WAVES + w; rt < nrt; rt += nwv) {
+    const int64_t n = rt_cnt[rt];
+    if (n > LR_CAP) continue;   // uniform: long_dense's item
+    if (n == 0) {
+      if (lane == 0) rt_nnz[rt] = 0;
+      continue;
+    }
+    const int64_t base = rt_off[rt];
+    const uint32_t c0 = (uint32_t)(rt % nch) << LONG_LGW;
+    const int nu = (int)((n + 63) >> 6);   // wave-uniform rounds
+    unsigned long long x[LR_R];
+#pragma unroll
+    for (int u = 0; u < LR_R; ++u) {   // unconditional issue: no per-load branch
+      const int64_t i = u * 64 + lane;
+      x[u] = ~0ull;
+      if (u < nu && i < n) x[u] = scratch[base + i];
+    }
+    uint32_t dupm = 0;
+    {
+      uint32_t old[LR_R];
+#pragma unroll
+      for (int u = 0; u < LR_R; ++u) {
+        old[u] = 0u;
+        if (x[u] != ~0ull) {
+          const uint32_t c = (uint32_t)x[u] - c0;
+          old[u] = atomicOr(bm32 + (c >> 5), 1u << (c & 31));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LR_R; ++u)
+        if (x[u] != ~0ull) dupm |= ((old[u] >> (((uint32_t)x[u] - c0) & 31)) & 1u) << u;
+    }
+    lr_wave_fence();
+    int run = 0;
+#pragma unroll
+    for (int k = 0; k < LR_WORDS / 64; ++k) {
+      const int cnt = __popcll(bm[k * 64 + lane]);
+      const int incl = wave_incl_scan_dpp(cnt);
+      pre[k * 64 + lane] = (uint16_t)(run + incl - cnt);
+      run += __builtin_amdgcn_readlane(incl, 63);
+    }
+    lr_wave_fence();
+    const int total = run;
+    if constexpr (VALUES) {
+      auto rank = [&](uint32_t c) {
+        const uint32_t wd = c >> 6;
+        return (int)pre[wd] + (int)__popcll(bm[wd] & ((1ull << (c & 63)) - 1ull));
+      };
+#pragma unroll
+      for (int u = 0; u < LR_R; ++u)
+        if (x[u] != ~0ull && !((dupm >> u) & 1u)) it[rank((uint32_t)x[u] - c0)] = x[u];
+      if (__ballot(dupm != 0)) {   // uniform
+        lr_wave_fence();
+#pragma unroll
+        for (int u = 0; u < LR_R; ++u)
+          if ((dupm >> u) & 1u)
+            atomicAdd(reinterpret_cast<float*>(&it[rank((uint32_t)x[u] - c0)]) + 1, __uint_as_float((uint32_t)(x[u] >> 32)));
+      }
+      lr_wave_fence();
+      for (int i = lane; i < total; i += 64) scratch[base + i] = it[i];
+    }
+    if (lane == 0) rt_nnz[rt] = total;
+#pragma unroll
+    for (int k = 0; k < LR_WORDS / 64; ++k) bm[k * 64 + lane] = 0ull;
+    lr_wave_fence();
   }
 }
 
@@ -1498,13 +1617,30 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
+  // items of <= LR_CAP products: one wave each (long_rank); the rest: long_dense
+  // (SPMM_LONG_RANK=0: every item on long_dense, for A/B runs)
+  static const int use_rank = [] {
+    const char* e = getenv("SPMM_LONG_RANK");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  const int64_t small = use_rank ? LR_CAP : -1;
+  if (use_rank) {
+    const unsigned rgrid = (unsigned)std::min<int64_t>((nrt + LR_WAVES - 1) / LR_WAVES, (values ? 3 : 8) * (int64_t)ncu);
+    if (values)
+      hipLaunchKernelGGL(long_rank<true>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rt_off, rt_cnt, nrt, nch,
+                         (unsigned long long*)scratch, rt_nnz);
+    else
+      hipLaunchKernelGGL(long_rank<false>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rt_off, rt_cnt, nrt, nch,
+                         (unsigned long long*)scratch, rt_nnz);
+    SPMM_LAUNCH_CHECK();
+  }
   const unsigned grid = (unsigned)std::min<int64_t>(nrt, (values ? 2 : 4) * (int64_t)ncu);
   if (values)
     hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nrt, nch,
-                       (unsigned long long*)scratch, rt_nnz);
+                       (unsigned long long*)scratch, rt_nnz, small);
   else
     hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nrt, nch,
-                       (unsigned long long*)scratch, rt_nnz);
+                       (unsigned long long*)scratch, rt_nnz, small);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

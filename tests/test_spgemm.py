@@ -757,3 +757,45 @@ def test_spgemm_gpu_rmat18_streamed_panels_match_resident():
     assert len(seen) >= 4 and seen[0][0] == 0 and seen[-1][1] == A.m
     assert all(a[1] == b[0] for a, b in zip(seen, seen[1:]))
     assert sinfo.flops == info.flops and sinfo.nnz == info.nnz == C.nnz
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("onepass", ["on", "off"])
+def test_spgemm_gpu_long_rows_wave_items(monkeypatch, onepass):
+    """Hub rows spread over 256 column chunks: items of a few hundred
+    products go to the wave-per-item kernel (long_rank), the heavy rows'
+    items (> 1024 products) to long_dense, in the same product; duplicates
+    within an item are summed and exact cancellations keep their entry."""
+    from spmm_amd.utils.config import CONFIG
+
+    k, n = 20000, 1 << 22
+    B = gen_csr.uniform_csr(k, n, 16 / n, seed=51, values="small_int")
+    rows, cols, vals = [], [], []
+    g = torch.Generator().manual_seed(5)
+    for r, na in enumerate([8000, 8000, 12000, 19000, 0, 9000]):   # ~128k .. ~300k products per hub row
+        if na:
+            rows.append(torch.full((na,), r))
+            cols.append(torch.randperm(k, generator=g)[:na])
+            vals.append(torch.randint(-2, 3, (na,), generator=g).float())
+    light = gen_csr.uniform_csr(40, k, 0.002, seed=52)   # ordinary rows around them
+    rows.append(light.row_ids() + 6)
+    cols.append(light.col.long())
+    vals.append(light.val)
+    A = CS.from_coo(torch.cat(rows), torch.cat(cols), torch.cat(vals), 46, k)
+    # one hub row made of two identical halves with opposite signs: exact 0 everywhere
+    cancel = torch.randperm(k // 2, generator=g)[:5000]
+    A2 = CS.from_coo(torch.cat([torch.cat(rows), torch.full((10000,), 46)]),
+                     torch.cat([torch.cat(cols), cancel, cancel + k // 2]),
+                     torch.cat([torch.cat(vals), torch.ones(5000), -torch.ones(5000)]), 47, k)
+    Bc = CS.from_coo(torch.cat([B.row_ids(), (B.row_ids() + k // 2) % k]), torch.cat([B.col, B.col]).long(),
+                     torch.cat([B.val, B.val]), k, n, sum_duplicates=True)
+    for Am, Bm in ((A, B), (A2, Bc)):
+        Cc = SG.spgemm(Am, Bm)
+        monkeypatch.setattr(CONFIG, "spgemm_onepass", onepass)
+        info = SG.SpgemmInfo()
+        dev = torch.device("cuda")
+        Cg = SG.spgemm(Am.to(dev), Bm.to(dev), info)
+        assert SG.NUM_GLOBAL in info.rows_per_bin_num
+        assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+        assert torch.equal(Cg.col.cpu(), Cc.col)
+        assert torch.equal(Cg.val.cpu(), Cc.val)   # small integers: every order sums exactly
