@@ -1,7 +1,8 @@
 """CSR SpGEMM / SpMM command line (north-star configs).
 
-    # C = A . B from Matrix Market files (one process, or torchrun/mpirun P ranks:
-    # 1D row-block, B all-gathered over RCCL, C gathered to rank 0 for output)
+    # C = A . B from Matrix Market files (one process, or torchrun P ranks: each
+    # rank parses 1/P of the files, 1D row-block, B all-gathered over RCCL, C
+    # streamed to rank 0 point-to-point and written as it arrives)
     python -m spmm_amd.apps.spgemm mult A.mtx B.mtx -o C.mtx
 
     # C = A . A^T  (e.g. R-MAT graphs)
@@ -30,49 +31,49 @@ def _sync(comm):
 
 
 def cmd_mult(args) -> int:
+    """Every rank parses 1/P of each input file and gets its row panel by an
+    all-to-all-v shuffle (``read_mtx_rowblock``); B (or A^T, by a distributed
+    transpose) is all-gathered inside the multiply; C's panels are streamed
+    to rank 0 point-to-point and appended to the output file as they arrive."""
     import torch
 
-    from ..models.spgemm import allgather_csr_rows, gather_rows
-    from ..ops.spgemm import SpgemmInfo, spgemm
+    from ..models import spgemm as MS
+    from ..ops.spgemm import SpgemmInfo
     from ..parallel import comm as CM
-    from ..parallel.partition import row_panels
-    from ..utils.mtx import read_mtx, write_mtx
 
     comm = CM.init(backend=args.comm, device=args.device)
     t0 = time.perf_counter()
-    A = read_mtx(args.a, device=comm.device)
-    B = A.transpose() if args.aat else read_mtx(args.b, device=comm.device)
-    lo, hi = row_panels(A.m, comm.world)[comm.rank]
-    Ap = A.row_slice(lo, hi)
-    blo, bhi = row_panels(B.m, comm.world)[comm.rank]
-    Bp = B.row_slice(blo, bhi)
-    del A, B
+    Ap, row0, cuts = MS.read_mtx_rowblock(args.a, comm)
+    if args.aat:
+        Bp, _ = MS.transpose_rowblock(Ap, row0, cuts[-1], comm)
+    else:
+        Bp, _, bcuts = MS.read_mtx_rowblock(args.b, comm)
+        if bcuts[-1] != Ap.n:
+            raise SystemExit(f"inner dimensions differ: A has {Ap.n} columns, B has {bcuts[-1]} rows")
     _sync(comm)
-    t_load = time.perf_counter() - t0
+    t_load = comm.allreduce_max(time.perf_counter() - t0)
     comm.barrier()
     t1 = time.perf_counter()
     info = SpgemmInfo()
-    Bfull = allgather_csr_rows(Bp, comm)
-    Cp = spgemm(Ap, Bfull, info)
+    Cp = MS.rowblock_spgemm(Ap, Bp, comm, info)
     _sync(comm)
     t_mult = comm.allreduce_max(time.perf_counter() - t1)
-    flops = info.flops
+    flops, nnz_c = info.flops, Cp.nnz
     if comm.is_dist:
         import torch.distributed as dist
 
-        t = torch.tensor([float(flops)], dtype=torch.float64,
+        t = torch.tensor([float(flops), float(nnz_c)], dtype=torch.float64,
                          device=comm.device if comm.backend == "nccl" else "cpu")
         dist.all_reduce(t)
-        flops = int(t.item())
-    C = gather_rows(Cp, comm) if args.output else None
+        flops, nnz_c = (int(x) for x in t.tolist())
     t2 = time.perf_counter()
-    if comm.rank == 0 and args.output:
-        write_mtx(args.output, C)
-    t_write = time.perf_counter() - t2
+    if args.output:
+        MS.write_rows_p2p(args.output, Cp, row0, comm)
+    t_write = comm.allreduce_max(time.perf_counter() - t2)
     if comm.rank == 0:
-        print(json.dumps(dict(op="spgemm", ranks=comm.world, device=str(comm.device), m=Ap.m if comm.world == 1 else None,
-                              nnz_C=(C.nnz if C is not None else None), flops=flops, t_load_s=t_load,
-                              t_mult_s=t_mult, t_write_s=t_write, gflops=flops / t_mult / 1e9 if t_mult > 0 else None)))
+        print(json.dumps(dict(op="spgemm", ranks=comm.world, device=str(comm.device), m=cuts[-1], n=Cp.n,
+                              nnz_C=nnz_c, flops=flops, t_load_s=t_load, t_mult_s=t_mult, t_write_s=t_write,
+                              gflops=flops / t_mult / 1e9 if t_mult > 0 else None)))
     comm.close()
     return 0
 

@@ -332,26 +332,145 @@ def _allreduce_sum_(comm: Comm, t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def shuffle_pairs(comm: Comm, rows: torch.Tensor, cols: torch.Tensor, cuts: List[int]) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Send every (row, col) pair to the rank that owns ``row`` (rank r owns
-    [cuts[r], cuts[r + 1])): one all-to-all-v of the counts, one of the
-    packed int64 pairs.  Returns the pairs this rank received (any order)."""
+def shuffle_entries(comm: Comm, rows: torch.Tensor, cols: torch.Tensor, vals: Optional[torch.Tensor],
+                    cuts: List[int]):
+    """Send every entry (row, col[, val]) to the rank that owns ``row`` (rank r
+    owns rows [cuts[r], cuts[r + 1])): one all-to-all-v of the counts, one of
+    the packed int64 records (float64 values travel as their bit patterns).
+    Returns the (rows, cols, vals) this rank received, in rank order."""
     if not comm.is_dist:
-        return rows, cols
+        return rows, cols, vals
     W = comm.world
     dev = rows.device
     inner = torch.tensor(cuts[1:-1], dtype=torch.int64, device=dev)
     dest = torch.searchsorted(inner, rows, right=True)
     order = torch.argsort(dest, stable=True)
     send = torch.bincount(dest, minlength=W)
-    packed = torch.stack([rows[order], cols[order]], 1).reshape(-1)
-    del order, dest
+    fields = [rows[order], cols[order]]
+    if vals is not None:
+        fields.append(vals.to(torch.float64)[order].view(torch.int64))
+    k = len(fields)
+    packed = torch.stack(fields, 1).reshape(-1)
+    del order, dest, fields
     wd = dev if comm.backend == "nccl" else torch.device("cpu")
     send_w = send.to(wd)
     recv_w = _alltoall_v(comm, send_w, [1] * W, [1] * W)
-    sn, rn = (2 * send_w).tolist(), (2 * recv_w).tolist()
-    got = _alltoall_v(comm, packed.to(wd), sn, rn).to(dev).view(-1, 2)
-    return got[:, 0].contiguous(), got[:, 1].contiguous()
+    got = _alltoall_v(comm, packed.to(wd), (k * send_w).tolist(), (k * recv_w).tolist()).to(dev).view(-1, k)
+    return got[:, 0].contiguous(), got[:, 1].contiguous(), (got[:, 2].contiguous().view(torch.float64)
+                                                             if vals is not None else None)
+
+
+def shuffle_pairs(comm: Comm, rows: torch.Tensor, cols: torch.Tensor, cuts: List[int]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """:func:`shuffle_entries` of a 0/1 pattern."""
+    r, c, _ = shuffle_entries(comm, rows, cols, None, cuts)
+    return r, c
+
+
+def read_mtx_rowblock(path: str, comm: Comm, dtype=torch.float32) -> Tuple[CSR, int, List[int]]:
+    """This rank's row panel of a Matrix Market file (row_panels split): every
+    rank parses 1/P of the file's text, the entries go to their row owners
+    (all-to-all-v) and each owner sums duplicates into its CSR panel — no rank
+    reads or holds the whole matrix (reference: rank-local loading of its
+    share of the chain, sparse_matrix_mult.cu:437-456).  Returns (panel,
+    its first row, the panel cuts of every rank)."""
+    from ..ops.csr import from_coo
+    from ..utils.mtx import read_mtx_coo
+
+    m, n, ri, ci, v = read_mtx_coo(path, comm.rank, comm.world)
+    cuts = [lo for lo, _ in row_panels(m, comm.world)] + [m]
+    dev = comm.device
+    ri, ci, v = shuffle_entries(comm, ri.to(dev), ci.to(dev), v.to(dev), cuts)
+    lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
+    A = from_coo(ri - lo, ci, v, hi - lo, n, sum_duplicates=True, dtype=dtype)
+    return A, lo, cuts
+
+
+def transpose_rowblock(panel: CSR, row0: int, m_total: int, comm: Comm) -> Tuple[CSR, int]:
+    """This rank's row panel of A^T (row_panels split of A's columns) from
+    the row panels of A: every entry (i, j, v) goes as (j, i, v) to the owner
+    of row j of A^T (all-to-all-v).  Returns (panel, its first row)."""
+    from ..ops.csr import from_coo
+
+    tcuts = [lo for lo, _ in row_panels(panel.n, comm.world)] + [panel.n]
+    tj, ti, tv = shuffle_entries(comm, panel.col.long(), panel.row_ids() + row0, panel.val, tcuts)
+    lo, hi = tcuts[comm.rank], tcuts[comm.rank + 1]
+    return from_coo(tj - lo, ti, tv, hi - lo, m_total, sum_duplicates=True, dtype=panel.val.dtype), lo
+
+
+def write_rows_p2p(path: str, panel: CSR, row0: int, comm: Comm, dst: int = 0, pattern: bool = False) -> None:
+    """Write a row-distributed CSR (rank r holds rows row0_r .. in rank order)
+    as one Matrix Market file on rank ``dst``: the total nnz and row count
+    are summed first (header), then ``dst`` receives the panels point-to-point
+    in rank order and appends each as it arrives — C is never all-gathered or
+    held whole anywhere (reference: partials sent to rank 0, which writes
+    ``matrix``, sparse_matrix_mult.cu:466-607)."""
+    from ..utils.mtx import MtxWriter
+
+    wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
+    tot = torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)
+    if comm.is_dist:
+        dist.all_reduce(tot)
+    m_tot, nnz_tot = (int(x) for x in tot.tolist())
+    if comm.rank != dst:
+        hdr = torch.tensor([row0, panel.m, panel.nnz], dtype=torch.int64, device=wd)
+        dist.send(hdr, dst)
+        if panel.m:
+            dist.send((panel.rowptr[1:] - panel.rowptr[:-1]).to(wd).contiguous(), dst)
+        if panel.nnz:
+            dist.send(panel.col.to(wd).contiguous(), dst)
+            if not pattern:
+                dist.send(panel.val.float().to(wd).contiguous(), dst)
+        return
+    w = MtxWriter(path, m_tot, panel.n, nnz_tot, pattern)
+    try:
+        for r in range(comm.world):
+            if r == dst:
+                w.panel(row0, panel)
+                continue
+            hdr = torch.empty(3, dtype=torch.int64, device=wd)
+            dist.recv(hdr, r)
+            r0, mp, nz = (int(x) for x in hdr.tolist())
+            cnt = torch.zeros(mp, dtype=torch.int64, device=wd)
+            col = torch.empty(nz, dtype=torch.int32, device=wd)
+            val = torch.empty(0 if pattern else nz, dtype=torch.float32, device=wd)
+            if mp:
+                dist.recv(cnt, r)
+            if nz:
+                dist.recv(col, r)
+                if not pattern:
+                    dist.recv(val, r)
+            rp = torch.zeros(mp + 1, dtype=torch.int64)
+            torch.cumsum(cnt.cpu(), 0, out=rp[1:])
+            w.panel(r0, CSR(mp, panel.n, rp, col.cpu(), val.cpu()))
+    finally:
+        w.close()
+
+
+def csr_chain(paths: List[str], comm: Comm, out_path: Optional[str] = None,
+              log: Optional[Callable[[str], None]] = None, info: Optional[SpgemmInfo] = None) -> Tuple[CSR, int]:
+    """Ordered product M_1 . M_2 . ... . M_N of Matrix Market files on the CSR
+    engine (fp32), the CSR counterpart of the reference's chain
+    (sparse_matrix_mult.cu:402-681): the running product stays distributed in
+    row panels, every next factor is read 1/P per rank and all-gathered inside
+    the row-block multiply, and the result is streamed to rank 0 for writing.
+    ``log`` gets the reference's "multiplying i i+1" line per product (rank 0).
+    Returns (this rank's row panel of the product, its first row)."""
+    if not paths:
+        raise ValueError("empty chain")
+    panel, row0, _ = read_mtx_rowblock(paths[0], comm)
+    for i, path in enumerate(paths[1:], start=1):
+        if log is not None and comm.rank == 0:
+            log(f"multiplying {i} {i + 1}")
+        Bp, _, bcuts = read_mtx_rowblock(path, comm)
+        if bcuts[-1] != panel.n:
+            raise ValueError(f"{path}: {bcuts[-1]} rows, the product so far has {panel.n} columns")
+        pi = SpgemmInfo()
+        panel = rowblock_spgemm(panel, Bp, comm, pi)
+        if info is not None:
+            info.flops += pi.flops
+    if out_path:
+        write_rows_p2p(out_path, panel, row0, comm)
+    return panel, row0
 
 
 @dataclass

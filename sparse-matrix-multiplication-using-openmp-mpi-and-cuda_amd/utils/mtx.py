@@ -19,7 +19,7 @@ class MtxError(RuntimeError):
     pass
 
 
-def read_mtx(path: str, device="cpu", dtype=torch.float32, nthreads: int = 0) -> CSR:
+def _open(path: str):
     lib = _native.host()
     err = C.create_string_buffer(512)
     m, n, nnz = C.c_int64(), C.c_int64(), C.c_int64()
@@ -28,29 +28,83 @@ def read_mtx(path: str, device="cpu", dtype=torch.float32, nthreads: int = 0) ->
                           err, 512)
     if not h:
         raise MtxError(f"{path}: {err.value.decode()}")
+    return h, m.value, n.value, nnz.value, field.value, sym.value
+
+
+def read_mtx_coo(path: str, part: int = 0, nparts: int = 1, nthreads: int = 0):
+    """Entries of part ``part`` of ``nparts`` of the file (line-aligned byte
+    ranges of the entry section: a distributed read parses 1/nparts of the
+    text per rank), symmetric storage expanded.  Returns (m, n, rows, cols,
+    values) as int64 / int64 / float64 host tensors, 0-based, any order."""
+    lib = _native.host()
+    h, m, n, nnz, field, sym = _open(path)
     try:
-        ri = torch.empty(nnz.value, dtype=torch.int64)
-        ci = torch.empty(nnz.value, dtype=torch.int64)
-        v = torch.empty(nnz.value, dtype=torch.float64)
-        if nnz.value and lib.spmm_mtx_fill(h, ri.data_ptr(), ci.data_ptr(), v.data_ptr(), nthreads, err, 512) != 0:
-            raise MtxError(f"{path}: {err.value.decode()}")
+        if nparts == 1:
+            ne = nnz
+            ri = torch.empty(ne, dtype=torch.int64)
+            ci = torch.empty(ne, dtype=torch.int64)
+            v = torch.empty(ne, dtype=torch.float64)
+            err = C.create_string_buffer(512)
+            if ne and lib.spmm_mtx_fill(h, ri.data_ptr(), ci.data_ptr(), v.data_ptr(), nthreads, err, 512) != 0:
+                raise MtxError(f"{path}: {err.value.decode()}")
+        else:
+            b0, b1, ne_ = C.c_int64(), C.c_int64(), C.c_int64()
+            if lib.spmm_mtx_part(h, part, nparts, C.byref(b0), C.byref(b1), C.byref(ne_), nthreads) != 0:
+                raise MtxError(f"{path}: part {part}/{nparts} does not hold whole entries")
+            ne = ne_.value
+            ri = torch.empty(ne, dtype=torch.int64)
+            ci = torch.empty(ne, dtype=torch.int64)
+            v = torch.ones(ne, dtype=torch.float64)
+            if ne:
+                lib.spmm_mtx_fill_part(h, b0.value, b1.value, ri.data_ptr(), ci.data_ptr(), v.data_ptr(), nthreads)
     finally:
         lib.spmm_mtx_close(h)
-    if nnz.value and (int(ri.min()) < 0 or int(ri.max()) >= m.value or int(ci.min()) < 0 or int(ci.max()) >= n.value):
+    if ne and (int(ri.min()) < 0 or int(ri.max()) >= m or int(ci.min()) < 0 or int(ci.max()) >= n):
         raise MtxError(f"{path}: coordinates out of range")
-    if sym.value in (1, 2, 3):
+    if sym in (1, 2, 3):
         off = ri != ci
-        sign = -1.0 if sym.value == 2 else 1.0
+        sign = -1.0 if sym == 2 else 1.0
         ri, ci, v = torch.cat([ri, ci[off]]), torch.cat([ci, ri[off]]), torch.cat([v, sign * v[off]])
-    M = from_coo(ri.to(device), ci.to(device), v.to(device), m.value, n.value, sum_duplicates=True, dtype=dtype)
-    return M
+    return m, n, ri, ci, v
+
+
+def read_mtx(path: str, device="cpu", dtype=torch.float32, nthreads: int = 0) -> CSR:
+    m, n, ri, ci, v = read_mtx_coo(path, nthreads=nthreads)
+    return from_coo(ri.to(device), ci.to(device), v.to(device), m, n, sum_duplicates=True, dtype=dtype)
+
+
+class MtxWriter:
+    """Streaming coordinate-file writer: the header (total nnz known up
+    front), then row panels appended in row order (``write_rows_p2p`` feeds
+    it one received panel of C at a time), then ``close``.  The bytes are the
+    same for any split of the matrix into panels."""
+
+    def __init__(self, path: str, m: int, n: int, nnz: int, pattern: bool = False, nthreads: int = 0):
+        self.path, self.pattern, self.nthreads = path, pattern, nthreads
+        self.h = _native.host().spmm_mtx_write_begin(path.encode(), m, n, nnz, int(pattern))
+        if not self.h:
+            raise OSError(f"cannot open {path} for writing")
+
+    def panel(self, row0: int, M: CSR) -> None:
+        rp = M.rowptr.to("cpu", torch.int64).contiguous()
+        ci = M.col.to("cpu", torch.int32).contiguous()
+        vals = None if self.pattern else M.val.to("cpu", torch.float32).contiguous()
+        rc = _native.host().spmm_mtx_write_panel(self.h, row0, M.m, rp.data_ptr(), ci.data_ptr(),
+                                                  vals.data_ptr() if vals is not None else None, self.nthreads)
+        if rc != 0:
+            raise OSError(-rc, f"writing {self.path} failed")
+
+    def close(self) -> None:
+        if self.h:
+            rc = _native.host().spmm_mtx_write_end(self.h)
+            self.h = None
+            if rc != 0:
+                raise OSError(-rc, f"writing {self.path} failed")
 
 
 def write_mtx(path: str, M: CSR, pattern: bool = False, nthreads: int = 0) -> None:
-    rp = M.rowptr.to("cpu", torch.int64).contiguous()
-    ci = M.col.to("cpu", torch.int32).contiguous()
-    vals = None if pattern else M.val.to("cpu", torch.float32).contiguous()
-    rc = _native.host().spmm_mtx_write(path.encode(), M.m, M.n, rp.data_ptr(), ci.data_ptr(),
-                                        vals.data_ptr() if vals is not None else None, nthreads)
-    if rc != 0:
-        raise OSError(-rc, f"writing {path} failed")
+    w = MtxWriter(path, M.m, M.n, M.nnz, pattern, nthreads)
+    try:
+        w.panel(0, M)
+    finally:
+        w.close()

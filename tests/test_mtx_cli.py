@@ -59,3 +59,82 @@ def test_spgemm_cli_plumbing_config(tmp_path):
     ref = A.to_dense().double() @ B.to_dense().double()
     assert torch.allclose(C.to_dense().double(), ref, atol=1e-5)
     assert rec["flops"] > 0 and rec["nnz_C"] == C.nnz
+
+
+def _shuffled_mtx(path, M, seed, symmetric=False):
+    """Write M as a coordinate file with its entries in random line order
+    (symmetric: the lower triangle of M + M^T with symmetric storage)."""
+    r, c, v = M.row_ids(), M.col.long(), M.val.double()
+    if symmetric:
+        keep = r >= c
+        r, c, v = r[keep], c[keep], v[keep]
+    p = torch.randperm(r.numel(), generator=torch.Generator().manual_seed(seed))
+    kind = "symmetric" if symmetric else "general"
+    lines = [f"%%MatrixMarket matrix coordinate real {kind}", f"{M.m} {M.n} {r.numel()}"]
+    lines += [f"{int(r[i]) + 1} {int(c[i]) + 1} {float(v[i])!r}" for i in p.tolist()]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+@pytest.mark.parametrize("mode", ["ab", "aat", "sym"])
+def test_spgemm_cli_four_ranks_byte_identical(tmp_path, mode):
+    """``apps.spgemm mult -o`` on 4 gloo ranks (each rank parses a quarter of
+    every input file, entries shuffled to their row owners, C streamed to rank
+    0 point-to-point) writes the same bytes as the 1-rank run; inputs with
+    random line order, duplicate-free general and symmetric storage."""
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    A = gen_csr.uniform_csr(700, 500, 0.02, seed=3)
+    B = gen_csr.uniform_csr(500, 900, 0.02, seed=4)
+    a, b = str(tmp_path / "A.mtx"), str(tmp_path / "B.mtx")
+    if mode == "sym":
+        S = gen_csr.uniform_csr(600, 600, 0.02, seed=5)
+        _shuffled_mtx(a, S, 1, symmetric=True)
+        _shuffled_mtx(b, S, 2, symmetric=True)
+    else:
+        _shuffled_mtx(a, A, 1)
+        _shuffled_mtx(b, B, 2)
+    out = {}
+    for world in (1, 4):
+        c = str(tmp_path / f"C{world}.mtx")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={29650 + world + 10 * ['ab', 'aat', 'sym'].index(mode)}",
+               "-m", "spmm_amd.apps.spgemm", "mult", a] + (["--aat"] if mode == "aat" else [b]) + \
+              ["-o", c, "--device", "cpu", "--comm", "gloo"]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[world] = (json.loads(r.stdout.strip().splitlines()[-1]), open(c, "rb").read())
+    assert out[1][1] == out[4][1]
+    assert out[4][0]["ranks"] == 4 and out[1][0]["flops"] == out[4][0]["flops"]
+    Am = mtx.read_mtx(a)
+    Bm = Am.transpose() if mode == "aat" else mtx.read_mtx(b)
+    C = mtx.read_mtx(str(tmp_path / "C4.mtx"))
+    assert torch.allclose(C.to_dense().double(), Am.to_dense().double() @ Bm.to_dense().double(), atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_a4_format_mtx_chain(tmp_path, world):
+    """One command line for both workloads: ``a4 --format mtx`` multiplies a
+    chain of Matrix Market files on the CSR engine (1 and 3 gloo ranks, a
+    folder of naturally ordered files), prints the reference's stdout lines
+    and writes the product."""
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    d = tmp_path / "chain"
+    d.mkdir()
+    dims = [300, 250, 280, 260, 310]
+    mats = [gen_csr.uniform_csr(dims[i], dims[i + 1], 0.03, seed=10 + i) for i in range(4)]
+    for i, M in enumerate(mats):
+        mtx.write_mtx(str(d / f"m{i + 1}.mtx"), M)
+    out = str(tmp_path / f"P{world}.mtx")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={29690 + world}", "-m", "spmm_amd.apps.a4", "--format", "mtx",
+           str(d), "--out", out, "--device", "cpu", "--comm", "gloo"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert [x for x in lines if x.startswith("multiplying")] == ["multiplying 1 2", "multiplying 2 3", "multiplying 3 4"]
+    assert sum(x.startswith("time taken ") for x in lines) == world
+    ref = mats[0].to_dense().double()
+    for M in mats[1:]:
+        ref = ref @ M.to_dense().double()
+    got = mtx.read_mtx(out).to_dense().double()
+    assert got.shape == ref.shape and torch.allclose(got, ref, atol=1e-4)
