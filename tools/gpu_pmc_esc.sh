@@ -9,7 +9,7 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 pass() {  # name, counters...
   echo "== $1"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc "${@:2}" -d ${PMC_DIR:-$O}/$1 -o pmc --output-format csv -- python3 $R/bench.py --workload ${WL:-spgemm} --steps 1 --warmup 0 > $O/$1.log 2>&1 || { tail -20 $O/$1.log; return 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace ${KREGEX:+--kernel-include-regex "$KREGEX"} --pmc "${@:2}" -d ${PMC_DIR:-$O}/$1 -o pmc --output-format csv -- python3 $R/bench.py --workload ${WL:-spgemm} --steps 1 --warmup 0 ${BENCH_ARGS} > $O/$1.log 2>&1 || { tail -20 $O/$1.log; return 1; }
 }
 PASSES=${PASSES:-pmcA pmcB pmcC pmcD}
 declare -A CTR=(
