@@ -19,6 +19,13 @@ is timed by this script's own clock around the subprocess, and the program's
 metrics are reported.
 
     python benches/bench_a4_e2e.py --preset medium [--p 1] [--device hip|cpu]
+
+Several runs over the same generated input (comma lists, cartesian product):
+the CPU-only column of report Table 1 and the thread scaling of Table 3
+(1 rank, 100k tiles, 4 / 8 / 16 / 32 threads) come from
+
+    python benches/bench_a4_e2e.py --preset medium --device hip,cpu
+    python benches/bench_a4_e2e.py --preset medium --device cpu --threads 4,8,16,32
 """
 from __future__ import annotations
 
@@ -69,8 +76,10 @@ def generate(folder: str, preset: str, seed: int, k: int = 32) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", choices=sorted(REPORT), default="medium")
-    ap.add_argument("--p", type=int, default=1, help="MPI ranks (one GPU each when GPUs are visible)")
-    ap.add_argument("--device", default="auto", choices=["auto", "hip", "cpu"])
+    ap.add_argument("--p", default="1", help="MPI ranks (one GPU each when GPUs are visible); comma list")
+    ap.add_argument("--device", default="auto", help="auto / hip / cpu; comma list")
+    ap.add_argument("--threads", default="0", help="a4 --threads (host parser/writer/CPU-engine threads; 0 = all); "
+                    "comma list")
     ap.add_argument("--comm", default="auto")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--workdir", default=None, help="where the input folder goes (default: a temp dir)")
@@ -92,31 +101,36 @@ def main() -> None:
         t0 = time.perf_counter()
         info = generate(folder, a.preset, a.seed)
         t_gen = time.perf_counter() - t0
-        out = os.path.join(work, "matrix")
-        met = os.path.join(work, "m.json")
-        cmd = [mpiexec, "-n", str(a.p), a4, folder, "--quiet", "--out", out, "--metrics-json", met,
-               "--device", a.device, "--comm", a.comm]
-        if a.streams is not None:
-            cmd += ["--streams", str(a.streams)]
-        t0 = time.perf_counter()
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout)
-        wall = time.perf_counter() - t0
-        if r.returncode != 0:
-            sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
-            raise SystemExit(f"a4 failed with {r.returncode}")
-        taken = max(float(x) for x in re.findall(r"time taken ([0-9.eE+-]+) seconds", r.stdout))
-        m = json.load(open(met))
-        tiles_ref, t_opt, t_cpu = REPORT[a.preset]
-        rec = dict(metric="a4 end-to-end wall-clock (report.pdf Table 1)", preset=a.preset, ranks=a.p, streams=a.streams,
-                   device=m.get("device"), comm=m.get("comm"), value=round(taken, 3), unit="s",
-                   higher_is_better=False, wall_s_outer=round(wall, 3), report_tiles=tiles_ref,
-                   report_optimized_s=t_opt, report_cpu_only_s=t_cpu,
-                   speedup_vs_report=round(t_opt / taken, 2), output_bytes=os.path.getsize(out),
-                   gen_s=round(t_gen, 2), **info, phases=m)
-        print(json.dumps(rec), flush=True)
+        runs = [(d, int(p), int(t)) for d in a.device.split(",") for p in a.p.split(",") for t in a.threads.split(",")]
+        recs = []
+        for dev, nranks, threads in runs:
+            out = os.path.join(work, "matrix")
+            met = os.path.join(work, "m.json")
+            cmd = [mpiexec, "-n", str(nranks), a4, folder, "--quiet", "--out", out, "--metrics-json", met,
+                   "--device", dev, "--comm", a.comm, "--threads", str(threads)]
+            if a.streams is not None:
+                cmd += ["--streams", str(a.streams)]
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout)
+            wall = time.perf_counter() - t0
+            if r.returncode != 0:
+                sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
+                raise SystemExit(f"a4 failed with {r.returncode}")
+            taken = max(float(x) for x in re.findall(r"time taken ([0-9.eE+-]+) seconds", r.stdout))
+            m = json.load(open(met))
+            tiles_ref, t_opt, t_cpu = REPORT[a.preset]
+            rec = dict(metric="a4 end-to-end wall-clock (report.pdf Table 1)", preset=a.preset, ranks=nranks,
+                       threads=m.get("threads", threads), streams=a.streams, device=m.get("device"), comm=m.get("comm"),
+                       value=round(taken, 3), unit="s", higher_is_better=False, wall_s_outer=round(wall, 3),
+                       report_tiles=tiles_ref, report_optimized_s=t_opt, report_cpu_only_s=t_cpu,
+                       speedup_vs_report=round(t_opt / taken, 2),
+                       speedup_vs_report_cpu_only=round(t_cpu / taken, 2), output_bytes=os.path.getsize(out),
+                       gen_s=round(t_gen, 2), **info, metrics=m)
+            print(json.dumps(rec), flush=True)
+            recs.append(rec)
         if a.json:
             with open(a.json, "w") as f:
-                json.dump(rec, f, indent=1)
+                json.dump(recs if len(recs) > 1 else recs[0], f, indent=1)
     finally:
         if not a.keep:
             shutil.rmtree(work, ignore_errors=True)

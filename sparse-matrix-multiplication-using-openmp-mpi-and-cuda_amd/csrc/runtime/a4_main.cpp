@@ -227,11 +227,45 @@ Node make_node(DevMat&& M, hipStream_t s) {
   return n;
 }
 
+// Phase accounting for --metrics-json, the breakdown of report.pdf Table 2
+// (pack / H2D / kernel / D2H / MPI, timers at sparse_matrix_mult.cu:160-274).
+// Host phases are wall-clock sums; H2D and kernel time are device time from
+// HIP event pairs on the upload and product streams, summed after the final
+// device synchronisation.  Phases overlap (parsing runs on the loader thread
+// while earlier products run on the pool streams), so their sum exceeds
+// t_reduce; the ratio is reported as the overlap factor.
 struct Stats {
   int64_t products = 0, tile_pairs = 0;
   double t_load = 0, t_reduce = 0, t_comm = 0, t_write = 0;
+  double t_parse = 0, t_kernel_cpu = 0, t_p2p = 0, t_d2h = 0, t_prune = 0, t_format = 0;
   size_t bytes_h2d = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_h2d, ev_kernel;
   std::mutex mu;
+  void add(double& acc, double dt) {
+    std::lock_guard<std::mutex> g(mu);
+    acc += dt;
+  }
+  // (start, stop) timing events; record start now, the caller records stop
+  std::pair<hipEvent_t, hipEvent_t> begin(std::vector<std::pair<hipEvent_t, hipEvent_t>>& list, hipStream_t s) {
+    std::pair<hipEvent_t, hipEvent_t> e;
+    A4_HIP(hipEventCreate(&e.first));
+    A4_HIP(hipEventCreate(&e.second));
+    A4_HIP(hipEventRecord(e.first, s));
+    std::lock_guard<std::mutex> g(mu);
+    list.push_back(e);
+    return e;
+  }
+  static double drain(std::vector<std::pair<hipEvent_t, hipEvent_t>>& list) {   // after a device sync
+    double ms = 0;
+    for (auto& e : list) {
+      float t = 0;
+      if (hipEventElapsedTime(&t, e.first, e.second) == hipSuccess) ms += t;
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    list.clear();
+    return ms / 1e3;
+  }
 };
 
 // Page-locked staging slot: a file is parsed straight into it and DMA'd from
@@ -272,7 +306,9 @@ struct PinnedSlot {
 // Parse matrix file `path` into `slot` and upload it on `s` (GPU loader).
 // Files whose tiles are not already sorted and unique take the canonicalising
 // host path.
-Node load_pinned(const Options& o, const std::string& path, int k, PinnedSlot& slot, hipStream_t s, size_t* bytes) {
+Node load_pinned(const Options& o, const std::string& path, int k, PinnedSlot& slot, hipStream_t s, size_t* bytes,
+                 Stats& st) {
+  const double tp0 = now_s();
   char err[512] = {0};
   int64_t rows = 0, cols = 0, blocks = 0;
   void* h = spmm_ref_open(path.c_str(), k, &rows, &cols, &blocks, err, sizeof err);
@@ -285,6 +321,7 @@ Node load_pinned(const Options& o, const std::string& path, int k, PinnedSlot& s
   bool canonical = true;
   for (int64_t b = 1; b < blocks && canonical; ++b)
     canonical = encode_key(slot.keys[2 * b - 2], slot.keys[2 * b - 1]) < encode_key(slot.keys[2 * b], slot.keys[2 * b + 1]);
+  st.add(st.t_parse, now_s() - tp0);
   if (!canonical || o.dump) {
     Mat M;
     M.rows = rows; M.cols = cols; M.k = k;
@@ -302,8 +339,10 @@ Node load_pinned(const Options& o, const std::string& path, int k, PinnedSlot& s
   D.keys = DevBuf<int32_t>((size_t)blocks * 2, s);
   D.vals = DevBuf<uint64_t>((size_t)(blocks * kk), s);
   if (blocks) {
+    const auto ev = st.begin(st.ev_h2d, s);
     A4_HIP(hipMemcpyAsync(D.keys.get(), slot.keys, (size_t)blocks * 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
     A4_HIP(hipMemcpyAsync(D.vals.get(), slot.vals, (size_t)(blocks * kk) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    A4_HIP(hipEventRecord(ev.second, s));
   }
   if (!slot.done) A4_HIP(hipEventCreateWithFlags(&slot.done, hipEventDisableTiming));
   A4_HIP(hipEventRecord(slot.done, s));
@@ -328,14 +367,16 @@ class Loader {
           const std::string path = o.folder + "/matrix" + std::to_string(i + 1);
           if constexpr (std::is_same<T, Node>::value) {
             size_t bytes = 0;
-            Node n = load_pinned(o, path, k, slots[(i - lo) & 1], s, &bytes);
+            Node n = load_pinned(o, path, k, slots[(i - lo) & 1], s, &bytes, st);
             {
               std::lock_guard<std::mutex> g(st.mu);
               st.bytes_h2d += bytes;
             }
             push(std::move(n));
           } else {
+            const double tp0 = now_s();
             Mat M = read_ref(path, k, o.threads);
+            st.add(st.t_parse, now_s() - tp0);
             if (o.dump) dump("matrix" + std::to_string(i + 1), M);
             push(std::move(M));
           }
@@ -392,7 +433,9 @@ std::future<Node> gpu_product(Pool& pool, std::shared_future<Node> fa, std::shar
     A4_HIP(hipStreamWaitEvent(s, b.ev, 0));
     int64_t pairs = 0;
     Range r("multiply");
+    const auto ev = st.begin(st.ev_kernel, s);
     DevMat C = dev_multiply(*a.m, *b.m, s, &pairs);
+    A4_HIP(hipEventRecord(ev.second, s));
     // operands die on this stream, after the product's kernels; the product
     // is drained first so a later free never races a pending kernel
     a.m->keys.retarget(s); a.m->vals.retarget(s);
@@ -443,7 +486,9 @@ Mat cpu_reduce_local(const Options& o, int lo, int hi, int k, Stats& st) {
   const int n = hi - lo + 1;
   auto mul = [&](const Mat& a, const Mat& b) {
     int64_t pairs = 0;
+    const double tk = now_s();
     Mat c = cpu_multiply(a, b, o.threads, &pairs);
+    st.add(st.t_kernel_cpu, now_s() - tk);
     st.products += 1;
     st.tile_pairs += pairs;
     return c;
@@ -474,13 +519,30 @@ struct GpuOps {
   using M = DevMat;
   hipStream_t s;
   Comm* comm;
-  M mul(const M& a, const M& b, int64_t* pairs) { return dev_multiply(a, b, s, pairs); }
-  void send(const M& m, int dst) { comm->send_dev(m, dst, s); }
-  M recv(int src) { return comm->recv_dev(src, s); }
+  Stats* st;
+  M mul(const M& a, const M& b, int64_t* pairs) {
+    const auto ev = st->begin(st->ev_kernel, s);
+    M c = dev_multiply(a, b, s, pairs);
+    A4_HIP(hipEventRecord(ev.second, s));
+    return c;
+  }
+  void send(const M& m, int dst) {
+    const double t = now_s();
+    comm->send_dev(m, dst, s);
+    st->add(st->t_p2p, now_s() - t);
+  }
+  M recv(int src) {
+    const double t = now_s();
+    M m = comm->recv_dev(src, s);
+    st->add(st->t_p2p, now_s() - t);
+    return m;
+  }
   std::vector<int32_t> keys(const M& m) {
+    const double t = now_s();
     std::vector<int32_t> h((size_t)m.nb * 2);
     if (m.nb) A4_HIP(hipMemcpyAsync(h.data(), m.keys.get(), h.size() * 4, hipMemcpyDeviceToHost, s));
     A4_HIP(hipStreamSynchronize(s));
+    st->add(st->t_d2h, now_s() - t);
     return h;
   }
   M slice(const M& m, int64_t t0, int64_t t1) {
@@ -519,9 +581,24 @@ struct CpuOps {
   using M = Mat;
   Comm* comm;
   int threads;
-  M mul(const M& a, const M& b, int64_t* pairs) { return cpu_multiply(a, b, threads, pairs); }
-  void send(const M& m, int dst) { comm->send_host(m, dst); }
-  M recv(int src) { return comm->recv_host(src); }
+  Stats* st;
+  M mul(const M& a, const M& b, int64_t* pairs) {
+    const double t = now_s();
+    M c = cpu_multiply(a, b, threads, pairs);
+    st->add(st->t_kernel_cpu, now_s() - t);
+    return c;
+  }
+  void send(const M& m, int dst) {
+    const double t = now_s();
+    comm->send_host(m, dst);
+    st->add(st->t_p2p, now_s() - t);
+  }
+  M recv(int src) {
+    const double t = now_s();
+    M m = comm->recv_host(src);
+    st->add(st->t_p2p, now_s() - t);
+    return m;
+  }
   std::vector<int32_t> keys(const M& m) { return m.keys; }
   M slice(const M& m, int64_t t0, int64_t t1) {
     const int64_t kk = (int64_t)m.k * m.k;
@@ -720,10 +797,10 @@ int run(const Options& o, int rank, int world, double t_start) {
   }
   if (N / world != 0 && world > 1) {
     if (gpu) {
-      GpuOps ops{s, comm.get()};
+      GpuOps ops{s, comm.get(), &st};
       gm = cross_rank_tree(ops, std::move(gm), rank, world, o.split, o, st);
     } else {
-      CpuOps ops{comm.get(), o.threads};
+      CpuOps ops{comm.get(), o.threads, &st};
       cpart = cross_rank_tree(ops, std::move(cpart), rank, world, o.split, o, st);
     }
   }
@@ -738,15 +815,26 @@ int run(const Options& o, int rank, int world, double t_start) {
       final_.k = k;   // empty chain: an empty product (0 x 0, no tiles), not a dereference of nothing
     } else if (gpu) {
       A4_CHECK(gm.has_value(), "rank 0 holds no partial product");
-      final_ = dev_download(dev_prune(std::move(*gm), s), s);
+      DevMat pruned = dev_prune(std::move(*gm), s);
+      A4_HIP(hipStreamSynchronize(s));
+      const double t3 = now_s();
+      st.t_prune = t3 - t2;
+      final_ = dev_download(pruned, s);
+      st.t_d2h += now_s() - t3;
     } else {
       A4_CHECK(cpart.has_value(), "rank 0 holds no partial product");
       final_ = cpu_prune(std::move(*cpart));
+      st.t_prune = now_s() - t2;
     }
     if (o.dump) dump("result", final_);
+    const double t4 = now_s();
     write_ref(o.out, final_, o.threads);
+    st.t_format = now_s() - t4;
     st.t_write = now_s() - t2;
     if (!o.metrics.empty()) {
+      if (gpu) A4_HIP(hipDeviceSynchronize());
+      const double t_h2d = Stats::drain(st.ev_h2d), t_kernel = gpu ? Stats::drain(st.ev_kernel) : st.t_kernel_cpu;
+      const double busy = st.t_parse + t_h2d + t_kernel;
       std::ofstream m(o.metrics);
       const double ops = (double)st.tile_pairs * 2.0 * k * k * k;
       m << "{\"engine\": \"native\", \"device\": \"" << (gpu ? "hip" : "cpu") << "\", \"comm\": \"" << comm->name()
@@ -754,7 +842,11 @@ int run(const Options& o, int rank, int world, double t_start) {
         << ", \"tile_pairs\": " << st.tile_pairs << ", \"int_ops\": " << ops << ", \"t_reduce_s\": " << st.t_reduce
         << ", \"t_comm_s\": " << st.t_comm << ", \"t_write_s\": " << st.t_write << ", \"bytes_h2d\": " << st.bytes_h2d
         << ", \"bytes_p2p\": " << (comm->bytes_sent + comm->bytes_recv) << ", \"reduce_gops\": "
-        << (st.t_reduce > 0 ? ops / st.t_reduce / 1e9 : 0.0) << ", \"wall_s\": " << (now_s() - t_start) << "}\n";
+        << (st.t_reduce > 0 ? ops / st.t_reduce / 1e9 : 0.0) << ", \"wall_s\": " << (now_s() - t_start)
+        << ", \"phases\": {\"parse_s\": " << st.t_parse << ", \"h2d_s\": " << t_h2d << ", \"kernel_s\": " << t_kernel
+        << ", \"p2p_s\": " << st.t_p2p << ", \"prune_s\": " << st.t_prune << ", \"d2h_s\": " << st.t_d2h
+        << ", \"format_write_s\": " << st.t_format << ", \"overlap\": " << (st.t_reduce > 0 ? busy / st.t_reduce : 0.0)
+        << "}, \"threads\": " << (o.threads > 0 ? o.threads : (int)std::thread::hardware_concurrency()) << "}\n";
     }
   }
   gpart.reset();
