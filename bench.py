@@ -184,6 +184,9 @@ def main() -> None:
     comm = CM.init(backend=args.backend, device="auto")
     if comm.device.type == "cuda":
         _native.hip()
+    if comm.rank == 0:
+        print(f"[bench] {args.workload}: process group up ({comm.world} rank(s), {comm.device})", file=sys.stderr,
+              flush=True)
     if args.workload == "spgemm":
         step, flops, extra, cfg = run_spgemm(comm, args, args.n, args.density,
                                              "1Mx1M CSR SpGEMM at 0.01% density, 1D row-block via RCCL/xGMI")
@@ -196,6 +199,8 @@ def main() -> None:
     else:
         step, flops, extra, cfg = run_chain(comm, args)
 
+    if comm.rank == 0:
+        print(f"[bench] setup done: {args.workload}, {comm.world} rank(s)", file=sys.stderr, flush=True)
     last = [time.perf_counter()]
 
     def progress(what: str, i: int) -> None:   # long steps (R-MAT scale 24: ~25 s on one GPU) report liveness

@@ -3,8 +3,9 @@
 # (same code path as RCCL apart from the wire).  For each workload the 1-rank and N-rank runs
 # must report the same whole-job work (flops_per_step, nnz_C / nnz_A when present).
 #   NRANKS="1 8" WORKLOADS="spgemm spgemm64k spmm rmat chain" bash tools/gpu_rehearsal.sh
-# R-MAT runs at --scale 20 here: eight ranks sharing one card would each size their streamed
-# panels from the same free memory.
+# R-MAT runs at --scale 20 here (eight ranks sharing one card would each size their streamed
+# panels from the same free memory) and spgemm at n = 2^18 (gloo stages every collective
+# through host memory).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out
@@ -14,6 +15,7 @@ port=29410
 for wl in ${WORKLOADS:-spgemm spgemm64k spmm rmat chain}; do
   extra=""
   [ "$wl" = rmat ] && extra="--scale ${RMAT_SCALE:-20}"
+  [ "$wl" = spgemm ] && extra="--matrix-n ${SPGEMM_N:-262144}"   # gloo moves B through the host: keep it small
   for n in ${NRANKS:-1 8}; do
     port=$((port + 1))
     log=$O/rehearsal_${wl}_$n.log
