@@ -140,7 +140,7 @@ def run_chain(comm, args):
     from bench_chain import PRESETS, device_random_bsr
     from spmm_amd.models.chain import ChainStats, chain_product, reduce_tree
 
-    cfg = PRESETS["medium"]
+    cfg = PRESETS[args.chain_preset]
     g = torch.Generator(device=comm.device)
     g.manual_seed(args.seed + comm.rank)
     mats = [device_random_bsr(cfg["blocks"], 32, cfg["density"], g, comm.device) for _ in range(cfg["n"])]
@@ -149,7 +149,7 @@ def run_chain(comm, args):
     ops = st.tile_pairs * 2 * 32 ** 3
     step = lambda: chain_product(mats)  # noqa: E731
     return step, _allreduce_sum(comm, ops), dict(tile_pairs=st.tile_pairs), dict(
-        model="block-sparse uint64 chain, report Medium preset (k=32, ~100k tiles/chain per GPU)", global_batch=comm.world,
+        model=f"block-sparse uint64 chain, report {args.chain_preset} preset (k=32)", global_batch=comm.world,
         seq_len=cfg["n"], parallelism=f"dp{comm.world}")
 
 
@@ -170,6 +170,8 @@ def main() -> None:
     ap.add_argument("--decomp", default="rowblock", choices=["rowblock", "inner"],
                     help="spgemm / spgemm64k: 1D row-block with B all-gathered (default), or inner-dimension "
                          "split with a sparse reduce-scatter of C")
+    ap.add_argument("--chain-preset", default="medium", choices=["small", "medium", "large"],
+                    help="chain workload: report preset per GPU (weak scaling)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (gloo on GPUs: rehearse several ranks on one card)")
@@ -231,6 +233,8 @@ def main() -> None:
         unit = "GOP/s (integer, 2k^3 per tile pair)"
         metric = "block-sparse uint64 chain product throughput (report.pdf §4.2)"
         vs = value / (500.0 * comm.world)
+    elif args.workload == "spmm":
+        metric = "GFLOP/s (whole node), CSR x dense 128-col SpMM, bf16 MFMA"
     if comm.rank == 0:
         rec = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": comm.world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,

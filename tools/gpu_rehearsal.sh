@@ -16,6 +16,7 @@ for wl in ${WORKLOADS:-spgemm spgemm64k spmm rmat chain}; do
   extra=""
   [ "$wl" = rmat ] && extra="--scale ${RMAT_SCALE:-20}"
   [ "$wl" = spgemm ] && extra="--matrix-n ${SPGEMM_N:-262144}"   # gloo moves B through the host: keep it small
+  [ "$wl" = chain ] && extra="--chain-preset small"                 # weak scaling: N chains share the one card
   for n in ${NRANKS:-1 8}; do
     port=$((port + 1))
     log=$O/rehearsal_${wl}_$n.log
