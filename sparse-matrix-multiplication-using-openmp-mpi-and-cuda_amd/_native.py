@@ -103,9 +103,9 @@ def hip():
                 _sig(lib, "spmm_bsr_u64_numeric", C.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int,
                      C.c_int64, c_vp)
                 _sig(lib, "spmm_bsr_u64_nonzero", C.c_int, c_vp, C.c_int, C.c_int64, c_vp, c_vp)
-                for name, args in _HIP_EXTRA.items():
+                for name, (res, args) in _HIP_EXTRA.items():
                     if hasattr(lib, name):
-                        _sig(lib, name, C.c_int, *args)
+                        _sig(lib, name, res, *args)
                 _hip = lib
     return _hip
 
@@ -115,10 +115,10 @@ def hip():
 _HIP_EXTRA: dict = {}
 
 
-def register_hip(name: str, *argtypes) -> None:
-    _HIP_EXTRA[name] = argtypes
+def register_hip(name: str, *argtypes, restype=C.c_int) -> None:
+    _HIP_EXTRA[name] = (restype, argtypes)
     if _hip is not None and hasattr(_hip, name):
-        _sig(_hip, name, C.c_int, *argtypes)
+        _sig(_hip, name, restype, *argtypes)
 
 
 def check(rc: int, what: str) -> None:

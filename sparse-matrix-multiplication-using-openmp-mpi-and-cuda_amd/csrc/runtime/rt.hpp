@@ -164,6 +164,16 @@ int spmm_bsr_u64_numeric(const void* Avals, const void* Bvals, const int32_t* pa
                          const int64_t* tile_ptr, void* Cvals, int32_t* nz_flag, int k, int64_t ntiles,
                          void* stream);
 int spmm_bsr_u64_nonzero(const void* vals, int k, int64_t ntiles, int32_t* nz_flag, void* stream);
+// in-tree primitives and the shared symbolic phase (csrc/kernels/prim.hip)
+size_t spmm_prim_scan_ws(int64_t n);
+int spmm_prim_scan(const void* in, int in_bytes, int64_t n, int64_t* out, int inclusive, void* ws, void* stream);
+size_t spmm_bsr_sym_plan_ws(int64_t na);
+int spmm_bsr_sym_plan(const int32_t* akeys, int64_t na, const int32_t* bkeys, int64_t nb, int64_t* start, int64_t* lo,
+                      void* ws, int64_t* plan, void* stream);
+size_t spmm_bsr_sym_build_ws(int64_t np);
+int spmm_bsr_sym_build(const int32_t* akeys, const int32_t* bkeys, int64_t na, const int64_t* start, const int64_t* lo,
+                       const int64_t* plan, void* ws, int32_t* okeys, int64_t* tile_ptr, int32_t* pa, int32_t* pb,
+                       int64_t* nt, void* stream);
 int spmm_cpu_bsr_u64_numeric(const uint64_t* A, const uint64_t* B, const int32_t* pa, const int32_t* pb,
                              const int64_t* tile_ptr, uint64_t* C, int32_t* nz_flag, int k, int64_t ntiles,
                              int nthreads);

@@ -26,9 +26,23 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import ctypes as C
+
 import torch
 
 from .. import _native
+from .._native import c_vp
+
+# the shared symbolic phase (csrc/kernels/prim.hip), also used by the native a4 engine
+_native.register_hip("spmm_bsr_sym_plan_ws", C.c_int64, restype=C.c_size_t)
+_native.register_hip("spmm_bsr_sym_plan", c_vp, C.c_int64, c_vp, C.c_int64, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_bsr_sym_build_ws", C.c_int64, restype=C.c_size_t)
+_native.register_hip("spmm_bsr_sym_build", c_vp, c_vp, C.c_int64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                     c_vp)
+_native.register_hip("spmm_prim_scan_ws", C.c_int64, restype=C.c_size_t)
+_native.register_hip("spmm_prim_scan", c_vp, C.c_int, C.c_int64, c_vp, C.c_int, c_vp, c_vp)
+_native.register_hip("spmm_prim_sort_ws", C.c_int64, restype=C.c_size_t)
+_native.register_hip("spmm_prim_sort_pairs_u64", c_vp, c_vp, C.c_int64, C.c_int, c_vp, c_vp)
 
 U64_MAX = (1 << 64) - 1
 _OFF = 1 << 31
@@ -134,7 +148,14 @@ def bsr_symbolic(a_keys: torch.Tensor, b_keys: torch.Tensor) -> BsrPairs:
     are already in ascending j for every (i, k); a stable sort by (i, k) groups
     them without disturbing that order — which is the per-element summation
     order the reference's kernel uses (:54-56), needed for bit-exactness.
+
+    On the GPU this is the in-tree symbolic phase of csrc/kernels/prim.hip
+    (pair counts, scan, fill with compact keys, stable LSD radix sort,
+    run-length encode) — the same code the native ``a4`` engine runs; the
+    torch formulation below serves CPU tensors.
     """
+    if a_keys.device.type == "cuda":
+        return _bsr_symbolic_native(a_keys.contiguous(), b_keys.contiguous())
     dev = a_keys.device
     a_r = a_keys[:, 0].contiguous()
     a_c = a_keys[:, 1].contiguous()
@@ -157,6 +178,39 @@ def bsr_symbolic(a_keys: torch.Tensor, b_keys: torch.Tensor) -> BsrPairs:
     tile_ptr = torch.zeros(uniq.shape[0] + 1, dtype=torch.int64, device=dev)
     torch.cumsum(counts, 0, out=tile_ptr[1:])
     return BsrPairs(decode_keys(uniq), tile_ptr, a_idx[perm].to(torch.int32), b_idx[perm].to(torch.int32))
+
+
+def _bsr_symbolic_native(a_keys: torch.Tensor, b_keys: torch.Tensor) -> BsrPairs:
+    dev = a_keys.device
+    lib = _native.hip()
+    P = _native.ptr
+    st = _native.stream_ptr(dev)
+    na, nb = a_keys.shape[0], b_keys.shape[0]
+    z = torch.zeros(1, dtype=torch.int64, device=dev)
+    e32 = torch.empty(0, dtype=torch.int32, device=dev)
+    empty = BsrPairs(torch.empty((0, 2), dtype=torch.int32, device=dev), z, e32, e32)
+    if na == 0 or nb == 0:
+        return empty
+    start = torch.empty(na + 1, dtype=torch.int64, device=dev)
+    lo = torch.empty(na, dtype=torch.int64, device=dev)
+    ws = torch.empty(int(lib.spmm_bsr_sym_plan_ws(na)), dtype=torch.uint8, device=dev)
+    plan = (C.c_int64 * 5)()
+    _native.check(lib.spmm_bsr_sym_plan(P(a_keys), na, P(b_keys), nb, P(start), P(lo), P(ws), plan, st),
+                  "spmm_bsr_sym_plan")
+    np_ = plan[0]
+    if np_ == 0:
+        return empty
+    del ws
+    ws = torch.empty(int(lib.spmm_bsr_sym_build_ws(np_)), dtype=torch.uint8, device=dev)
+    okeys = torch.empty((np_, 2), dtype=torch.int32, device=dev)
+    tile_ptr = torch.empty(np_ + 1, dtype=torch.int64, device=dev)
+    pa = torch.empty(np_, dtype=torch.int32, device=dev)
+    pb = torch.empty(np_, dtype=torch.int32, device=dev)
+    nt = C.c_int64()
+    _native.check(lib.spmm_bsr_sym_build(P(a_keys), P(b_keys), na, P(start), P(lo), plan, P(ws), P(okeys),
+                                         P(tile_ptr), P(pa), P(pb), C.byref(nt), st), "spmm_bsr_sym_build")
+    n = nt.value
+    return BsrPairs(okeys[:n].clone(), tile_ptr[:n + 1].clone(), pa, pb)   # (release the np-sized buffers)
 
 
 def bsr_numeric(A: BSR, B: BSR, sym: BsrPairs):
