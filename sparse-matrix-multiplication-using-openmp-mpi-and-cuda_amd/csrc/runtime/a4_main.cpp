@@ -537,6 +537,17 @@ struct GpuOps {
     st->add(st->t_p2p, now_s() - t);
     return m;
   }
+  void send_many(const std::vector<const M*>& ms, const std::vector<int>& dsts) {
+    const double t = now_s();
+    comm->send_many_dev(ms, dsts, s);
+    st->add(st->t_p2p, now_s() - t);
+  }
+  std::vector<M> recv_many(const std::vector<int>& srcs) {
+    const double t = now_s();
+    std::vector<M> r = comm->recv_many_dev(srcs, s);
+    st->add(st->t_p2p, now_s() - t);
+    return r;
+  }
   std::vector<int32_t> keys(const M& m) {
     const double t = now_s();
     std::vector<int32_t> h((size_t)m.nb * 2);
@@ -598,6 +609,17 @@ struct CpuOps {
     M m = comm->recv_host(src);
     st->add(st->t_p2p, now_s() - t);
     return m;
+  }
+  void send_many(const std::vector<const M*>& ms, const std::vector<int>& dsts) {
+    const double t = now_s();
+    comm->send_many_host(ms, dsts);
+    st->add(st->t_p2p, now_s() - t);
+  }
+  std::vector<M> recv_many(const std::vector<int>& srcs) {
+    const double t = now_s();
+    std::vector<M> r = comm->recv_many_host(srcs);
+    st->add(st->t_p2p, now_s() - t);
+    return r;
   }
   std::vector<int32_t> keys(const M& m) { return m.keys; }
   M slice(const M& m, int64_t t0, int64_t t1) {
@@ -677,7 +699,18 @@ std::optional<typename Ops::M> cross_rank_tree(Ops& ops, std::optional<typename 
     if (rank == g0) {
       say(o, "multiplying " + std::to_string(g0 / step) + " " + std::to_string(g0 / step + 1));
       const std::vector<int64_t> cut = row_cuts(ops.keys(*part), np);
-      for (int i = 1; i < np; ++i) ops.send(ops.slice(*part, cut[(size_t)i], cut[(size_t)i + 1]), g0 + i);
+      {   // every member's L panel in one fan-out
+        std::vector<M> panels;
+        std::vector<const M*> ms;
+        std::vector<int> dsts;
+        panels.reserve((size_t)np);
+        for (int i = 1; i < np; ++i) {
+          panels.push_back(ops.slice(*part, cut[(size_t)i], cut[(size_t)i + 1]));
+          dsts.push_back(g0 + i);
+        }
+        for (auto& p : panels) ms.push_back(&p);
+        ops.send_many(ms, dsts);
+      }
       M R = ops.recv(partner);
       std::vector<M> C;
       {
@@ -686,14 +719,20 @@ std::optional<typename Ops::M> cross_rank_tree(Ops& ops, std::optional<typename 
         C.push_back(ops.mul(L0, R, &pairs));
         count(pairs);
       }
-      for (int i = 1; i < np; ++i) C.push_back(ops.recv(g0 + i));
+      std::vector<int> srcs;
+      for (int i = 1; i < np; ++i) srcs.push_back(g0 + i);
+      for (M& Ci : ops.recv_many(srcs)) C.push_back(std::move(Ci));   // one fan-in
       part = ops.concat(C);
     } else if (rank < gend) {
       M Li = ops.recv(g0);
-      if (rank == partner) {
+      if (rank == partner) {   // R to every member and to g0 in one fan-out
+        std::vector<const M*> ms;
+        std::vector<int> dsts;
         for (int h = g0 + 1; h < gend; ++h)
-          if (h != partner) ops.send(*part, h);
-        ops.send(*part, g0);
+          if (h != partner) { ms.push_back(&*part); dsts.push_back(h); }
+        ms.push_back(&*part);
+        dsts.push_back(g0);
+        ops.send_many(ms, dsts);
         M Ci = ops.mul(Li, *part, &pairs);
         part.reset();
         count(pairs);

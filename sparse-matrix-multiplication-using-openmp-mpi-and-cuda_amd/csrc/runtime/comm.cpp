@@ -103,6 +103,8 @@ class RcclComm : public Comm {
   }
   ~RcclComm() override {
     if (comm_) ncclCommDestroy(comm_);
+    if (dh_) (void)hipFree(dh_);
+    if (hh_) (void)hipHostFree(hh_);
     if (dhdr_) (void)hipFree(dhdr_);
     if (hhdr_) (void)hipHostFree(hhdr_);
     if (own_) (void)hipStreamDestroy(own_);
@@ -135,6 +137,61 @@ class RcclComm : public Comm {
     }
     bytes_recv += M.bytes() + 32;
     return M;
+  }
+  // One group for the whole fan-out: the headers and payloads of every
+  // destination are in flight together (each peer over its own xGMI link),
+  // then one bounded wait.  Receivers post header then payload per source,
+  // which matches the per-peer order of the grouped sends.
+  void send_many_dev(const std::vector<const DevMat*>& ms, const std::vector<int>& dsts, hipStream_t s) override {
+    if (ms.empty()) return;
+    maybe_inject_fault("send");
+    const size_t n = ms.size();
+    ensure_hdrs(n);
+    for (size_t i = 0; i < n; ++i) {
+      const DevMat& M = *ms[i];
+      hh_[4 * i] = M.rows; hh_[4 * i + 1] = M.cols; hh_[4 * i + 2] = M.k; hh_[4 * i + 3] = M.nb;
+    }
+    A4_HIP(hipMemcpyAsync(dh_, hh_, n * 4 * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    A4_NCCL(ncclGroupStart());
+    for (size_t i = 0; i < n; ++i) {
+      const DevMat& M = *ms[i];
+      A4_NCCL(ncclSend(dh_ + 4 * i, 4, ncclInt64, dsts[i], comm_, s));
+      if (M.nb) {
+        A4_NCCL(ncclSend(M.keys.get(), (size_t)M.nb * 2, ncclInt32, dsts[i], comm_, s));
+        A4_NCCL(ncclSend(M.vals.get(), (size_t)M.nb * M.k * M.k, ncclUint64, dsts[i], comm_, s));
+      }
+      bytes_sent += M.bytes() + 32;
+    }
+    A4_NCCL(ncclGroupEnd());
+    wait(s);   // callers free the matrices right after
+  }
+  std::vector<DevMat> recv_many_dev(const std::vector<int>& srcs, hipStream_t s) override {
+    const size_t n = srcs.size();
+    std::vector<DevMat> out(n);
+    if (!n) return out;
+    ensure_hdrs(n);
+    A4_NCCL(ncclGroupStart());
+    for (size_t i = 0; i < n; ++i) A4_NCCL(ncclRecv(dh_ + 4 * i, 4, ncclInt64, srcs[i], comm_, s));
+    A4_NCCL(ncclGroupEnd());
+    A4_HIP(hipMemcpyAsync(hh_, dh_, n * 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    wait(s);
+    for (size_t i = 0; i < n; ++i) {
+      DevMat& M = out[i];
+      M.rows = hh_[4 * i]; M.cols = hh_[4 * i + 1]; M.k = (int)hh_[4 * i + 2]; M.nb = hh_[4 * i + 3];
+      M.keys = DevBuf<int32_t>((size_t)M.nb * 2, s);
+      M.vals = DevBuf<uint64_t>((size_t)M.nb * M.k * M.k, s);
+    }
+    A4_NCCL(ncclGroupStart());
+    for (size_t i = 0; i < n; ++i) {
+      DevMat& M = out[i];
+      if (M.nb) {
+        A4_NCCL(ncclRecv(M.keys.get(), (size_t)M.nb * 2, ncclInt32, srcs[i], comm_, s));
+        A4_NCCL(ncclRecv(M.vals.get(), (size_t)M.nb * M.k * M.k, ncclUint64, srcs[i], comm_, s));
+      }
+      bytes_recv += M.bytes() + 32;
+    }
+    A4_NCCL(ncclGroupEnd());
+    return out;
   }
   void send_host(const Mat& M, int dst) override {
     DevMat d = dev_upload(M, own_);
@@ -173,6 +230,18 @@ class RcclComm : public Comm {
       usleep(50);
     }
   }
+  // pinned host + device header slots for grouped transfers (4 int64 each)
+  void ensure_hdrs(size_t n) {
+    if (n <= nhdr_) return;
+    if (hh_) A4_HIP(hipHostFree(hh_));
+    if (dh_) A4_HIP(hipFree(dh_));
+    nhdr_ = std::max<size_t>(n, 8);
+    A4_HIP(hipHostMalloc(reinterpret_cast<void**>(&hh_), nhdr_ * 4 * sizeof(int64_t), hipHostMallocDefault));
+    A4_HIP(hipMalloc(reinterpret_cast<void**>(&dh_), nhdr_ * 4 * sizeof(int64_t)));
+  }
+  size_t nhdr_ = 0;
+  int64_t* hh_ = nullptr;
+  int64_t* dh_ = nullptr;
   double timeout_s_;
   ncclComm_t comm_ = nullptr;
   hipStream_t own_ = nullptr;

@@ -16,6 +16,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "rt.hpp"
 
@@ -33,6 +34,26 @@ class Comm {
   // device matrices (GPU engine), ordered on `s`
   virtual void send_dev(const DevMat& M, int dst, hipStream_t s) = 0;
   virtual DevMat recv_dev(int src, hipStream_t s) = 0;
+  // fan-out / fan-in of one tree step: ms[i] to dsts[i] (any may repeat a
+  // matrix), and one matrix from each of srcs.  Default: one peer at a time;
+  // RCCL issues each side as ONE group (concurrent over the xGMI links) with
+  // a single host wait.
+  virtual void send_many_dev(const std::vector<const DevMat*>& ms, const std::vector<int>& dsts, hipStream_t s) {
+    for (size_t i = 0; i < ms.size(); ++i) send_dev(*ms[i], dsts[i], s);
+  }
+  virtual std::vector<DevMat> recv_many_dev(const std::vector<int>& srcs, hipStream_t s) {
+    std::vector<DevMat> out;
+    for (int r : srcs) out.push_back(recv_dev(r, s));
+    return out;
+  }
+  virtual void send_many_host(const std::vector<const Mat*>& ms, const std::vector<int>& dsts) {
+    for (size_t i = 0; i < ms.size(); ++i) send_host(*ms[i], dsts[i]);
+  }
+  virtual std::vector<Mat> recv_many_host(const std::vector<int>& srcs) {
+    std::vector<Mat> out;
+    for (int r : srcs) out.push_back(recv_host(r));
+    return out;
+  }
   virtual void barrier() = 0;
   virtual double allreduce_max(double x) = 0;
   virtual void abort(int code) = 0;
