@@ -25,6 +25,8 @@ Extra options (all optional; env equivalents SPMM_*):
   --metrics-json PATH per-rank phase times, bytes moved and throughput
   --no-split          cross-rank tree products on one rank each (default: each
                       product is row-panel split over the ranks of its group)
+  --exact / --fast    chain split: the reference's count split (default, bit-exact
+                      by construction) or ranges balanced on the files' sizes
 """
 from __future__ import annotations
 
@@ -48,6 +50,9 @@ def main(argv=None) -> int:
     ap.add_argument("--quiet", action="store_true", default=bool(os.environ.get("SPMM_QUIET")))
     ap.add_argument("--metrics-json", default=os.environ.get("SPMM_METRICS_JSON"))
     ap.add_argument("--no-split", action="store_true", default=bool(os.environ.get("SPMM_NO_SPLIT")))
+    g = ap.add_mutually_exclusive_group()
+    g.add_argument("--fast", action="store_true", default=bool(os.environ.get("SPMM_FAST")))
+    g.add_argument("--exact", dest="fast", action="store_false")
     args = ap.parse_args(argv)
     if args.format == "ref" and len(args.inputs) != 1:
         ap.error("the reference format takes one folder")
@@ -70,7 +75,7 @@ def main(argv=None) -> int:
     try:
         log = None if args.quiet else (lambda s: print(s, flush=True))
         run_chain(args.folder, comm, out_path=args.out, log=log, nthreads=args.threads, stats=stats,
-                  split=not args.no_split)
+                  split=not args.no_split, fast=args.fast)
     except refio.FormatError as e:
         print(str(e), file=sys.stderr)
         rc = 1

@@ -56,7 +56,7 @@ namespace {
 struct Options {
   std::string folder, out = "matrix", device = "auto", comm = "auto", metrics, save_dir, load_dir;
   int threads = 0, streams = 4;
-  bool quiet = false, dump = false, split = true;
+  bool quiet = false, dump = false, split = true, fast = false;
   double timeout = 600.0;
 };
 
@@ -64,7 +64,7 @@ struct Options {
   std::cerr << "a4: " << why << "\n"
             << "usage: a4 <folder> [--out PATH] [--device auto|hip|cpu] [--comm auto|rccl|mpi] [--threads N]\n"
                "          [--streams N] [--quiet] [--dump] [--metrics-json PATH] [--save-partials DIR]\n"
-               "          [--load-partials DIR] [--timeout S] [--no-split]\n";
+               "          [--load-partials DIR] [--timeout S] [--no-split] [--exact | --fast]\n";
   std::exit(2);
 }
 
@@ -83,6 +83,8 @@ Options parse_args(int argc, char** argv) {
     else if (a == "--streams") o.streams = std::max(1, std::atoi(val().c_str()));
     else if (a == "--quiet") o.quiet = true;
     else if (a == "--no-split") o.split = false;
+    else if (a == "--fast") o.fast = true;     // cost-balanced chain ranges (SURVEY §5.6 fast mode)
+    else if (a == "--exact") o.fast = false;   // the reference's split and association (default)
     else if (a == "--dump") o.dump = true;
     else if (a == "--metrics-json") o.metrics = val();
     else if (a == "--save-partials") o.save_dir = val();
@@ -748,6 +750,38 @@ std::optional<typename Ops::M> cross_rank_tree(Ops& ops, std::optional<typename 
   return part;
 }
 
+// --fast: contiguous chain ranges balanced on the matrix files' sizes (a
+// proxy for their tile counts, known before anything is parsed), greedy on
+// prefix sums with >= 1 matrix per rank — parallel/partition.py
+// chain_ranges_balanced.  The reference splits by count (:437-456), which
+// --exact keeps: a different split re-associates the chain, and the
+// reference's ==2^64-1 -> 0 collapse makes the product order-sensitive
+// (SURVEY §0.1), so only the default split is bit-exact by construction.
+std::pair<int, int> balanced_range(const std::string& folder, int64_t n, int p, int rank) {
+  std::vector<double> cost((size_t)n, 1.0);
+  for (int64_t i = 0; i < n; ++i) {
+    struct stat sb;
+    if (stat((folder + "/matrix" + std::to_string(i + 1)).c_str(), &sb) == 0) cost[(size_t)i] = (double)sb.st_size;
+  }
+  double total = 0;
+  for (double c : cost) total += c;
+  int64_t lo = 0;
+  double acc = 0;
+  for (int r = 0; r < p; ++r) {
+    if (r == p - 1) return r == rank ? std::make_pair((int)lo, (int)n - 1) : std::make_pair(-1, -1);
+    const double target = total * (r + 1) / p;
+    int64_t hi = lo;
+    acc += cost[(size_t)hi];
+    while (hi + 1 < n - (p - r - 1) && acc + cost[(size_t)hi + 1] / 2 <= target) {
+      ++hi;
+      acc += cost[(size_t)hi];
+    }
+    if (r == rank) return {(int)lo, (int)hi};
+    lo = hi + 1;
+  }
+  return {-1, -1};
+}
+
 int local_rank() {
   for (const char* v : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "SLURM_LOCALID"}) {
     const char* x = std::getenv(v);
@@ -786,6 +820,10 @@ int run(const Options& o, int rank, int world, double t_start) {
   int lo = -1, hi = -1;
   if (N < world) {
     if (rank == 0) { lo = 0; hi = (int)N - 1; }
+  } else if (o.fast) {
+    const std::pair<int, int> r = balanced_range(o.folder, N, world, rank);
+    lo = r.first;
+    hi = r.second;
   } else {
     const int64_t op = N / world;
     lo = (int)(rank * op);

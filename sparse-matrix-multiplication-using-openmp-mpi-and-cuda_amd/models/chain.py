@@ -34,7 +34,7 @@ import torch
 
 from ..ops.bsr import BSR, bsr_matmul, prune_zero_tiles, tile_pair_count
 from ..parallel.comm import Comm
-from ..parallel.partition import chain_ranges
+from ..parallel.partition import chain_ranges, chain_ranges_balanced
 from ..utils import refio
 
 Log = Callable[[str], None]
@@ -146,12 +146,22 @@ def _sync(dev: torch.device) -> None:
 
 
 def run_chain(folder: str, comm: Comm, out_path: Optional[str] = "matrix", log: Optional[Log] = print,
-              nthreads: int = 0, stats: Optional[ChainStats] = None, split: bool = True) -> Optional[BSR]:
+              nthreads: int = 0, stats: Optional[ChainStats] = None, split: bool = True,
+              fast: bool = False) -> Optional[BSR]:
     """The full reference pipeline on this rank.  Returns the final product on
-    rank 0 (pruned), None elsewhere.  Writes ``out_path`` on rank 0 unless None."""
+    rank 0 (pruned), None elsewhere.  Writes ``out_path`` on rank 0 unless None.
+    ``fast``: chain ranges balanced on the matrix files' sizes instead of the
+    reference's count split (re-associates the chain: identical output unless
+    a partial sum hits the 2^64-1 collapse)."""
     stats = stats if stats is not None else ChainStats()
     n, k = refio.read_size(folder)
-    ranges = chain_ranges(n, comm.world)
+    if fast and n >= comm.world:
+        import os
+
+        costs = [os.path.getsize(refio.matrix_path(folder, i + 1)) for i in range(n)]
+        ranges = chain_ranges_balanced(costs, comm.world)
+    else:
+        ranges = chain_ranges(n, comm.world)
     my = ranges[comm.rank]
     dev = comm.device
     part: Optional[BSR] = None

@@ -73,6 +73,23 @@ def test_a4_cpu_row_panel_split_matches_unsplit(tmp_path, a4_bin, n, p):
     assert outs[0] == outs[1] == golden.to_text(golden.chain([golden.from_bsr(m) for m in mats], p=p))
 
 
+@pytest.mark.parametrize("p", [2, 3])
+def test_a4_cpu_fast_split(tmp_path, a4_bin, p):
+    """Native ``--fast`` (chain ranges balanced on file sizes) on unequal tile
+    grids: same output as the exact golden product (uniform 64-bit values
+    never hit the 2^64-1 collapse), every product logged once."""
+    shapes = [12, 14, 12, 13, 3, 2, 3, 2, 3]
+    mats = gen.random_chain(len(shapes) - 1, 0, 4, 0.6, "full", seed=40 + p, shapes=shapes)
+    folder = str(tmp_path / "in")
+    refio.write_folder(folder, mats, 4)
+    out = str(tmp_path / "matrix")
+    r = _run(a4_bin, p, folder, "--device", "cpu", "--out", out, "--threads", "2", "--fast")
+    want = golden.chain([golden.from_bsr(m) for m in mats], p=p)
+    with open(out) as f:
+        assert f.read() == golden.to_text(want)
+    assert len(re.findall(r"multiplying \d+ \d+", r.stdout)) == len(mats) - 1
+
+
 def test_a4_missing_size_file(tmp_path, a4_bin):
     r = _run(a4_bin, 1, str(tmp_path / "nowhere"), "--device", "cpu", check=False)
     assert r.returncode != 0
