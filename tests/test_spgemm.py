@@ -515,12 +515,20 @@ def test_free_mem_asks_allocator_only_when_needed(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,d", [(3000, 0.02), (70000, 0.0015)])
-def test_spgemm_row_splits_match_searchsorted(n, d):
+@pytest.mark.parametrize("m,n,d,empty", [(3000, 3000, 0.02, False), (70000, 70000, 0.0015, False),
+                                         (2999, 1237, 0.01, True), (5001, 77777, 0.0004, True)])
+def test_spgemm_row_splits_match_searchsorted(m, n, d, empty):
     """Eighth split points of every B row (8 lanes per row, one binary search
-    per lane) against torch.searchsorted on each row."""
+    per lane) against torch.searchsorted on each row; rectangular B whose
+    column count is not a multiple of 8 (the floor in q * n / 8 matters) and
+    with empty rows."""
     dev = torch.device("cuda")
-    B = gen_csr.uniform_csr(n, n, d, seed=81, device=dev)
+    B = gen_csr.uniform_csr(m, n, d, seed=81)
+    if empty:   # every 5th row empty, and the last one
+        keep = (B.row_ids() % 5 != 0) & (B.row_ids() != m - 1)
+        B = CS.from_coo(B.row_ids()[keep], B.col[keep].long(), B.val[keep], m, n)
+        assert int((B.rowptr[1:] == B.rowptr[:-1]).sum()) >= m // 5
+    B = B.to(dev)
     B = CS.CSR(B.m, B.n, B.rowptr, B.col, B.val)
     sp = SG._splits(B).view(B.m, 7).cpu()
     rp, col = B.rowptr.cpu(), B.col.cpu()
