@@ -104,23 +104,35 @@ def run_rmat(comm, args):
         torch.cuda.empty_cache()
     stream = args.rmat_stream == "on" or (args.rmat_stream == "auto" and local_products > MS.stream_budget(comm.device))
     info = SpgemmInfo()
+    check = dict(panels=0, sum_val=0.0, sum_col=0)
     if stream:
         nnz = [0]
 
         def consume(_lo, _hi, C):   # C's row panel is complete here; count it and let it go
             nnz[0] += C.nnz
 
-        prob.step(comm, info, consume)
+        def consume_check(_lo, _hi, C):   # setup run only (untimed): observe every panel
+            check["panels"] += 1
+            check["sum_val"] += float(C.val.double().sum())
+            check["sum_col"] += int(C.col.long().sum())
+            consume(_lo, _hi, C)
+
+        prob.step(comm, info, consume_check)
         step = lambda: prob.step(comm, None, consume)  # noqa: E731
     else:
         C = prob.step(comm, info)
+        check.update(panels=1, sum_val=float(C.val.double().sum()), sum_col=int(C.col.long().sum()))
         del C
         step = lambda: prob.step(comm)  # noqa: E731
     if comm.device.type == "cuda":
         torch.cuda.empty_cache()
     par = f"rowblock{comm.world}-product-balanced" + ("-streamed-C" if stream else "")
     return step, int(_allreduce_sum(comm, info.flops)), dict(
-        nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(_allreduce_sum(comm, info.nnz)), c_streamed=stream), dict(
+        nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(_allreduce_sum(comm, info.nnz)), c_streamed=stream,
+        # C observed in the untimed setup product: sums over all ranks' panels (unit weights: exact integers)
+        c_checksum=dict(panels=int(_allreduce_sum(comm, check["panels"])),
+                        sum_val=_allreduce_sum(comm, check["sum_val"]),
+                        sum_col=int(_allreduce_sum(comm, check["sum_col"])))), dict(
         model=f"R-MAT scale-{args.scale} A.A^T", scale=args.scale, edge_factor=args.edge_factor, global_batch=1,
         seq_len=1 << args.scale, parallelism=par)
 

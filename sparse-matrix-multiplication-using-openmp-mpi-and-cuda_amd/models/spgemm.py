@@ -276,9 +276,23 @@ def streamed_spgemm(A: CSR, B: CSR, consume: Callable[[int, int, CSR], None], bu
 
     nprod = row_nprod(A, B)
     budget = budget if budget is not None else stream_budget(A.device)
-    for lo, hi in stream_panels(nprod, budget):
+    todo = list(reversed(stream_panels(nprod, budget)))
+    while todo:
+        lo, hi = todo.pop()
         pi = SpgemmInfo()
-        C = spgemm(A.row_slice(lo, hi), B, pi)
+        try:
+            C = spgemm(A.row_slice(lo, hi), B, pi)
+        except torch.OutOfMemoryError:
+            # the budget was a forecast: split the panel and go on with a
+            # smaller budget (a single row that does not fit is a real limit)
+            if hi - lo <= 1:
+                raise
+            if A.device.type == "cuda":
+                torch.cuda.empty_cache()
+            mid = (lo + hi) // 2
+            todo += [(mid, hi), (lo, mid)]
+            info.rows_per_bin_num["oom_splits"] = info.rows_per_bin_num.get("oom_splits", 0) + 1
+            continue
         info.flops += pi.flops
         info.nnz += pi.nnz
         info.resorted_rows += pi.resorted_rows

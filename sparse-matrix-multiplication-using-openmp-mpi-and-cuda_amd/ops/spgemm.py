@@ -290,12 +290,37 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     """C = A . B.  ``B_ready``: B's columns / values are still in flight (a
     distributed gather); ``B`` then only needs a valid row pointer, and
     ``B_ready()`` is called for the complete operand right before the first
-    kernel that reads them (product counts and row binning overlap it)."""
+    kernel that reads them (product counts and row binning overlap it).
+
+    Memory admission is a forecast (free-memory fractions); when a one-pass
+    mode still runs out of device memory, the product is redone with the
+    two-phase symbolic + numeric path, which allocates exactly nnz(C) and no
+    staging buffer (``info.rows_per_bin_num["oom_fallback"]`` records it)."""
+    info = info if info is not None else SpgemmInfo()
+    if A.device.type != "cuda":
+        return _spgemm(A, B, info, B_ready)
+    try:
+        return _spgemm(A, B, info, B_ready)
+    except torch.OutOfMemoryError:
+        if CONFIG.spgemm_onepass == "off" and CONFIG.spgemm_bitmap == "off":
+            raise   # already the lowest-memory path
+    torch.cuda.empty_cache()
+    saved = (CONFIG.spgemm_onepass, CONFIG.spgemm_bitmap, CONFIG.spgemm_pipeline)
+    CONFIG.spgemm_onepass, CONFIG.spgemm_bitmap, CONFIG.spgemm_pipeline = "off", "off", "off"
+    try:
+        info.rows_per_bin_num = {}
+        C_ = _spgemm(A, B, info, B_ready)
+    finally:
+        CONFIG.spgemm_onepass, CONFIG.spgemm_bitmap, CONFIG.spgemm_pipeline = saved
+    info.rows_per_bin_num["oom_fallback"] = 1
+    return C_
+
+
+def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None) -> CSR:
     if A.n != B.m:
         raise ValueError(f"inner dimensions differ: {A.n} vs {B.m}")
     if A.device != B.device:
         raise ValueError("operands on different devices")
-    info = info if info is not None else SpgemmInfo()
     if A.device.type != "cuda":
         return _spgemm_cpu(A, B_ready() if B_ready is not None else B, info)
     A = A if A.val.dtype == torch.float32 else A.with_values(A.val.float())

@@ -807,3 +807,52 @@ def test_spgemm_gpu_long_rows_wave_items(monkeypatch, onepass):
         assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
         assert torch.equal(Cg.col.cpu(), Cc.col)
         assert torch.equal(Cg.val.cpu(), Cc.val)   # small integers: every order sums exactly
+
+
+def test_streamed_spgemm_splits_panels_on_oom(monkeypatch):
+    """A streamed panel that runs out of device memory is split in half and
+    retried: consumers still get contiguous panels in row order and the
+    product is unchanged."""
+    from spmm_amd.models import spgemm as MS
+
+    A = gen_csr.uniform_csr(300, 200, 0.05, seed=61)
+    B = gen_csr.uniform_csr(200, 250, 0.05, seed=62)
+    real = MS.spgemm
+
+    def flaky(Ap, Bm, info=None, B_ready=None):
+        if Ap.m > 37:
+            raise torch.OutOfMemoryError("simulated")
+        return real(Ap, Bm, info)
+
+    monkeypatch.setattr(MS, "spgemm", flaky)
+    got = []
+    info = MS.streamed_spgemm(A, B, lambda lo, hi, C: got.append((lo, hi, C)), budget=10 ** 9)
+    assert info.rows_per_bin_num["oom_splits"] >= 3
+    assert got[0][0] == 0 and got[-1][1] == A.m and all(a[1] == b[0] for a, b in zip(got, got[1:]))
+    assert all(hi - lo <= 37 for lo, hi, _ in got)
+    ref = real(A, B)
+    dense = torch.cat([C.to_dense() for _, _, C in got])
+    assert torch.allclose(dense, ref.to_dense(), atol=1e-6)
+    assert info.nnz == ref.nnz
+
+
+@pytest.mark.gpu
+def test_spgemm_gpu_oom_falls_back_to_two_phase(monkeypatch):
+    """A one-pass mode that runs out of memory is redone by the two-phase
+    symbolic + numeric path (exact allocation), with the same result."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(4000, 3000, 0.004, seed=63, device=dev)
+    B = gen_csr.uniform_csr(3000, 200000, 0.0004, seed=64, device=dev)
+    ref = SG.spgemm(A, B)
+
+    def oom(*a, **k):
+        raise torch.OutOfMemoryError("simulated")
+
+    monkeypatch.setattr(SG, "onepass_bitmap", oom)
+    monkeypatch.setattr(SG, "onepass_ordered", oom)
+    monkeypatch.setattr(SG, "onepass", oom)
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, B, info)
+    assert info.rows_per_bin_num.get("oom_fallback") == 1
+    assert torch.equal(C.rowptr, ref.rowptr) and torch.equal(C.col, ref.col)
+    assert torch.allclose(C.val, ref.val, atol=1e-5, rtol=1e-5)
