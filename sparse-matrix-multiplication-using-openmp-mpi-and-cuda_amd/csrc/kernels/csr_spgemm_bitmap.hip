@@ -1261,7 +1261,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
 // runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
 // wave's own bitmap rows, clear of the same rows, one barrier.
 template <int LGW, int NSUB, int NT, int RR, int CCAP>
-__global__ __launch_bounds__(NT, NSUB == 1 ? 8 : 4) void spgemm_bm_rows_count(BmRowArgs ra) {
+__global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   // (8 waves per SIMD: <= 64 VGPRs)
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
@@ -1480,6 +1480,41 @@ __global__ __launch_bounds__(256) void bm_window_splits(const int64_t* __restric
   ws[t] = (uint32_t)lo;
 }
 
+// ---- operand layout kernels ------------------------------------------------
+// B as interleaved (column, value bits) pairs for the row-major numeric
+// kernel: 4 entries per thread, 16-byte loads and stores.
+__global__ __launch_bounds__(256) void bm_interleave(const int32_t* __restrict__ col, const uint32_t* __restrict__ val,
+                                                    int64_t n, uint2* __restrict__ cv) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 3 < n && ((reinterpret_cast<uintptr_t>(col + i) | reinterpret_cast<uintptr_t>(val + i)) & 15) == 0) {
+    const int4 c = *reinterpret_cast<const int4*>(col + i);
+    const uint4 v = *reinterpret_cast<const uint4*>(val + i);
+    reinterpret_cast<uint4*>(cv + i)[0] = make_uint4((uint32_t)c.x, v.x, (uint32_t)c.y, v.y);
+    reinterpret_cast<uint4*>(cv + i)[1] = make_uint4((uint32_t)c.z, v.z, (uint32_t)c.w, v.w);
+    return;
+  }
+  for (int64_t k = i; k < i + 4 && k < n; ++k) cv[k] = make_uint2((uint32_t)col[k], val[k]);
+}
+
+// The all-gathered right operand of a row-block SpGEMM (rank r's block of
+// the gathered buffer = [columns | value bits], each padded to emax) ->
+// contiguous columns, values and interleaved pairs in one pass (replaces two
+// concatenations and an interleave copy).  base[r] = first output index of
+// rank r, base[world] = total.
+__global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __restrict__ g, int64_t emax,
+                                                         const int64_t* __restrict__ base, int32_t* __restrict__ col,
+                                                         uint32_t* __restrict__ val, uint2* __restrict__ cv) {
+  const int r = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b0 = base[r], n = base[r + 1] - b0;
+  if (i >= n) return;
+  const uint32_t* src = g + (int64_t)r * 2 * emax;
+  const uint32_t c = src[i], v = src[emax + i];
+  col[b0 + i] = (int32_t)c;
+  val[b0 + i] = v;
+  cv[b0 + i] = make_uint2(c, v);
+}
+
 // ---- configurations -------------------------------------------------------
 // Every fast kernel: 256 threads and <= 40 KB of LDS, so four workgroups
 // (16 waves, 128 VGPRs each) share a CU; count and reload kernels take most
@@ -1540,14 +1575,14 @@ struct BmRowKernel {
 };
 
 template <typename Kern>
-int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s) {
+int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastNT) {
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kFastNT, 0) != hipSuccess || per <= 0) per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, nt, 0) != hipSuccess || per <= 0) per = 1;
   int64_t g = (int64_t)per * ncu;
   if (ra.a.m < g) g = ra.a.m;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(kFastNT), 0, s, ra);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(nt), 0, s, ra);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -1557,14 +1592,19 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s) {
 #ifndef SPMM_BM_COUNT_RR   // B loads in flight per thread (diagnostic builds: tools/bm_variants.py)
 #define SPMM_BM_COUNT_RR 8
 #endif
+#ifndef SPMM_BM_COUNT_NT   // threads per count workgroup (the host gates A rows <= this)
+#define SPMM_BM_COUNT_NT 256
+#endif
+constexpr int kCountNT = SPMM_BM_COUNT_NT;
 template <int C, int NSUB>
 struct BmRowCountKernel {
-  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kFastNT, SPMM_BM_COUNT_RR, 256>;
+  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kCountNT, SPMM_BM_COUNT_RR, 256>;
 };
 
 template <int C>
 int bm_count_rows(const BmRowArgs& ra, int nsub, hipStream_t s) {
-  return nsub == 2 ? launch_rows(BmRowCountKernel<C, 2>::k, ra, s) : launch_rows(BmRowCountKernel<C, 1>::k, ra, s);
+  return nsub == 2 ? launch_rows(BmRowCountKernel<C, 2>::k, ra, s, kCountNT)
+                   : launch_rows(BmRowCountKernel<C, 1>::k, ra, s, kCountNT);
 }
 
 template <int C>
@@ -1721,4 +1761,26 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
     case 1: return bm_count_rows<1>(ra, nsub, s);
     default: return bm_count_rows<2>(ra, nsub, s);
   }
+}
+
+// Interleaved (column, value bits) copy of B for the row-major numeric kernel.
+SPMM_EXPORT int spmm_spgemm_bm_interleave(const int32_t* col, const float* val, int64_t n, void* cv, void* stream) {
+  if (n <= 0) return 0;
+  const int64_t th = (n + 3) / 4;
+  hipLaunchKernelGGL(bm_interleave, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, (hipStream_t)stream, col,
+                     (const uint32_t*)val, n, (uint2*)cv);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Unpack an all-gathered operand payload (world blocks of [emax columns |
+// emax value bits]; base: device int64[world + 1] output offsets).
+SPMM_EXPORT int spmm_spgemm_bm_unpack_gathered(const void* g, int world, int64_t emax, const int64_t* base,
+                                               int64_t max_n, int32_t* col, float* val, void* cv, void* stream) {
+  if (world <= 0 || max_n <= 0) return 0;
+  if (world > 65535 || (max_n + 255) / 256 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bm_unpack_gathered, dim3((unsigned)((max_n + 255) / 256), (unsigned)world), dim3(256), 0,
+                     (hipStream_t)stream, (const uint32_t*)g, emax, base, col, (uint32_t*)val, (uint2*)cv);
+  SPMM_LAUNCH_CHECK();
+  return 0;
 }

@@ -28,6 +28,7 @@ large relative to C (deep inner dimension, few products per output).
 """
 from __future__ import annotations
 
+import itertools
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Tuple
 
@@ -147,7 +148,25 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
     meta_B = CSR(m, panel.n, rowptr, empty_c, torch.empty(0, dtype=torch.float32, device=panel.device))
 
     def ready() -> CSR:
-        Gv = payload().to(panel.device).view(comm.world, 2 * emax)
+        G = payload()
+        if G.device.type == "cuda":
+            # one native pass: columns, values and the interleaved pairs of the
+            # bitmap kernel straight out of the padded gather buffer
+            from ..ops.spgemm import _native as _nat
+
+            nnz = sum(nnzs)
+            base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=G.device)
+            col = torch.empty(nnz, dtype=torch.int32, device=G.device)
+            val = torch.empty(nnz, dtype=torch.float32, device=G.device)
+            cv = torch.empty((nnz, 2), dtype=torch.int32, device=G.device)
+            _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(_nat.ptr(G), comm.world, emax, _nat.ptr(base),
+                                                                  max(nnzs), _nat.ptr(col), _nat.ptr(val),
+                                                                  _nat.ptr(cv), _nat.stream_ptr(G.device)),
+                       "spgemm_bm_unpack_gathered")
+            B = CSR(m, panel.n, rowptr, col, val)
+            B._bcv = cv
+            return B
+        Gv = G.to(panel.device).view(comm.world, 2 * emax)
         col = torch.cat([Gv[r, :nnzs[r]] for r in W])
         val = torch.cat([Gv[r, emax:emax + nnzs[r]] for r in W]).view(torch.float32)
         return CSR(m, panel.n, rowptr, col, val)

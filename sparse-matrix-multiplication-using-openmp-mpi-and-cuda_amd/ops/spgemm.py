@@ -60,6 +60,8 @@ _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp,
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
                      C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
@@ -503,6 +505,20 @@ _BM_CFGS = {}
 BM_FILL = 0.7              # mean products per window <= BM_FILL * fast capacity
 
 
+def interleaved(B: CSR) -> torch.Tensor:
+    """B as [nnz, 2] int32 (column, value bits) pairs: the operand of the
+    row-major bitmap numeric kernel.  A distributed gather produces it while
+    unpacking (``B._bcv``); otherwise one native 16-byte-vector copy."""
+    cv = getattr(B, "_bcv", None)
+    if cv is not None and cv.shape[0] == B.nnz:
+        return cv
+    cv = torch.empty((B.nnz, 2), dtype=torch.int32, device=B.device)
+    _native.check(_native.hip().spmm_spgemm_bm_interleave(_native.ptr(B.col), _native.ptr(B.val), B.nnz,
+                                                           _native.ptr(cv), _native.stream_ptr(B.device)),
+                  "spgemm_bm_interleave")
+    return cv
+
+
 def _bm_config(cfg: int):
     """(log2 window, windows per count unit, fast-kernel product capacity,
     register rounds, longest stageable A row) of bitmap configuration ``cfg``."""
@@ -620,7 +636,7 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         pipe = rows_mode == "pipe" and nwin >= 4 and lg_num <= 5 and B.nnz < (1 << 27)
         # the row-major kernel reads B as interleaved (column, value) pairs: one
         # 8-byte stream per chunk instead of two 4-byte ones (fewer partial lines)
-        Bcv = None if pipe or not CONFIG.spgemm_bitmap_cv else torch.stack([B.col, B.val.view(torch.int32)], 1)
+        Bcv = None if pipe or not CONFIG.spgemm_bitmap_cv else interleaved(B)
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
                                                       lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
