@@ -1496,23 +1496,28 @@ __global__ __launch_bounds__(256) void bm_interleave(const int32_t* __restrict__
   for (int64_t k = i; k < i + 4 && k < n; ++k) cv[k] = make_uint2((uint32_t)col[k], val[k]);
 }
 
-// The all-gathered right operand of a row-block SpGEMM (rank r's block of
-// the gathered buffer = [columns | value bits], each padded to emax) ->
-// contiguous columns, values and interleaved pairs in one pass (replaces two
-// concatenations and an interleave copy).  base[r] = first output index of
-// rank r, base[world] = total.
-__global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __restrict__ g, int64_t emax,
-                                                         const int64_t* __restrict__ base, int32_t* __restrict__ col,
-                                                         uint32_t* __restrict__ val, uint2* __restrict__ cv) {
+// The all-gathered right operand of a row-block SpGEMM -> contiguous arrays
+// in one pass (replaces concatenations and an interleave copy).  Rank r's
+// columns are gc[r * gstride + i] and its value bits gv[r * gstride + i],
+// i < base[r + 1] - base[r] (base[r] = first output index of rank r).  Any of
+// col / val / cv may be null; with gc null the columns are read back from
+// col (already unpacked: the two-stage gather, columns first).
+__global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __restrict__ gc, const uint32_t* __restrict__ gv,
+                                                         int64_t gstride, const int64_t* __restrict__ base,
+                                                         int32_t* __restrict__ col, uint32_t* __restrict__ val,
+                                                         uint2* __restrict__ cv) {
   const int r = blockIdx.y;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t b0 = base[r], n = base[r + 1] - b0;
   if (i >= n) return;
-  const uint32_t* src = g + (int64_t)r * 2 * emax;
-  const uint32_t c = src[i], v = src[emax + i];
-  col[b0 + i] = (int32_t)c;
-  val[b0 + i] = v;
-  cv[b0 + i] = make_uint2(c, v);
+  const int64_t src = (int64_t)r * gstride + i;
+  const uint32_t c = gc ? gc[src] : (uint32_t)col[b0 + i];
+  if (gc && col) col[b0 + i] = (int32_t)c;
+  if (gv) {
+    const uint32_t v = gv[src];
+    if (val) val[b0 + i] = v;
+    if (cv) cv[b0 + i] = make_uint2(c, v);
+  }
 }
 
 // ---- configurations -------------------------------------------------------
@@ -1773,14 +1778,18 @@ SPMM_EXPORT int spmm_spgemm_bm_interleave(const int32_t* col, const float* val, 
   return 0;
 }
 
-// Unpack an all-gathered operand payload (world blocks of [emax columns |
-// emax value bits]; base: device int64[world + 1] output offsets).
-SPMM_EXPORT int spmm_spgemm_bm_unpack_gathered(const void* g, int world, int64_t emax, const int64_t* base,
-                                               int64_t max_n, int32_t* col, float* val, void* cv, void* stream) {
+// Unpack an all-gathered operand payload: rank r's columns at gc + r *
+// gstride, its value bits at gv + r * gstride (either may be null, see the
+// kernel); base: device int64[world + 1] output offsets.
+SPMM_EXPORT int spmm_spgemm_bm_unpack_gathered(const void* gc, const void* gv, int world, int64_t gstride,
+                                               const int64_t* base, int64_t max_n, int32_t* col, float* val, void* cv,
+                                               void* stream) {
   if (world <= 0 || max_n <= 0) return 0;
   if (world > 65535 || (max_n + 255) / 256 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  if (!gc && !col) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bm_unpack_gathered, dim3((unsigned)((max_n + 255) / 256), (unsigned)world), dim3(256), 0,
-                     (hipStream_t)stream, (const uint32_t*)g, emax, base, col, (uint32_t*)val, (uint2*)cv);
+                     (hipStream_t)stream, (const uint32_t*)gc, (const uint32_t*)gv, gstride, base, col,
+                     (uint32_t*)val, (uint2*)cv);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -108,24 +108,44 @@ def _allgather_async(comm: Comm, t: torch.Tensor):
     return finish_gloo
 
 
+class OperandReady:
+    """``ready()`` of :func:`allgather_operand_async`: the full right operand.
+    ``cols()`` returns it with columns only (values empty) as soon as the
+    first of the two payload collectives has landed: the SpGEMM's window
+    splits and count kernel read only B's columns, so they run while the
+    values are still crossing xGMI."""
+
+    def __init__(self, full: Callable[[], CSR], cols: Optional[Callable[[], CSR]] = None):
+        self._full, self._cols = full, cols
+
+    def __call__(self) -> CSR:
+        return self._full()
+
+    def cols(self) -> CSR:
+        return self._cols() if self._cols is not None else self._full()
+
+
 def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], CSR]]:
-    """Right operand of the row-block SpGEMM (every rank's B row panel), in two
+    """Right operand of the row-block SpGEMM (every rank's B row panel), in
     stages so the gather overlaps the SpGEMM's setup.
 
     1. sizes, then the row counts of every panel (small collectives): B's row
        pointer is complete, which is all the product-count / binning / memory
        planning phase of ``spgemm`` reads;
-    2. columns and values of every panel in ONE packed collective (each rank
-       contributes [cols | value bits] as int32 of a common size), started
-       asynchronously: RCCL moves the ~0.9 GB of the 1M config over the xGMI
-       ring while the compute stream runs the per-row product counts.
+    2. RCCL: the columns, then the value bits, as two collectives started
+       asynchronously (they run in issue order): the row plan overlaps the
+       columns, the window splits and count kernel (columns only) overlap the
+       values; each lands in a padded [world, emax] buffer and one native pass
+       unpacks it (the values together with the interleaved (column, value)
+       pairs of the bitmap kernel).  gloo: one packed [cols | values]
+       collective and host-side concatenation.
 
-    Returns (B with row pointer only, ready) where ``ready()`` makes the
-    current stream wait for the payload and returns the full CSR (panels'
-    columns and values packed back-to-back: two device copies, ~0.4 ms).
+    Returns (B with row pointer only, ready): ``ready()`` makes the current
+    stream wait for the payload and returns the full CSR; ``ready.cols()``
+    the columns-only operand (see :class:`OperandReady`).
     """
     if not comm.is_dist:
-        return panel, lambda: panel
+        return panel, OperandReady(lambda: panel)
     wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
     meta = _allgather_equal(comm, torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)).view(-1, 2)
     ms, nnzs = meta[:, 0].tolist(), meta[:, 1].tolist()
@@ -133,44 +153,67 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
     W = range(comm.world)
     cbuf = torch.zeros(mmax, dtype=torch.int64, device=wd)
     cbuf[:panel.m] = (panel.rowptr[1:] - panel.rowptr[:-1]).to(wd)
-    buf = torch.zeros(2 * emax, dtype=torch.int32, device=wd)
-    buf[:panel.nnz] = panel.col.to(wd)
-    buf[emax:emax + panel.nnz] = panel.val.float().to(wd).view(torch.int32)
     # counts first: collectives of one group run in issue order, so the small
     # one must not queue behind the payload
     cnt = _allgather_equal(comm, cbuf).to(panel.device).view(comm.world, mmax)
-    payload = _allgather_async(comm, buf)
     counts = cnt.reshape(-1) if all(x == mmax for x in ms) else torch.cat([cnt[r, :ms[r]] for r in W])
     m = sum(ms)
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=panel.device)
     torch.cumsum(counts, 0, out=rowptr[1:])
     empty_c = torch.empty(0, dtype=torch.int32, device=panel.device)
-    meta_B = CSR(m, panel.n, rowptr, empty_c, torch.empty(0, dtype=torch.float32, device=panel.device))
+    empty_v = torch.empty(0, dtype=torch.float32, device=panel.device)
+    meta_B = CSR(m, panel.n, rowptr, empty_c, empty_v)
+    nnz = sum(nnzs)
+
+    if comm.backend == "nccl":
+        from ..ops.spgemm import _native as _nat
+
+        dev = panel.device
+        cb = torch.zeros(emax, dtype=torch.int32, device=dev)
+        cb[:panel.nnz] = panel.col
+        vb = torch.zeros(emax, dtype=torch.int32, device=dev)
+        vb[:panel.nnz] = panel.val.float().view(torch.int32)
+        pay_c = _allgather_async(comm, cb)
+        pay_v = _allgather_async(comm, vb)
+        base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=dev)
+        got = {}
+
+        def unpack(gc, gv, col, val, cv):
+            _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(
+                _nat.ptr(gc) if gc is not None else None, _nat.ptr(gv) if gv is not None else None, comm.world,
+                emax, _nat.ptr(base), max(nnzs), _nat.ptr(col), _nat.ptr(val) if val is not None else None,
+                _nat.ptr(cv) if cv is not None else None, _nat.stream_ptr(dev)), "spgemm_bm_unpack_gathered")
+
+        def cols() -> CSR:
+            if "col" not in got:
+                col = torch.empty(nnz, dtype=torch.int32, device=dev)
+                unpack(pay_c(), None, col, None, None)
+                got["col"] = col
+            return CSR(m, panel.n, rowptr, got["col"], empty_v)
+
+        def full() -> CSR:
+            if "B" not in got:
+                col = cols().col
+                val = torch.empty(nnz, dtype=torch.float32, device=dev)
+                cv = torch.empty((nnz, 2), dtype=torch.int32, device=dev)
+                unpack(None, pay_v(), col, val, cv)
+                B = CSR(m, panel.n, rowptr, col, val)
+                B._bcv = cv
+                got["B"] = B
+            return got["B"]
+        return meta_B, OperandReady(full, cols)
+
+    buf = torch.zeros(2 * emax, dtype=torch.int32, device=wd)
+    buf[:panel.nnz] = panel.col.to(wd)
+    buf[emax:emax + panel.nnz] = panel.val.float().to(wd).view(torch.int32)
+    payload = _allgather_async(comm, buf)
 
     def ready() -> CSR:
-        G = payload()
-        if G.device.type == "cuda":
-            # one native pass: columns, values and the interleaved pairs of the
-            # bitmap kernel straight out of the padded gather buffer
-            from ..ops.spgemm import _native as _nat
-
-            nnz = sum(nnzs)
-            base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=G.device)
-            col = torch.empty(nnz, dtype=torch.int32, device=G.device)
-            val = torch.empty(nnz, dtype=torch.float32, device=G.device)
-            cv = torch.empty((nnz, 2), dtype=torch.int32, device=G.device)
-            _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(_nat.ptr(G), comm.world, emax, _nat.ptr(base),
-                                                                  max(nnzs), _nat.ptr(col), _nat.ptr(val),
-                                                                  _nat.ptr(cv), _nat.stream_ptr(G.device)),
-                       "spgemm_bm_unpack_gathered")
-            B = CSR(m, panel.n, rowptr, col, val)
-            B._bcv = cv
-            return B
-        Gv = G.to(panel.device).view(comm.world, 2 * emax)
+        Gv = payload().to(panel.device).view(comm.world, 2 * emax)
         col = torch.cat([Gv[r, :nnzs[r]] for r in W])
         val = torch.cat([Gv[r, emax:emax + nnzs[r]] for r in W]).view(torch.float32)
         return CSR(m, panel.n, rowptr, col, val)
-    return meta_B, ready
+    return meta_B, OperandReady(ready)
 
 
 def allgather_operand(panel: CSR, comm: Comm) -> CSR:

@@ -61,7 +61,8 @@ _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_v
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp,
+                     c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
                      C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
@@ -346,6 +347,8 @@ def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None) -> CSR:
             if not cached:
                 cached.append(fetch())
             return cached[0]
+        # the columns-only stage of a two-stage gather (see models.spgemm.OperandReady)
+        B_ready.cols = getattr(fetch, "cols", B_ready)
     if _bitmap_ok(A, B, info.flops // 2, pre):
         C_ = onepass_bitmap(A, B, info, B_ready, pre)
         if C_ is not None:
@@ -582,8 +585,8 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     nwin = max(1, -(-B.n // (1 << lgw)))
     if m * nwin >= (1 << 31):
         return None
-    if B_ready is not None:
-        B = B_ready()
+    if B_ready is not None:   # columns only: the values may still be in flight (two-stage gather)
+        B = getattr(B_ready, "cols", B_ready)()
     lib = _native.hip()
     P = _native.ptr
     st = _native.stream_ptr(dev)
@@ -626,6 +629,8 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         if count_rows:
             uoff, (nnz, e0) = count(False)
     del ucnt
+    if B_ready is not None:   # the numeric kernels read the values
+        B = B_ready()
     err.zero_()
     info.nnz = nnz
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)

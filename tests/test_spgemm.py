@@ -334,11 +334,16 @@ def test_rowblock_spgemm_rccl_one_rank(monkeypatch):
     comm = CM.init(backend="nccl", device="cuda")
     try:
         assert comm.is_dist and comm.backend == "nccl"
-        prob = MS.UniformProblem.build(50000, 4e-4, comm, seed=5)
-        C1 = MS.rowblock_spgemm(prob.A, prob.B, comm)
-        C2 = SG.spgemm(prob.A, prob.B)
-        assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
-        assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+        for n, d in ((50000, 4e-4), (65536, 1e-3)):
+            prob = MS.UniformProblem.build(n, d, comm, seed=5)
+            info = SG.SpgemmInfo()
+            C1 = MS.rowblock_spgemm(prob.A, prob.B, comm, info)
+            C2 = SG.spgemm(prob.A, prob.B)
+            assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+            assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+        # the second one ran the bitmap kernels on the two-stage gather (columns
+        # unpacked first for the count kernel, values + pairs before the numeric)
+        assert "bitmap_units" in info.rows_per_bin_num
     finally:
         comm.close()
 
