@@ -19,7 +19,9 @@ Extra options (all optional; env equivalents SPMM_*):
   --format ref|mtx    input format (default ref: the reference folder format)
   --out PATH          output file (default ./matrix, ./matrix.mtx for mtx)
   --device cuda|cpu   compute device (default: cuda when present)
-  --comm nccl|gloo    process-group backend (default: nccl on GPU, gloo on CPU)
+  --comm nccl|gloo|loopback
+                      process-group backend (default: nccl on GPU, gloo on CPU);
+                      loopback runs --ranks P ranks as threads of this process
   --threads N         host parser/writer threads (default: all)
   --quiet             suppress the "multiplying" lines
   --metrics-json PATH per-rank phase times, bytes moved and throughput
@@ -47,6 +49,8 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default=os.environ.get("SPMM_DEVICE", "auto"))
     ap.add_argument("--comm", default=os.environ.get("SPMM_COMM", "auto"))
     ap.add_argument("--threads", type=int, default=int(os.environ.get("SPMM_THREADS", "0")))
+    ap.add_argument("--ranks", type=int, default=int(os.environ.get("SPMM_RANKS", "1")),
+                    help="--comm loopback: in-process ranks")
     ap.add_argument("--quiet", action="store_true", default=bool(os.environ.get("SPMM_QUIET")))
     ap.add_argument("--metrics-json", default=os.environ.get("SPMM_METRICS_JSON"))
     ap.add_argument("--no-split", action="store_true", default=bool(os.environ.get("SPMM_NO_SPLIT")))
@@ -64,6 +68,8 @@ def main(argv=None) -> int:
 
     if args.format == "mtx":
         return _main_mtx(args, t_start)
+    if args.comm == "loopback":
+        return _main_loopback(args, t_start)
 
     from ..models.chain import ChainStats, run_chain
     from ..parallel import comm as commmod
@@ -94,6 +100,35 @@ def main(argv=None) -> int:
         with open(path, "w") as f:
             json.dump(rec, f, indent=1)
     return rc
+
+
+def _main_loopback(args, t_start: float) -> int:
+    """P ranks as threads of this process (parallel/loopback.py): the same
+    chain split, cross-rank tree and output as P processes."""
+    import torch
+
+    from ..models.chain import ChainStats, run_chain
+    from ..parallel.loopback import run_loopback
+    from ..utils import refio
+
+    dev = args.device if args.device != "auto" else ("cuda" if torch.cuda.is_available() else "cpu")
+    log = None if args.quiet else (lambda s: print(s, flush=True))
+
+    def rank_main(comm):
+        st = ChainStats()
+        run_chain(args.folder, comm, out_path=args.out, log=log, nthreads=args.threads, stats=st,
+                  split=not args.no_split, fast=args.fast)
+        return st
+
+    try:
+        run_loopback(max(1, args.ranks), rank_main, device=dev)
+    except refio.FormatError as e:
+        print(str(e), file=sys.stderr)
+        return 1
+    elapsed = time.perf_counter() - t_start
+    for _ in range(max(1, args.ranks)):   # one line per rank, as P processes print
+        print(f"time taken {elapsed} seconds", flush=True)
+    return 0
 
 
 def _mtx_paths(inputs):
