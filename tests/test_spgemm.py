@@ -211,9 +211,13 @@ def test_spgemm_gpu_rmat_aat():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("brow,bcols", [(60, 200000), (100, 200000), (100, 40000)])
-def test_spgemm_gpu_column_sliced_bins(brow, bcols):
+def test_spgemm_gpu_column_sliced_bins(monkeypatch, brow, bcols):
     """Rows long enough for the 2- and 4-slice LDS passes (and the overflow
-    hand-off to the HBM path) must match the CPU result exactly in structure."""
+    hand-off to the HBM path) must match the CPU result exactly in structure.
+    (The bitmap path, which would take the uniform rows, is switched off.)"""
+    from spmm_amd.utils.config import CONFIG
+
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap", "off")
     dev = torch.device("cuda")
     A = gen_csr.uniform_csr(300, 2000, 0.1, seed=5)
     B = gen_csr.uniform_csr(2000, bcols, brow / bcols, seed=6)
