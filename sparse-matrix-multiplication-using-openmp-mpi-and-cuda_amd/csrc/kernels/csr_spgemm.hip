@@ -955,6 +955,7 @@ __global__ __launch_bounds__(256) void spgemm_row_splits(const int64_t* __restri
 
 // One-pass mode: rows were written at their product-count offsets (src_off);
 // copy each row's n[i] entries to the final CSR (dst_off).  One wave per row.
+// src_off < 0: the row is placed by another kernel (long rows, long_place).
 __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict__ src_off,
                                                       const int64_t* __restrict__ dst_off, int64_t m,
                                                       const int32_t* __restrict__ sci, const float* __restrict__ sv,
@@ -963,6 +964,7 @@ __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict_
   const int lane = threadIdx.x & 63;
   if (row >= m) return;
   const int64_t s0 = src_off[row], d0 = dst_off[row], n = dst_off[row + 1] - d0;
+  if (s0 < 0) return;
   int64_t i = lane;
   for (; i + 192 < n; i += 256) {   // 4 loads in flight per lane
     const int c0 = sci[s0 + i], c1 = sci[s0 + i + 64], c2 = sci[s0 + i + 128], c3 = sci[s0 + i + 192];
@@ -999,8 +1001,15 @@ __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict_
 constexpr int LONG_NT = 512;
 constexpr int LONG_EPW = SPMM_LONG_EPW; // A entries per routing workgroup
 constexpr int LONG_DL = SPMM_LONG_DLOADS;   // scratch loads in flight per lane (long_dense)
-constexpr int LONG_LGW = 14;            // W = 16384 columns per chunk
+#ifndef SPMM_LONG_XCD
+#define SPMM_LONG_XCD 1
+#endif
+#ifndef SPMM_LONG_LGW
+#define SPMM_LONG_LGW 15
+#endif
+constexpr int LONG_LGW = SPMM_LONG_LGW; // W = 32768 columns per chunk (2^14: 3 % slower at R-MAT 24)
 constexpr int LONG_W = 1 << LONG_LGW;
+constexpr int LONG_DNT = LONG_W / 32;  // long_dense: one occupancy word per thread
 constexpr int LONG_MAXCH = 4096;        // chunks per row (ncols <= 2^26)
 
 template <bool SCATTER>
@@ -1012,7 +1021,14 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
   __shared__ unsigned long long cur[SCATTER ? LONG_MAXCH : 1];
   __shared__ int hist[SCATTER ? 1 : LONG_MAXCH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // Neighbouring workgroups own neighbouring scratch runs of every chunk, so
+  // they share cache lines: give them one XCD (one L2) so the partial lines
+  // merge there instead of reaching the fabric as masked partial writes.
+#if SPMM_LONG_XCD
+  const int64_t wg = spmm::xcd_remap(blockIdx.x, gridDim.x);
+#else
   const int64_t wg = blockIdx.x;
+#endif
   for (int t = tid; t < nch; t += LONG_NT) {
     if constexpr (SCATTER) cur[t] = (unsigned long long)wg_base[wg * nch + t];
     else hist[t] = 0;
@@ -1085,19 +1101,19 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x) {
 // permutes, empty items cost nothing, and the next item's counts and first
 // scratch loads are in flight during the current write-back.
 template <bool VALUES>
-__global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restrict__ rt_off,
+__global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int64_t* __restrict__ rt_off,
                                                          const int64_t* __restrict__ rt_cnt, int64_t nrt, int nch,
                                                          unsigned long long* __restrict__ scratch,
                                                          int64_t* __restrict__ rt_nnz, int64_t small) {
   __shared__ float vals[VALUES ? LONG_W : 1];
   __shared__ uint32_t bits[LONG_W / 32];
-  __shared__ int wsum[LONG_NT / 64];
-  static_assert(LONG_W / 32 == LONG_NT, "one occupancy word per thread");
-  constexpr int NW = LONG_NT / 64;
+  __shared__ int wsum[LONG_DNT / 64];
+  static_assert(LONG_W / 32 == LONG_DNT, "one occupancy word per thread");
+  constexpr int NW = LONG_DNT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   bits[tid] = 0u;
   if constexpr (VALUES)
-    for (int i = tid; i < LONG_W / 4; i += LONG_NT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = tid; i < LONG_W / 4; i += LONG_DNT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   // items of <= small products belong to long_rank (it runs first and writes their counts)
   auto count_of = [&](int64_t r) { const int64_t c = rt_cnt[r]; return c <= small ? int64_t(0) : c; };
   int64_t rt = blockIdx.x;
@@ -1106,7 +1122,7 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
   unsigned long long x[LONG_DL];
 #pragma unroll
   for (int u = 0; u < LONG_DL; ++u) {
-    const int64_t i = tid + u * LONG_NT;
+    const int64_t i = tid + u * LONG_DNT;
     x[u] = i < n ? scratch[base + i] : ~0ull;
   }
   __syncthreads();
@@ -1119,7 +1135,7 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
       if (rt < nrt) { n = count_of(rt); base = rt_off[rt]; }
 #pragma unroll
       for (int u = 0; u < LONG_DL; ++u) {
-        const int64_t i = tid + u * LONG_NT;
+        const int64_t i = tid + u * LONG_DNT;
         x[u] = i < n ? scratch[base + i] : ~0ull;
       }
       continue;
@@ -1133,12 +1149,12 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
         atomicOr(&bits[c >> 5], 1u << (c & 31));
         if constexpr (VALUES) atomicAdd(&vals[c], __uint_as_float((uint32_t)(x[u] >> 32)));
       }
-      i0 += LONG_DL * LONG_NT;
+      i0 += LONG_DL * LONG_DNT;
       if (i0 >= n) break;
       // LONG_DL scratch loads in flight per lane before the LDS updates
 #pragma unroll
       for (int u = 0; u < LONG_DL; ++u) {
-        const int64_t i = i0 + u * LONG_NT;
+        const int64_t i = i0 + u * LONG_DNT;
         x[u] = i < n ? scratch[base + i] : ~0ull;
       }
     }
@@ -1172,7 +1188,7 @@ __global__ __launch_bounds__(LONG_NT, 2) void long_dense(const int64_t* __restri
     if (tid == 0) rt_nnz[rt] = total;
 #pragma unroll
     for (int u = 0; u < LONG_DL; ++u) {
-      const int64_t i = tid + u * LONG_NT;
+      const int64_t i = tid + u * LONG_DNT;
       x[u] = i < n2 ? scratch[base2 + i] : ~0ull;
     }
     rt = rt2; n = n2; base = base2;
@@ -1634,12 +1650,16 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
                          (unsigned long long*)scratch, rt_nnz);
     SPMM_LAUNCH_CHECK();
   }
-  const unsigned grid = (unsigned)std::min<int64_t>(nrt, (values ? 2 : 4) * (int64_t)ncu);
+  int per = 0;   // resident workgroups per CU (LDS-bound with values: 66 KB at W = 2^14)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, values ? long_dense<true> : long_dense<false>, LONG_DNT, 0) !=
+          hipSuccess || per <= 0)
+    per = values ? 2 : 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(nrt, (int64_t)per * ncu);
   if (values)
-    hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nrt, nch,
+    hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_DNT), 0, s, rt_off, rt_cnt, nrt, nch,
                        (unsigned long long*)scratch, rt_nnz, small);
   else
-    hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_NT), 0, s, rt_off, rt_cnt, nrt, nch,
+    hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_DNT), 0, s, rt_off, rt_cnt, nrt, nch,
                        (unsigned long long*)scratch, rt_nnz, small);
   SPMM_LAUNCH_CHECK();
   return 0;

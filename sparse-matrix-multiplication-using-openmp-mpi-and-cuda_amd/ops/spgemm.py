@@ -215,12 +215,17 @@ def _long_params():
 
 def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torch.Tensor, stream,
                out_nnz: Optional[torch.Tensor] = None, Crp=None, Cci=None, Cv=None,
-               expect_nnz: Optional[torch.Tensor] = None) -> None:
+               expect_nnz: Optional[torch.Tensor] = None, defer: Optional[list] = None) -> None:
     """Rows beyond the LDS bins: column-chunked dense accumulation through an
     HBM scratch (csr_spgemm.hip "long rows").  ``values=0`` only counts
     (writes ``out_nnz[rows]``); ``values=1`` also writes each row at
     ``Crp[row]`` (and its count to ``out_nnz`` when given).  Rows are
-    processed in batches whose products fit the scratch budget."""
+    processed in batches whose products fit the scratch budget.
+
+    ``defer``: instead of placing the rows at ``Crp``, append each batch's
+    ``(rows, rt_off, rt_nnz, scratch)`` (chunk results still in the scratch)
+    so the caller places them at final offsets once those are known
+    (``place_long``): the pipelined one-pass skips a staging round trip."""
     dev = A.device
     lib = _native.hip()
     P = _native.ptr
@@ -280,13 +285,28 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
             raise RuntimeError("spgemm long rows: numeric count differs from the symbolic count")
         if out_nnz is not None:
             out_nnz[rb] = nnz_r.to(out_nnz.dtype)
-        if values:
+        if values and defer is not None:
+            defer.append((rb, rt_off, rt_nnz, scratch))
+        elif values:
             dst = (Crp[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
             _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
                                                      P(Cv), stream), "long_place")
         del scratch
         done = int(csum[end - 1])
         start = end
+
+
+def place_long(defer: list, rowptr: torch.Tensor, Cci: torch.Tensor, Cv: torch.Tensor, stream) -> None:
+    """Copy deferred long-row results (``_long_rows(..., defer=)``) from their
+    scratch to the final CSR rows at ``rowptr`` (on ``stream``; the caller
+    keeps the scratch alive until that stream passes this point)."""
+    lib = _native.hip()
+    P = _native.ptr
+    for rb, rt_off, rt_nnz, scratch in defer:
+        nnz_rt = rt_nnz.view(rb.numel(), -1)
+        dst = (rowptr[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
+        _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), rt_nnz.numel(), P(scratch), P(Cci),
+                                                 P(Cv), stream), "long_place")
 
 
 def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> CSR:
@@ -753,10 +773,13 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
         if spill.numel():
             info.rows_per_bin_num["lds_overflow"] = info.rows_per_bin_num.get("lds_overflow", 0) + int(spill.numel())
             long_rows.append((spill + lo).to(torch.int32))
+        deferred = []
         if long_rows:
+            # hub rows stay in their chunk scratch and go straight to C once
+            # the chunk's row pointer exists (the compaction skips them)
             rows = torch.cat(long_rows)
-            _long_rows(1, A, B, rows, nprod[rows.long()], sA.cuda_stream, out_nnz=out_nnz, Crp=ub_rel, Cci=sci,
-                       Cv=sv)
+            _long_rows(1, A, B, rows, nprod[rows.long()], sA.cuda_stream, out_nnz=out_nnz, defer=deferred)
+            ub_rel[rows.long()] = -1
         done = torch.cuda.Event()
         done.record(sA)
         with torch.cuda.stream(sB):
@@ -765,6 +788,11 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
             rowptr[lo + 1:hi + 1] += rowptr[lo]
             _native.check(lib.spmm_spgemm_compact(P(ub_rel) + 8 * lo, P(rowptr) + 8 * lo, hi - lo, P(sci), P(sv),
                                                   P(Cci), P(Cv), sB.cuda_stream), "spgemm_compact(pipelined)")
+            for d in deferred:   # allocated on sA, last read on sB
+                for t in d:
+                    t.record_stream(sB)
+            place_long(deferred, rowptr, Cci, Cv, sB.cuda_stream)
+            del deferred
             free[c % 2] = torch.cuda.Event()
             free[c % 2].record(sB)
     sA.wait_stream(sB)
