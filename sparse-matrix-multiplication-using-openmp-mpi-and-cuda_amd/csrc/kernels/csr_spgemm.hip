@@ -1101,10 +1101,12 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x) {
 // permutes, empty items cost nothing, and the next item's counts and first
 // scratch loads are in flight during the current write-back.
 template <bool VALUES>
-__global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int64_t* __restrict__ rt_off,
-                                                         const int64_t* __restrict__ rt_cnt, int64_t nrt, int nch,
+__global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restrict__ list,
+                                                         const int32_t* __restrict__ nlist,
+                                                         const int64_t* __restrict__ rt_off,
+                                                         const int64_t* __restrict__ rt_cnt, int nch,
                                                          unsigned long long* __restrict__ scratch,
-                                                         int64_t* __restrict__ rt_nnz, int64_t small) {
+                                                         int64_t* __restrict__ rt_nnz) {
   __shared__ float vals[VALUES ? LONG_W : 1];
   __shared__ uint32_t bits[LONG_W / 32];
   __shared__ int wsum[LONG_DNT / 64];
@@ -1114,11 +1116,12 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int64_t* __restr
   bits[tid] = 0u;
   if constexpr (VALUES)
     for (int i = tid; i < LONG_W / 4; i += LONG_DNT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  // items of <= small products belong to long_rank (it runs first and writes their counts)
-  auto count_of = [&](int64_t r) { const int64_t c = rt_cnt[r]; return c <= small ? int64_t(0) : c; };
-  int64_t rt = blockIdx.x;
+  // the items of this kernel (long_partition: more than LR_CAP products)
+  const int64_t nl = *nlist;
+  int64_t it = blockIdx.x;   // position in the list
+  int64_t rt = it < nl ? list[it] : -1;
   int64_t n = 0, base = 0;
-  if (rt < nrt) { n = count_of(rt); base = rt_off[rt]; }
+  if (rt >= 0) { n = rt_cnt[rt]; base = rt_off[rt]; }
   unsigned long long x[LONG_DL];
 #pragma unroll
   for (int u = 0; u < LONG_DL; ++u) {
@@ -1126,20 +1129,9 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int64_t* __restr
     x[u] = i < n ? scratch[base + i] : ~0ull;
   }
   __syncthreads();
-  while (rt < nrt) {
-    const int64_t rt2 = rt + gridDim.x;
-    if (n == 0) {   // uniform over the workgroup: no LDS state touched
-      if (tid == 0 && small < 0) rt_nnz[rt] = 0;
-      rt = rt2;
-      n = 0;
-      if (rt < nrt) { n = count_of(rt); base = rt_off[rt]; }
-#pragma unroll
-      for (int u = 0; u < LONG_DL; ++u) {
-        const int64_t i = tid + u * LONG_DNT;
-        x[u] = i < n ? scratch[base + i] : ~0ull;
-      }
-      continue;
-    }
+  while (it < nl) {
+    const int64_t it2 = it + gridDim.x;
+    const int64_t rt2 = it2 < nl ? list[it2] : -1;   // in flight during the atomics
     const int c0 = (int)(rt % nch) << LONG_LGW;
     for (int64_t i0 = tid;;) {
 #pragma unroll
@@ -1160,7 +1152,7 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int64_t* __restr
     }
     __syncthreads();
     int64_t n2 = 0, base2 = 0;
-    if (rt2 < nrt) { n2 = count_of(rt2); base2 = rt_off[rt2]; }
+    if (rt2 >= 0) { n2 = rt_cnt[rt2]; base2 = rt_off[rt2]; }
     // one occupancy word per thread: its columns in order; the write-back
     // clears what it reads
     const uint32_t word = bits[tid];
@@ -1191,7 +1183,7 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int64_t* __restr
       const int64_t i = tid + u * LONG_DNT;
       x[u] = i < n2 ? scratch[base2 + i] : ~0ull;
     }
-    rt = rt2; n = n2; base = base2;
+    it = it2; rt = rt2; n = n2; base = base2;
     __syncthreads();   // write-back clears and wsum reads done before the next item's atomics / wsum writes
   }
 }
@@ -1221,8 +1213,10 @@ __device__ __forceinline__ void lr_wave_fence() {
 }
 
 template <bool VALUES>
-__global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int64_t* __restrict__ rt_off,
-                                                           const int64_t* __restrict__ rt_cnt, int64_t nrt, int nch,
+__global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int32_t* __restrict__ list,
+                                                           const int32_t* __restrict__ nlist,
+                                                           const int64_t* __restrict__ rt_off,
+                                                           const int64_t* __restrict__ rt_cnt, int nch,
                                                            unsigned long long* __restrict__ scratch,
                                                            int64_t* __restrict__ rt_nnz) {
   __shared__ __attribute__((aligned(16))) unsigned long long bm_all[LR_WAVES][LR_WORDS];
@@ -1238,13 +1232,10 @@ __global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int64_t* __rest
   for (int k = 0; k < LR_WORDS / 64; ++k) bm[k * 64 + lane] = 0ull;
   lr_wave_fence();
   const int64_t nwv = (int64_t)gridDim.x * LR_WAVES;
-  for (int64_t rt = (int64_t)blockIdx.x * LR_WAVES + w; rt < nrt; rt += nwv) {
+  const int64_t nl = *nlist;   // items of 1..LR_CAP products (long_partition)
+  for (int64_t li = (int64_t)blockIdx.x * LR_WAVES + w; li < nl; li += nwv) {
+    const int64_t rt = list[li];
     const int64_t n = rt_cnt[rt];
-    if (n > LR_CAP) continue;   // uniform: long_dense's item
-    if (n == 0) {
-      if (lane == 0) rt_nnz[rt] = 0;
-      continue;
-    }
     const int64_t base = rt_off[rt];
     const uint32_t c0 = (uint32_t)(rt % nch) << LONG_LGW;
     const int nu = (int)((n + 63) >> 6);   // wave-uniform rounds
@@ -1304,6 +1295,34 @@ __global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int64_t* __rest
     for (int k = 0; k < LR_WORDS / 64; ++k) bm[k * 64 + lane] = 0ull;
     lr_wave_fence();
   }
+}
+
+// (row, chunk) items -> the work lists of long_rank (1..small products) and
+// long_dense (more); nl[0], nl[1] = their lengths (zeroed by the caller).
+// Empty items get their zero count here.  The persistent kernels then walk
+// only their own items: a walk over all items costs a dependent count load
+// per skipped item (R-MAT 24: 82 % of the items are long_rank's).
+__global__ __launch_bounds__(256) void long_partition(const int64_t* __restrict__ rt_cnt, int64_t nrt, int64_t small,
+                                                      int32_t* __restrict__ rank_list,
+                                                      int32_t* __restrict__ dense_list, int32_t* __restrict__ nl,
+                                                      int64_t* __restrict__ rt_nnz) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t n = i < nrt ? rt_cnt[i] : 0;
+  if (i < nrt && n == 0) rt_nnz[i] = 0;
+  const bool r = n > 0 && n <= small;
+  const bool d = n > 0 && n > small;
+  const unsigned long long mr = __ballot(r), md = __ballot(d);
+  int br = 0, bd = 0;
+  if (lane == 0) {
+    if (mr) br = atomicAdd(&nl[0], __popcll(mr));
+    if (md) bd = atomicAdd(&nl[1], __popcll(md));
+  }
+  br = __shfl(br, 0);
+  bd = __shfl(bd, 0);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  if (r) rank_list[br + __popcll(mr & below)] = (int32_t)i;
+  if (d) dense_list[bd + __popcll(md & below)] = (int32_t)i;
 }
 
 // chunk results -> final CSR positions (one wave per (row, chunk))
@@ -1621,11 +1640,11 @@ SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const fl
 }
 
 SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_cnt, int64_t nrt, int nch,
-                                       void* scratch, int64_t* rt_nnz, void* stream) {
+                                       void* scratch, int64_t* rt_nnz, int32_t* ws, void* stream) {
+  // ws: 2 * nrt + 2 int32 (the two work lists and their lengths)
   if (nrt <= 0) return 0;
+  if (nrt >= (int64_t(1) << 31)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  // persistent grid: the resident capacity (two 66 KB workgroups per CU with
-  // values, LDS-light count pass: more)
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
@@ -1639,28 +1658,36 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
     const char* e = getenv("SPMM_LONG_RANK");
     return e && e[0] == '0' ? 0 : 1;
   }();
-  const int64_t small = use_rank ? LR_CAP : -1;
+  int32_t* nl = ws;
+  int32_t* rank_list = ws + 2;
+  int32_t* dense_list = ws + 2 + nrt;
+  hipError_t e = hipMemsetAsync(nl, 0, 2 * sizeof(int32_t), s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(long_partition, dim3((unsigned)((nrt + 255) / 256)), dim3(256), 0, s, rt_cnt, nrt,
+                     use_rank ? (int64_t)LR_CAP : int64_t(0), rank_list, dense_list, nl, rt_nnz);
+  SPMM_LAUNCH_CHECK();
+  // persistent grids at the resident capacity (list lengths are device-side)
   if (use_rank) {
     const unsigned rgrid = (unsigned)std::min<int64_t>((nrt + LR_WAVES - 1) / LR_WAVES, (values ? 3 : 8) * (int64_t)ncu);
     if (values)
-      hipLaunchKernelGGL(long_rank<true>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rt_off, rt_cnt, nrt, nch,
+      hipLaunchKernelGGL(long_rank<true>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rank_list, nl, rt_off, rt_cnt, nch,
                          (unsigned long long*)scratch, rt_nnz);
     else
-      hipLaunchKernelGGL(long_rank<false>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rt_off, rt_cnt, nrt, nch,
+      hipLaunchKernelGGL(long_rank<false>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rank_list, nl, rt_off, rt_cnt, nch,
                          (unsigned long long*)scratch, rt_nnz);
     SPMM_LAUNCH_CHECK();
   }
-  int per = 0;   // resident workgroups per CU (LDS-bound with values: 66 KB at W = 2^14)
+  int per = 0;   // resident workgroups per CU (LDS-bound with values: 132 KB at W = 2^15)
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, values ? long_dense<true> : long_dense<false>, LONG_DNT, 0) !=
           hipSuccess || per <= 0)
-    per = values ? 2 : 4;
+    per = 1;
   const unsigned grid = (unsigned)std::min<int64_t>(nrt, (int64_t)per * ncu);
   if (values)
-    hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_DNT), 0, s, rt_off, rt_cnt, nrt, nch,
-                       (unsigned long long*)scratch, rt_nnz, small);
+    hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
+                       (unsigned long long*)scratch, rt_nnz);
   else
-    hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_DNT), 0, s, rt_off, rt_cnt, nrt, nch,
-                       (unsigned long long*)scratch, rt_nnz, small);
+    hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
+                       (unsigned long long*)scratch, rt_nnz);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

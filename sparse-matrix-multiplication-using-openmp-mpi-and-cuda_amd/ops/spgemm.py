@@ -46,7 +46,7 @@ _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_
 _native.register_hip("spmm_spgemm_compact", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, c_vp,
                      c_vp, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
@@ -202,6 +202,18 @@ def _onepass_mode(total_products: int, dev: torch.device, allow_pipeline: bool =
 
 
 _LONG = None
+LONG_STATS: Optional[dict] = None   # diagnostics (tools/long_items.py): item-size histogram of the long-row path
+
+
+def _long_stats(rt_cnt: torch.Tensor) -> None:
+    """Accumulate (items, products) per log2 item-size bucket into LONG_STATS."""
+    b = torch.floor(torch.log2(rt_cnt.double() + 1)).long()
+    items = torch.bincount(b, minlength=40).tolist()
+    prods = torch.bincount(b, weights=rt_cnt.double(), minlength=40).tolist()
+    for k in range(40):
+        if items[k]:
+            it, pr = LONG_STATS.get(k, (0, 0.0))
+            LONG_STATS[k] = (it + items[k], pr + prods[k])
 
 
 def _long_params():
@@ -276,9 +288,13 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         del wg_base, Hc, H, wg_hist
         rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()
         rt_cnt = T.reshape(-1).contiguous()
+        if LONG_STATS is not None:
+            _long_stats(rt_cnt)
         rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
+        lists = torch.empty(2 * R * nch + 2, dtype=torch.int32, device=dev)   # the two kernels' item lists
         _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
-                                                 stream), "long_dense")
+                                                 P(lists), stream), "long_dense")
+        del lists
         nnz_rt = rt_nnz.view(R, nch)
         nnz_r = nnz_rt.sum(1)
         if expect_nnz is not None and not torch.equal(nnz_r, expect_nnz[rb].long()):
