@@ -1017,7 +1017,8 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
     const int32_t* __restrict__ Aci, const float* __restrict__ Av, const int64_t* __restrict__ Brp,
     const int32_t* __restrict__ Bci, const float* __restrict__ Bv, const int64_t* __restrict__ wg_e0,
     const int64_t* __restrict__ wg_e1, int nch, int32_t* __restrict__ wg_hist,
-    const int64_t* __restrict__ wg_base, unsigned long long* __restrict__ scratch) {
+    const int64_t* __restrict__ wg_base, unsigned long long* __restrict__ scratch,
+    const int32_t* __restrict__ lidx, const uint32_t* __restrict__ btab) {
   __shared__ unsigned long long cur[SCATTER ? LONG_MAXCH : 1];
   __shared__ int hist[SCATTER ? 1 : LONG_MAXCH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1038,6 +1039,19 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
   for (int64_t e = wg_e0[wg] + w; e < e1; e += LONG_NT / 64) {
     const int j = Aci[e];
     const float a = SCATTER ? Av[e] : 0.f;
+    if constexpr (!SCATTER) {
+      // a long B row (long_btab): its chunk histogram is the difference of
+      // its chunk offsets, nch + 1 words instead of its whole column list
+      const int k = lidx != nullptr ? lidx[j] : -1;
+      if (k >= 0) {   // wave-uniform
+        const uint32_t* tk = btab + (int64_t)k * (nch + 1);
+        for (int t = lane; t < nch; t += 64) {
+          const int n = (int)(tk[t + 1] - tk[t]);
+          if (n) atomicAdd(&hist[t], n);
+        }
+        continue;
+      }
+    }
     const int64_t b0 = Brp[j], b1 = Brp[j + 1];
     for (int64_t f0 = b0; f0 < b1; f0 += 256) {   // 4 loads in flight per lane
       int c[4];
@@ -1077,6 +1091,32 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
     __syncthreads();
     for (int t = tid; t < nch; t += LONG_NT) wg_hist[wg * nch + t] = hist[t];
   }
+}
+
+// Chunk offsets of the long rows of B (the routing histogram's shortcut):
+// tab[k * (nch + 1) + c] = first entry of B row lrows[k] whose column is
+// >= c * W, relative to the row start (c = nch: the row length).  One thread
+// per (row, chunk boundary), a binary search each.  Built once per right
+// operand; a hub row of B (R-MAT: up to ~10^6 entries, referenced by as many
+// A entries) then costs nch + 1 words per A entry in the histogram pass.
+__global__ __launch_bounds__(256) void long_btab(const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci,
+                                                 const int32_t* __restrict__ lrows, int64_t nlong, int nch,
+                                                 uint32_t* __restrict__ tab) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= nlong * (nch + 1)) return;
+  const int64_t k = t / (nch + 1);
+  const int c = (int)(t - k * (nch + 1));
+  const int j = lrows[k];
+  const int64_t r0 = Brp[j], r1 = Brp[j + 1];
+  int64_t lo = c < nch ? r0 : r1, hi = r1;   // boundary nch: the row end
+  if (c < nch) {
+    const int bound = c << LONG_LGW;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (Bci[mid] < bound) lo = mid + 1; else hi = mid;
+    }
+  }
+  tab[t] = (uint32_t)(lo - r0);
 }
 
 // 64-lane inclusive prefix sum on the DPP network (VALU; no LDS traffic):
@@ -1625,16 +1665,31 @@ SPMM_EXPORT int spmm_spgemm_esc_ordered(const int64_t* Arp, const int32_t* Aci, 
 SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp,
                                        const int32_t* Bci, const float* Bv, const int64_t* wg_e0,
                                        const int64_t* wg_e1, int64_t nwg, int nch, int32_t* wg_hist,
-                                       const int64_t* wg_base, void* scratch, void* stream) {
+                                       const int64_t* wg_base, void* scratch, const int32_t* lidx,
+                                       const uint32_t* btab, void* stream) {
+  // lidx / btab (histogram pass, optional): B row -> long-row index or -1,
+  // and the long rows' chunk offsets (spmm_spgemm_long_btab)
   if (nwg <= 0) return 0;
   if (nch > LONG_MAXCH) return (int)hipErrorInvalidValue;
+  if ((lidx == nullptr) != (btab == nullptr)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   if (scatter)
     hipLaunchKernelGGL(long_route<true>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0, wg_e1,
-                       nch, wg_hist, wg_base, (unsigned long long*)scratch);
+                       nch, wg_hist, wg_base, (unsigned long long*)scratch, nullptr, nullptr);
   else
     hipLaunchKernelGGL(long_route<false>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0,
-                       wg_e1, nch, wg_hist, wg_base, (unsigned long long*)scratch);
+                       wg_e1, nch, wg_hist, wg_base, (unsigned long long*)scratch, lidx, btab);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+SPMM_EXPORT int spmm_spgemm_long_btab(const int64_t* Brp, const int32_t* Bci, const int32_t* lrows, int64_t nlong,
+                                      int nch, uint32_t* tab, void* stream) {
+  if (nlong <= 0) return 0;
+  if (nch > LONG_MAXCH) return (int)hipErrorInvalidValue;
+  const int64_t n = nlong * (nch + 1);
+  hipLaunchKernelGGL(long_btab, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Brp, Bci, lrows,
+                     nlong, nch, tab);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

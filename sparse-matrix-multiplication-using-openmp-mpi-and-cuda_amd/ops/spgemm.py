@@ -45,7 +45,8 @@ _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_
                      C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_compact", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, c_vp,
-                     c_vp, c_vp, c_vp)
+                     c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_btab", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
@@ -225,6 +226,35 @@ def _long_params():
     return _LONG
 
 
+LONG_BTAB_MIN = 4   # B rows of >= this many entries per column chunk get a chunk-offset table
+
+
+def _long_btab(B: CSR, nch: int):
+    """(lidx, btab) of B for the routing histogram (csr_spgemm.hip long_btab):
+    lidx[j] = index of B row j among the rows of >= LONG_BTAB_MIN * nch
+    entries (else -1), btab = those rows' nch + 1 chunk offsets.  Memoised on
+    the operand like :func:`_splits` (a streamed product routes many A row
+    panels against one B).  (None, None) when B has no such row."""
+    key = (B.rowptr.data_ptr(), B.col.data_ptr(), B.m, B.n, B.nnz, nch)
+    hit = getattr(B, "_btab_memo", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    lens = B.rowptr[1:] - B.rowptr[:-1]
+    lrows = (lens >= LONG_BTAB_MIN * nch).nonzero().flatten().to(torch.int32)
+    nlong = lrows.numel()
+    out = (None, None)
+    if nlong:
+        lidx = torch.full((B.m,), -1, dtype=torch.int32, device=B.device)
+        lidx[lrows.long()] = torch.arange(nlong, dtype=torch.int32, device=B.device)
+        btab = torch.empty(nlong * (nch + 1), dtype=torch.int32, device=B.device)
+        _native.check(_native.hip().spmm_spgemm_long_btab(_native.ptr(B.rowptr), _native.ptr(B.col), _native.ptr(lrows),
+                                                           nlong, nch, _native.ptr(btab), _native.stream_ptr(B.device)),
+                      "spgemm_long_btab")
+        out = (lidx, btab)
+    B._btab_memo = (key, out)
+    return out
+
+
 def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torch.Tensor, stream,
                out_nnz: Optional[torch.Tensor] = None, Crp=None, Cci=None, Cv=None,
                expect_nnz: Optional[torch.Tensor] = None, defer: Optional[list] = None) -> None:
@@ -246,6 +276,7 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
     if nch > maxch:
         raise ValueError(f"long-row path supports at most {maxch << lgw} columns, got {B.n}")
     cap = max(GLOBAL_WS_BYTES // 8, int(nprod_rows.max()))
+    lidx, btab = _long_btab(B, nch) if CONFIG.spgemm_long_btab else (None, None)
     rows = rows.long()
     csum = torch.cumsum(nprod_rows.long(), 0)
     nrows = rows.numel()
@@ -269,7 +300,9 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         wg_hist = torch.empty(nwg * nch, dtype=torch.int32, device=dev)
         nil = None
         _native.check(lib.spmm_spgemm_long_route(0, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
-                                                 P(wg_e1), nwg, nch, P(wg_hist), nil, nil, stream), "long_route")
+                                                 P(wg_e1), nwg, nch, P(wg_hist), nil, nil,
+                                                 P(lidx) if lidx is not None else nil,
+                                                 P(btab) if btab is not None else nil, stream), "long_route")
         H = wg_hist.view(nwg, nch).long()
         T = torch.zeros((R, nch), dtype=torch.int64, device=dev).index_add_(0, row_of_wg, H)
         chunk_off = torch.cumsum(T, 1) - T
@@ -281,9 +314,14 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         Hc = torch.cumsum(H.t().contiguous(), 1).t() - H
         Hc = Hc - Hc[first_wg][row_of_wg]
         wg_base = (row_base[row_of_wg, None] + chunk_off[row_of_wg] + Hc).contiguous()
-        scratch = torch.empty(int(row_tot.sum()), dtype=torch.int64, device=dev)
+        # the scatter pass writes exactly the histogram's slots: a histogram
+        # that disagrees with the rows' product counts would overrun them
+        ntot, nbad = torch.stack([row_tot.sum(), (row_tot != nprod_rows[start:end]).sum()]).tolist()
+        if nbad:
+            raise RuntimeError(f"spgemm long rows: routing histogram disagrees with the product counts ({nbad} rows)")
+        scratch = torch.empty(ntot, dtype=torch.int64, device=dev)
         _native.check(lib.spmm_spgemm_long_route(1, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
-                                                 P(wg_e1), nwg, nch, nil, P(wg_base), P(scratch), stream),
+                                                 P(wg_e1), nwg, nch, nil, P(wg_base), P(scratch), nil, nil, stream),
                       "long_route")
         del wg_base, Hc, H, wg_hist
         rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()
@@ -417,19 +455,29 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None)
     """Numeric without a symbolic phase: rows are binned by their product count
     and written at product-count offsets (an upper bound of their nnz), then
     compacted into the final CSR by one copy kernel.  Trades one extra pass
-    over C for the whole symbolic phase."""
+    over C for the whole symbolic phase.
+
+    Hub rows (the HBM long-row path) skip the staging buffer: their chunk
+    results stay in the long-row scratch and ``place_long`` copies them
+    straight to their final rows once the row pointer exists, so the
+    compaction only moves the LDS-bin rows (R-MAT: most of C is hub rows,
+    which were otherwise written three times)."""
     dev = A.device
     m = A.m
+    staged = torch.where(_bins(nprod, 1) == NUM_GLOBAL, torch.zeros_like(nprod), nprod)
     ub = torch.zeros(m + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(nprod, 0, out=ub[1:])
-    tot = info.flops // 2
+    torch.cumsum(staged, 0, out=ub[1:])
+    tot = int(ub[-1])
     Uci = torch.empty(tot, dtype=torch.int32, device=dev)
     Uv = torch.empty(tot, dtype=torch.float32, device=dev)
     out_nnz = torch.zeros(m, dtype=torch.int32, device=dev)
     flags = torch.zeros(m, dtype=torch.int32, device=dev)
     cap = nprod.to(torch.int32)
+    deferred = []
     _run_bins(1, A, B, nprod, cap, ub, Uci, Uv, flags, info.rows_per_bin_num, info.mean_seg, out_nnz=out_nnz,
-              B_ready=B_ready)
+              B_ready=B_ready, defer=deferred)
+    for rb, *_ in deferred:   # placed by place_long, not copied by the compaction
+        ub[rb] = -1
     rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     torch.cumsum(out_nnz, 0, out=rowptr[1:])
     nnz = int(rowptr[-1])
@@ -437,9 +485,12 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None)
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     P = _native.ptr
-    _native.check(_native.hip().spmm_spgemm_compact(P(ub), P(rowptr), m, P(Uci), P(Uv), P(Cci), P(Cv),
-                                                     _native.stream_ptr(dev)), "spgemm_compact")
+    stream = _native.stream_ptr(dev)
+    _native.check(_native.hip().spmm_spgemm_compact(P(ub), P(rowptr), m, P(Uci), P(Uv), P(Cci), P(Cv), stream),
+                  "spgemm_compact")
     del Uci, Uv
+    place_long(deferred, rowptr, Cci, Cv, stream)
+    del deferred
     return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
 
 
@@ -871,10 +922,12 @@ def _splits(B: CSR) -> torch.Tensor:
 
 def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, Cci, Cv, flags, info_bins,
               mean_seg: float = 0.0, out_nnz: Optional[torch.Tensor] = None,
-              nprod: Optional[torch.Tensor] = None, B_ready=None):
+              nprod: Optional[torch.Tensor] = None, B_ready=None, defer: Optional[list] = None):
     """Run the LDS bins, then the HBM path for the rest.  Numeric: ``row_nnz`` is
     each row's capacity in the output (exact nnz, or the product count in
-    one-pass mode where ``out_nnz`` receives the real counts)."""
+    one-pass mode where ``out_nnz`` receives the real counts).  ``defer``
+    (one-pass): the long rows' results stay in their scratch for
+    :func:`place_long` instead of being written at ``Crp``."""
     dev = A.device
     lib = _native.hip()
     P = _native.ptr
@@ -912,7 +965,7 @@ def _run_bins(numeric: int, A: CSR, B: CSR, counts: torch.Tensor, row_nnz, Crp, 
         if not numeric:            # symbolic: exact counts
             _long_rows(0, A, B, rows, nprod_rows, stream, out_nnz=row_nnz)
         elif out_nnz is not None:  # one-pass: values at product-count offsets, real counts out
-            _long_rows(1, A, B, rows, nprod_rows, stream, out_nnz=out_nnz, Crp=Crp, Cci=Cci, Cv=Cv)
+            _long_rows(1, A, B, rows, nprod_rows, stream, out_nnz=out_nnz, Crp=Crp, Cci=Cci, Cv=Cv, defer=defer)
         else:                      # two-phase numeric: into the layout fixed by symbolic
             _long_rows(1, A, B, rows, nprod_rows, stream, Crp=Crp, Cci=Cci, Cv=Cv, expect_nnz=row_nnz)
 

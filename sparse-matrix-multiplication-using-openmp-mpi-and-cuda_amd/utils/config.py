@@ -52,6 +52,8 @@ class Config:
     # windows per row-major count unit (1: 16 KB bitmaps, 8 per CU; 2: 32 KB, 4 per CU)
     spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
+    # long-row routing histogram reads a chunk-offset table for the long rows of B (1) or their columns (0)
+    spgemm_long_btab: int = field(default_factory=lambda: _env("SPMM_SPGEMM_LONG_BTAB", 1, int))
     # MFMA panel SpMM when the panel column reuse reaches this: it wins even at
     # reuse 1.03 (65536^2 @ 0.1 % x 128 cols: 135 us vs 147 us rowwise, profiles/PERF_LOG.md)
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.0, float))

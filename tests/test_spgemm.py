@@ -818,6 +818,48 @@ def test_spgemm_gpu_long_rows_wave_items(monkeypatch, onepass):
         assert torch.equal(Cg.val.cpu(), Cc.val)   # small integers: every order sums exactly
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("onepass", ["on", "off"])
+def test_spgemm_gpu_long_rows_btab_histogram(monkeypatch, onepass):
+    """B with hub rows (>= LONG_BTAB_MIN entries per column chunk) next to
+    short rows: the routing histogram takes the hub rows' chunk counts from
+    the chunk-offset table (long_btab) and the short rows from their
+    columns; C is identical with the table on and off and matches the CPU
+    product (small integers: exact in every summation order)."""
+    from spmm_amd.ops import spgemm as OS
+    from spmm_amd.utils.config import CONFIG
+
+    k, n = 6000, (1 << 20) + 77                   # nch = 33 column chunks, a partial last one
+    g = torch.Generator().manual_seed(11)
+    rows, cols = [], []
+    for r in range(k):
+        ln = 3000 if r % 97 == 0 else (140 if r % 13 == 0 else 9)   # hub / near-threshold / short
+        rows.append(torch.full((ln,), r))
+        cols.append(torch.randperm(n, generator=g)[:ln])
+    rr, cc = torch.cat(rows), torch.cat(cols)
+    B = CS.from_coo(rr, cc, torch.randint(-3, 4, (rr.numel(),), generator=g).float(), k, n)
+    ra, ca = [], []
+    for r, na in enumerate([2500, 0, 4000, 1800, 3000]):
+        ra.append(torch.full((na,), r))
+        ca.append(torch.randperm(k, generator=g)[:na])
+    ra, ca = torch.cat(ra), torch.cat(ca)
+    A = CS.from_coo(ra, ca, torch.randint(-2, 3, (ra.numel(),), generator=g).float(), 5, k)
+    Cc = SG.spgemm(A, B)
+    dev = torch.device("cuda")
+    Ad, Bd = A.to(dev), B.to(dev)
+    lidx, btab = OS._long_btab(Bd, (n + (1 << OS._long_params()[0]) - 1) >> OS._long_params()[0])
+    assert lidx is not None and int((lidx >= 0).sum()) == int(((B.rowptr[1:] - B.rowptr[:-1]) >= 4 * 33).sum())
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", onepass)
+    for tab in (1, 0):
+        monkeypatch.setattr(CONFIG, "spgemm_long_btab", tab)
+        info = SG.SpgemmInfo()
+        Cg = SG.spgemm(Ad, Bd, info)
+        assert SG.NUM_GLOBAL in info.rows_per_bin_num
+        assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+        assert torch.equal(Cg.col.cpu(), Cc.col)
+        assert torch.equal(Cg.val.cpu(), Cc.val)
+
+
 def test_streamed_spgemm_splits_panels_on_oom(monkeypatch):
     """A streamed panel that runs out of device memory is split in half and
     retried: consumers still get contiguous panels in row order and the
