@@ -127,7 +127,10 @@ def check(rc: int, what: str) -> None:
 
 
 def ptr(t) -> int:
-    """Raw data pointer of a torch tensor / numpy array (0 for empty)."""
+    """Raw data pointer of a torch tensor / numpy array (0 for empty; None,
+    i.e. a null pointer, for None)."""
+    if t is None:
+        return None
     if hasattr(t, "data_ptr"):
         return t.data_ptr()
     return t.ctypes.data
