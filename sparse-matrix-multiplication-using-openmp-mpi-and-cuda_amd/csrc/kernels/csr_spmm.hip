@@ -24,8 +24,9 @@
 //   cost because the MFMA rate is ~2.5 PF.
 //
 // spmm_rowwise — VALU path: one wave per row, each lane owns 2 of every 128
-//   output columns, 4 gathered X rows in flight per lane.  Best when rows share
-//   no columns (uniform random at very low density): no inspector needed.
+//   output columns, the row's indices read once and 16 gathered X rows in
+//   flight per lane.  Best when rows share no columns (uniform random at very
+//   low density): no inspector needed.
 #include <hip/hip_bf16.h>
 
 #include "common.hpp"
@@ -143,7 +144,14 @@ __global__ __launch_bounds__(NT) void spmm_panel_mfma(
   }
 }
 
-// One wave per row; lane owns columns 2*lane, 2*lane+1 of each 128-column block.
+// One wave per row; lane owns columns 2*lane, 2*lane+1 of each 128-column
+// block.  The row's column indices and values are read once, coalesced, 64
+// per lane-round; each entry's X row address is then a readlane (scalar) and
+// RW_DEPTH gathered X rows are in flight per lane: the gather of a row costs
+// ~nnz / RW_DEPTH memory latencies instead of two dependent latencies (index,
+// then X row) per 4 entries.
+constexpr int RW_DEPTH = 16;
+
 template <bool OUT_BF16>
 __global__ __launch_bounds__(NT) void spmm_rowwise(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
                                                    const unsigned short* __restrict__ av,
@@ -151,33 +159,37 @@ __global__ __launch_bounds__(NT) void spmm_rowwise(const int64_t* __restrict__ r
                                                    int64_t D, void* __restrict__ Yv, int64_t ldy) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-  if (row >= m) return;
+  if (row >= m) return;   // wave-uniform
   const int64_t e0 = rp[row], e1 = rp[row + 1];
   for (int64_t d0 = 0; d0 < D; d0 += 128) {
     const int64_t col = d0 + 2 * lane;
+    const bool live = col < D;
+    const unsigned short* Xc = X + (live ? col : 0);
     float s0 = 0.f, s1 = 0.f;
-    if (col < D) {
-      int64_t e = e0;
-      for (; e + 4 <= e1; e += 4) {
-        unsigned x[4];
-        float a[4];
+    for (int64_t eb = e0; eb < e1; eb += 64) {   // 64 entries per lane-round
+      const int ne = (int)(e1 - eb < 64 ? e1 - eb : 64);
+      const int myj = lane < ne ? ci[eb + lane] : 0;
+      const float mya = lane < ne ? bf2f(av[eb + lane]) : 0.f;
+      for (int k0 = 0; k0 < ne; k0 += RW_DEPTH) {
+        unsigned x[RW_DEPTH];
+        float a[RW_DEPTH];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          x[u] = *reinterpret_cast<const unsigned*>(X + (int64_t)ci[e + u] * ldx + col);
-          a[u] = bf2f(av[e + u]);
+        for (int u = 0; u < RW_DEPTH; ++u) {
+          const int k = k0 + u < ne ? k0 + u : ne - 1;   // (tail: reload the last entry, not accumulated)
+          const int j = __builtin_amdgcn_readlane(myj, k);
+          a[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mya), k));
+          x[u] = *reinterpret_cast<const unsigned*>(Xc + (int64_t)j * ldx);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          s0 += a[u] * bf2f((unsigned short)(x[u] & 0xFFFF));
-          s1 += a[u] * bf2f((unsigned short)(x[u] >> 16));
+        for (int u = 0; u < RW_DEPTH; ++u) {
+          if (k0 + u < ne) {   // wave-uniform
+            s0 += a[u] * bf2f((unsigned short)(x[u] & 0xFFFF));
+            s1 += a[u] * bf2f((unsigned short)(x[u] >> 16));
+          }
         }
       }
-      for (; e < e1; ++e) {
-        const unsigned x = *reinterpret_cast<const unsigned*>(X + (int64_t)ci[e] * ldx + col);
-        const float a = bf2f(av[e]);
-        s0 += a * bf2f((unsigned short)(x & 0xFFFF));
-        s1 += a * bf2f((unsigned short)(x >> 16));
-      }
+    }
+    if (live) {
       if (OUT_BF16) {
         unsigned short* Y = reinterpret_cast<unsigned short*>(Yv) + row * ldy + col;
         Y[0] = f2bf(s0);

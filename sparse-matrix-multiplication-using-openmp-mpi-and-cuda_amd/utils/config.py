@@ -54,8 +54,9 @@ class Config:
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     # long-row routing histogram reads a chunk-offset table for the long rows of B (1) or their columns (0)
     spgemm_long_btab: int = field(default_factory=lambda: _env("SPMM_SPGEMM_LONG_BTAB", 1, int))
-    # MFMA panel SpMM when the panel column reuse reaches this: it wins even at
-    # reuse 1.03 (65536^2 @ 0.1 % x 128 cols: 135 us vs 147 us rowwise, profiles/PERF_LOG.md)
+    # MFMA panel SpMM when the panel column reuse reaches this.  At reuse 1.03
+    # (65536^2 @ 0.1 % x 128 cols, BASELINE config 3, which names the MFMA path)
+    # the two kernels are within 5 %: MFMA 149 us, row kernel 142 us (PERF_LOG)
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.0, float))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))
 

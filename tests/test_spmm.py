@@ -119,6 +119,24 @@ def test_spmm_mfma_exact_small_integers():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D", [128, 256])
+def test_spmm_rowwise_exact_small_integers(D):
+    """Row kernels (XCD-sliced at D = 128, full width otherwise) on exact
+    integer data: rows of 0 .. ~150 entries (several 64-entry rounds), a row
+    count that leaves the last wave partly empty, both output types."""
+    dev = torch.device("cuda")
+    m, n = 301, 2000
+    A = gen_csr.uniform_csr(m, n, 0.05, seed=19, values="small_int")
+    keep = (A.row_ids() % 7) != 3                       # every 7th row empty
+    A = CS.from_coo(A.row_ids()[keep], A.col[keep].long(), A.val[keep].float(), m, n)
+    A = A.with_values(A.val.to(torch.bfloat16)).to(dev)
+    X = (torch.arange(n * D, device=dev).view(n, D) % 13 - 6).to(torch.bfloat16)
+    R = ref(A, X)
+    assert torch.equal(SM.spmm(A, X, method="rowwise"), R)
+    assert torch.equal(SM.spmm(A, X, method="rowwise", out_dtype=torch.bfloat16).float(), R.to(torch.bfloat16).float())
+
+
+@pytest.mark.gpu
 def test_spmm_graph_replay_matches_eager():
     """The HIP-graph replay of the SpMM step gives the eager result, also after
     new operands are copied into the static input."""
