@@ -6,7 +6,7 @@ import time
 
 import torch
 
-sys.path.insert(0, "/root/repo")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import spmm_amd  # noqa: F401,E402
 from spmm_amd.ops import spgemm as SG  # noqa: E402
 from spmm_amd.utils import gen_csr  # noqa: E402
