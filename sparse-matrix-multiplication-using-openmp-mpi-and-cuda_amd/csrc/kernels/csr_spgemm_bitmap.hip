@@ -32,6 +32,10 @@
 
 #include <type_traits>
 
+#ifndef SPMM_BM_SKIP_ROUNDS   // numeric pass 2: skip register rounds past the unit's chunk count (uniform)
+#define SPMM_BM_SKIP_ROUNDS 1
+#endif
+
 namespace {
 
 // 64-lane inclusive prefix sum on the DPP network (VALU only; no LDS
@@ -558,6 +562,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         // ranks of 4 rounds at a time (their LDS reads in flight together)
 #pragma unroll
         for (int d0 = 0; d0 < RR; d0 += 4) {
+#if SPMM_BM_SKIP_ROUNDS
+          if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
+#endif
           int r[4];
 #pragma unroll
           for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
@@ -871,6 +878,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       };
 #pragma unroll
       for (int d0 = 0; d0 < RR; d0 += 4) {
+#if SPMM_BM_SKIP_ROUNDS
+        if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
+#endif
         int r[4];
 #pragma unroll
         for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
