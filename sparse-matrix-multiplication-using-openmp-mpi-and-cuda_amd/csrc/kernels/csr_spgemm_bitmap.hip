@@ -32,6 +32,10 @@
 
 #include <type_traits>
 
+#ifndef SPMM_BM_SWEEP_G   // numeric rank prefix: bitmap words per lane and scan step (1, 2, 4 or 8)
+#define SPMM_BM_SWEEP_G 2
+#endif
+
 #ifndef SPMM_BM_SKIP_ROUNDS   // numeric pass 2: skip register rounds past the unit's chunk count (uniform)
 #define SPMM_BM_SKIP_ROUNDS 1
 #endif
@@ -528,14 +532,41 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       __syncthreads();
       BM_STAMP(1);
       // ---- rank prefix per 64-bit word: wave w owns words [w*WPW, (w+1)*WPW)
-      int run[WPT];
+      // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
+      // wave scan of their sum, 16-bit prefixes stored SG at a time)
+      constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+      constexpr bool PAIRS = SG > 1;
+      int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
       int wtot = 0;
+      if constexpr (PAIRS) {
 #pragma unroll
-      for (int kk = 0; kk < WPT; ++kk) {
-        const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
-        const int incl = bm_wave_incl(cnt);
-        run[kk] = wtot + incl - cnt;
-        wtot += __builtin_amdgcn_readlane(incl, 63);
+        for (int kk = 0; kk < WPT / SG; ++kk) {
+          const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&bm[w * WPW + kk * 64 * SG + SG * lane]);
+          int c[SG];
+#pragma unroll
+          for (int h = 0; h < SG / 2; ++h) {
+            const ulonglong2 x = src[h];
+            c[2 * h] = __popcll(x.x);
+            c[2 * h + 1] = __popcll(x.y);
+          }
+          int sum = 0;
+#pragma unroll
+          for (int i = 0; i < SG; ++i) {
+            if (i > 0) run[SG * kk + i] = sum;
+            sum += c[i];
+          }
+          const int incl = bm_wave_incl(sum);
+          run[SG * kk] = wtot + incl - sum;
+          wtot += __builtin_amdgcn_readlane(incl, 63);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < WPT; ++kk) {
+          const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
+          const int incl = bm_wave_incl(cnt);
+          run[kk] = wtot + incl - cnt;
+          wtot += __builtin_amdgcn_readlane(incl, 63);
+        }
       }
       const int any_dup = sdup;
       if (lane == 0) wsum[w] = wtot;
@@ -547,8 +578,31 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         base += (i < w) ? sw : 0;
         total += sw;
       }
+      if constexpr (PAIRS) {
 #pragma unroll
-      for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
+        for (int kk = 0; kk < WPT / SG; ++kk) {
+          const uint32_t g0 = (uint32_t)(base + run[SG * kk]);
+          uint32_t pk[SG / 2];
+#pragma unroll
+          for (int h = 0; h < SG / 2; ++h) {
+            const uint32_t lo = g0 + (h > 0 ? (uint32_t)run[SG * kk + 2 * h] : 0u);
+            const uint32_t hi = g0 + (uint32_t)run[SG * kk + 2 * h + 1];
+            pk[h] = (lo & 0xffffu) | (hi << 16);
+          }
+          uint16_t* dst = &pre16[w * WPW + kk * 64 * SG + SG * lane];
+          if constexpr (SG == 2) {
+            *reinterpret_cast<uint32_t*>(dst) = pk[0];
+          } else if constexpr (SG == 4) {
+            *reinterpret_cast<uint2*>(dst) = make_uint2(pk[0], pk[1]);
+          } else {
+            static_assert(SG == 8, "sweep group of 2, 4 or 8 words");
+            *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
+      }
       if (tid == 0) sdup = 0;
       __syncthreads();
       BM_STAMP(2);
@@ -847,14 +901,41 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       __syncthreads();
       BM_STAMP(1);
       // ---- rank prefix per 64-bit word ---------------------------------
-      int run[WPT];
+      // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
+      // wave scan of their sum, 16-bit prefixes stored SG at a time)
+      constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+      constexpr bool PAIRS = SG > 1;
+      int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
       int wtot = 0;
+      if constexpr (PAIRS) {
 #pragma unroll
-      for (int kk = 0; kk < WPT; ++kk) {
-        const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
-        const int incl = bm_wave_incl(cnt);
-        run[kk] = wtot + incl - cnt;
-        wtot += __builtin_amdgcn_readlane(incl, 63);
+        for (int kk = 0; kk < WPT / SG; ++kk) {
+          const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&bm[w * WPW + kk * 64 * SG + SG * lane]);
+          int c[SG];
+#pragma unroll
+          for (int h = 0; h < SG / 2; ++h) {
+            const ulonglong2 x = src[h];
+            c[2 * h] = __popcll(x.x);
+            c[2 * h + 1] = __popcll(x.y);
+          }
+          int sum = 0;
+#pragma unroll
+          for (int i = 0; i < SG; ++i) {
+            if (i > 0) run[SG * kk + i] = sum;
+            sum += c[i];
+          }
+          const int incl = bm_wave_incl(sum);
+          run[SG * kk] = wtot + incl - sum;
+          wtot += __builtin_amdgcn_readlane(incl, 63);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < WPT; ++kk) {
+          const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
+          const int incl = bm_wave_incl(cnt);
+          run[kk] = wtot + incl - cnt;
+          wtot += __builtin_amdgcn_readlane(incl, 63);
+        }
       }
       const int any_dup = sdup;
       if (lane == 0) wsum[w] = wtot;
@@ -866,8 +947,31 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
         base += (i < w) ? sw : 0;
         total += sw;
       }
+      if constexpr (PAIRS) {
 #pragma unroll
-      for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
+        for (int kk = 0; kk < WPT / SG; ++kk) {
+          const uint32_t g0 = (uint32_t)(base + run[SG * kk]);
+          uint32_t pk[SG / 2];
+#pragma unroll
+          for (int h = 0; h < SG / 2; ++h) {
+            const uint32_t lo = g0 + (h > 0 ? (uint32_t)run[SG * kk + 2 * h] : 0u);
+            const uint32_t hi = g0 + (uint32_t)run[SG * kk + 2 * h + 1];
+            pk[h] = (lo & 0xffffu) | (hi << 16);
+          }
+          uint16_t* dst = &pre16[w * WPW + kk * 64 * SG + SG * lane];
+          if constexpr (SG == 2) {
+            *reinterpret_cast<uint32_t*>(dst) = pk[0];
+          } else if constexpr (SG == 4) {
+            *reinterpret_cast<uint2*>(dst) = make_uint2(pk[0], pk[1]);
+          } else {
+            static_assert(SG == 8, "sweep group of 2, 4 or 8 words");
+            *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
+      }
       if (tid == 0) sdup = 0;
       __syncthreads();
       BM_STAMP(2);
