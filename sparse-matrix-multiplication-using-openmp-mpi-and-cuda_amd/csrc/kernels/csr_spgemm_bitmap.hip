@@ -32,6 +32,10 @@
 
 #include <type_traits>
 
+#ifndef SPMM_BM_ROWS_R   // register rounds of the row-major numeric kernel (chunk capacity 16 * R per unit)
+#define SPMM_BM_ROWS_R 10
+#endif
+
 #ifndef SPMM_BM_SWEEP_G   // numeric rank prefix: bitmap words per lane and scan step (1, 2, 4 or 8)
 #define SPMM_BM_SWEEP_G 2
 #endif
@@ -1688,7 +1692,7 @@ int bm_count(int64_t work, const BmArgs& a, hipStream_t s) {
 template <int C>
 struct BmRowKernel {
   static constexpr BmCfg K = kCfgs[C];
-  static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;   // (the pipeline registers cost 2 rounds)
+  static constexpr int R = K.rounds_fast > SPMM_BM_ROWS_R ? SPMM_BM_ROWS_R : K.rounds_fast;   // (the row pipeline's registers cost rounds)
   static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false>;
   static constexpr auto kcv = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true>;
 };
