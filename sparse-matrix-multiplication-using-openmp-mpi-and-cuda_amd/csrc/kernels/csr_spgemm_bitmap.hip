@@ -30,6 +30,7 @@
 // row come from one binary-search kernel (bm_window_splits), uint32 indices.
 #include "common.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 #ifndef SPMM_BM_ROWS_R   // register rounds of the row-major numeric kernel (chunk capacity 16 * R per unit)
@@ -691,7 +692,20 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 struct BmRowArgs {
   BmArgs a;
   const uint4* ws8;
+  int q0, q1;   // windows [q0, q1) of every row (window-major passes: the B column slice of a
+                // pass stays in the MALL while every row's products in it are formed)
 };
+
+// First B index of window q0 inside this entry's B row: the row start plus
+// the packed 16-bit lengths of windows 0 .. q0-1.
+__device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb, int q0) {
+  uint32_t b = wa.x;
+  for (int q = 0; q < q0; ++q) {
+    const uint32_t wl = q < 2 ? wa.y : q < 4 ? wa.z : q < 6 ? wa.w : wb;
+    b += (wl >> (16 * (q & 1))) & 0xffffu;
+  }
+  return b;
+}
 
 template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
@@ -795,11 +809,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   float v[RR];
   for (; row < m; row += NG) {
     const int na = cna;
-    uint32_t bq = cwa.x;   // first B index of window q of this thread's entry
-    for (int q = 0; q < nwin; ++q) {
-      const bool last = q == nwin - 1;
+    const int q0 = ra.q0, q1 = ra.q1;
+    uint32_t bq = bm_window_start(cwa, cwb, q0);   // first B index of window q of this thread's entry
+    for (int q = q0; q < q1; ++q) {
+      const bool last = q == q1 - 1;
       // ---- pipeline hooks (every path) ---------------------------------
-      if (q == 0) {
+      if (q == q0) {
         ld_entries(row + NG, n1a, n1b);
         ld_arp(row + 2 * NG, n2a, n2b);
       }
@@ -1454,10 +1469,11 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
 
   for (; row < m; row += NG) {
     const int na = cna;
-    uint32_t bq = cwa.x;
-    for (int q = 0; q < nwin; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
-      const bool last = q + NSUB >= nwin;
-      if (q == 0) {
+    const int q0 = ra.q0, q1 = ra.q1;   // (q0 a multiple of NSUB)
+    uint32_t bq = bm_window_start(cwa, cwb, q0);
+    for (int q = q0; q < q1; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
+      const bool last = q + NSUB >= q1;
+      if (q == q0) {
         ld_entries(row + NG);
         ld_arp(row + 2 * NG, n2a, n2b);
       }
@@ -1724,10 +1740,19 @@ struct BmRowCountKernel {
   static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kCountNT, SPMM_BM_COUNT_RR, 256>;
 };
 
+// passes > 0: window-major, one launch per `passes` windows (a multiple of nsub)
 template <int C>
-int bm_count_rows(const BmRowArgs& ra, int nsub, hipStream_t s) {
-  return nsub == 2 ? launch_rows(BmRowCountKernel<C, 2>::k, ra, s, kCountNT)
-                   : launch_rows(BmRowCountKernel<C, 1>::k, ra, s, kCountNT);
+int bm_count_rows(BmRowArgs ra, int nsub, int passes, hipStream_t s) {
+  const int nwin = ra.a.nwin;
+  const int step = passes > 0 ? ((passes + nsub - 1) / nsub) * nsub : nwin;
+  for (int q = 0; q < nwin; q += step) {
+    ra.q0 = q;
+    ra.q1 = q + step < nwin ? q + step : nwin;
+    const int rc = nsub == 2 ? launch_rows(BmRowCountKernel<C, 2>::k, ra, s, kCountNT)
+                             : launch_rows(BmRowCountKernel<C, 1>::k, ra, s, kCountNT);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 template <int C>
@@ -1740,11 +1765,20 @@ struct BmPipeKernel {
 
 // pipe: the software-pipelined kernel (needs nwin >= 4 for its row pipeline)
 template <int C>
-int bm_numeric_rows(const BmRowArgs& ra, int pipe, hipStream_t s) {
-  const int rc = pipe       ? launch_rows(BmPipeKernel<C>::k, ra, s)
-                 : ra.a.Bcv ? launch_rows(BmRowKernel<C>::kcv, ra, s)
-                            : launch_rows(BmRowKernel<C>::k, ra, s);
-  if (rc) return rc;
+int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, hipStream_t s) {
+  if (pipe) {
+    const int rc = launch_rows(BmPipeKernel<C>::k, ra, s);
+    if (rc) return rc;
+  } else {   // passes > 0: window-major, one launch per `passes` windows
+    const int nwin = ra.a.nwin;
+    const int step = passes > 0 ? passes : nwin;
+    for (int q = 0; q < nwin; q += step) {
+      ra.q0 = q;
+      ra.q1 = q + step < nwin ? q + step : nwin;
+      const int rc = ra.a.Bcv ? launch_rows(BmRowKernel<C>::kcv, ra, s) : launch_rows(BmRowKernel<C>::k, ra, s);
+      if (rc) return rc;
+    }
+  }
   return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
 }
 
@@ -1752,6 +1786,12 @@ template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, hipStream_t s) {
   const int rc = launch_bm(BmKernels<C>::fast, kFastNT, work, a, s);
   return rc ? rc : launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, a, s);
+}
+
+// integer knob from the environment (read once per name by the caller's static)
+int bm_env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
 }
 
 }  // namespace
@@ -1858,12 +1898,13 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
   if (pipe && (nwin < 4 || lg > 5)) return (int)hipErrorInvalidValue;   // (+ B.nnz < 2^27: host)
   BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
                       (const uint2*)Bcv, err},
-               (const uint4*)ws8};
+               (const uint4*)ws8, 0, nwin};
   hipStream_t s = (hipStream_t)stream;
+  const int passes = bm_env_int("SPMM_BM_NUM_PASS_WINDOWS", 0);
   switch (cfg) {
-    case 0: return bm_numeric_rows<0>(ra, pipe, s);
-    case 1: return bm_numeric_rows<1>(ra, pipe, s);
-    default: return bm_numeric_rows<2>(ra, pipe, s);
+    case 0: return bm_numeric_rows<0>(ra, pipe, passes, s);
+    case 1: return bm_numeric_rows<1>(ra, pipe, passes, s);
+    default: return bm_numeric_rows<2>(ra, pipe, passes, s);
   }
 }
 
@@ -1877,12 +1918,13 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   BmRowArgs ra{BmArgs{Arp, Aci, nullptr, nullptr, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr,
                       nullptr, 0, 0, nullptr, err},
-               (const uint4*)ws8};
+               (const uint4*)ws8, 0, nwin};
   hipStream_t s = (hipStream_t)stream;
+  const int passes = bm_env_int("SPMM_BM_COUNT_PASS_WINDOWS", 0);
   switch (cfg) {
-    case 0: return bm_count_rows<0>(ra, nsub, s);
-    case 1: return bm_count_rows<1>(ra, nsub, s);
-    default: return bm_count_rows<2>(ra, nsub, s);
+    case 0: return bm_count_rows<0>(ra, nsub, passes, s);
+    case 1: return bm_count_rows<1>(ra, nsub, passes, s);
+    default: return bm_count_rows<2>(ra, nsub, passes, s);
   }
 }
 
