@@ -582,6 +582,26 @@ def test_spgemm_gpu_bitmap_matches_binned(monkeypatch, cfg, m, k, n, da, db):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("num,count", [(1, 2), (2, 4), (3, 1)])
+def test_spgemm_gpu_bitmap_window_passes(monkeypatch, num, count):
+    """Window-major launches of the row kernels (SPMM_BM_NUM_PASS_WINDOWS /
+    SPMM_BM_COUNT_PASS_WINDOWS; 5 windows per row, so passes end ragged) give
+    the single-launch product exactly."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(1500, 20000, 0.002, seed=95, device=dev)
+    B = gen_csr.uniform_csr(20000, 600000, 1.4e-4, seed=96, device=dev)
+    C1 = SG.spgemm(A, B)
+    monkeypatch.setenv("SPMM_BM_NUM_PASS_WINDOWS", str(num))
+    monkeypatch.setenv("SPMM_BM_COUNT_PASS_WINDOWS", str(count))
+    info = SG.SpgemmInfo()
+    C2 = SG.spgemm(A, B, info)
+    assert info.rows_per_bin_num.get("bitmap_rows") == 1
+    assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+    # (duplicates are summed with LDS float atomics: the order, and so the last bit, may differ run to run)
+    assert torch.allclose(C1.val, C2.val, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rows", ["pipe", "nopipe", "off"])
 def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows):
     """The three numeric kernels of the widest-window configuration on a
