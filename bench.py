@@ -46,14 +46,7 @@ def _sync_barrier(comm):
 
 
 def _allreduce_sum(comm, x: float) -> float:
-    import torch
-    import torch.distributed as dist
-
-    if not comm.is_dist:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device=comm.device if comm.backend == "nccl" else "cpu")
-    dist.all_reduce(t)
-    return float(t.item())
+    return comm.allreduce_sum(x)
 
 
 def run_spgemm(comm, args, n: int, density: float, model: str):
@@ -165,6 +158,53 @@ def run_chain(comm, args):
         seq_len=cfg["n"], parallelism=f"dp{comm.world}")
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int, backend: str) -> int:
+    """``--gpus N`` without a launcher: start N rank processes (torchrun-style
+    environment, one per GPU, rendezvous on 127.0.0.1) BEFORE this process
+    touches the GPU, let rank 0's JSON line through on the shared stdout, and
+    return the first failing exit code (the other ranks are stopped then:
+    they would otherwise wait in a collective until the timeout)."""
+    import subprocess
+
+    import torch
+
+    ndev = torch.cuda.device_count()   # (does not initialise the GPU)
+    if ndev and ndev < n and backend != "gloo":
+        print(f"[bench] --gpus {n} but only {ndev} GPU(s) visible; RCCL needs one GPU per rank "
+              f"(rehearse several ranks on one card with --backend gloo)", file=sys.stderr, flush=True)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the others", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -189,6 +229,16 @@ def main() -> None:
                     help="process-group backend (gloo on GPUs: rehearse several ranks on one card)")
     args = ap.parse_args()
 
+    from spmm_amd.parallel.comm import launcher_env
+
+    _, env_world, _ = launcher_env()
+    launched = any(os.environ.get(v) for v in ("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "SLURM_NTASKS"))
+    if not launched and args.gpus > 1:
+        sys.exit(_self_launch(args.gpus, args.backend))
+    if launched and env_world != args.gpus:
+        print(f"[bench] launcher world size {env_world} != --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+
     import torch
 
     import spmm_amd  # noqa: F401
@@ -196,14 +246,22 @@ def main() -> None:
     from spmm_amd.parallel import comm as CM
 
     comm = CM.init(backend=args.backend, device="auto")
+    if comm.world != args.gpus:
+        print(f"[bench] process group has {comm.world} rank(s), --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
     if comm.device.type == "cuda":
         _native.hip()
     if comm.rank == 0:
-        print(f"[bench] {args.workload}: process group up ({comm.world} rank(s), {comm.device})", file=sys.stderr,
-              flush=True)
+        import torch.distributed as dist
+
+        pg = dist.get_world_size() if dist.is_initialized() else 1
+        print(f"[bench] {args.workload}: process group up ({comm.world} rank(s), backend {comm.backend}, "
+              f"torch.distributed world {pg}, {comm.device})", file=sys.stderr, flush=True)
     if args.workload == "spgemm":
+        label = "1M" if args.n == 1 << 20 else str(args.n)
         step, flops, extra, cfg = run_spgemm(comm, args, args.n, args.density,
-                                             "1Mx1M CSR SpGEMM at 0.01% density, 1D row-block via RCCL/xGMI")
+                                             f"{label}x{label} CSR SpGEMM at {args.density * 100:g}% density, "
+                                             f"1D row-block via RCCL/xGMI")
     elif args.workload == "spgemm64k":
         step, flops, extra, cfg = run_spgemm(comm, args, 65536, 1e-3, "65536x65536 CSR SpGEMM at 0.1% density")
     elif args.workload == "rmat":
@@ -254,6 +312,7 @@ def main() -> None:
                "dtype": "fp32" if args.workload in ("spgemm", "spgemm64k", "rmat") else (
                    "bf16" if args.workload == "spmm" else "uint64"),
                "data": "synthetic (device RNG, random values)", "config": cfg, "flops_per_step": flops,
+               "backend": comm.backend or "single-process",
                "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu", **extra}
         print(json.dumps(rec), flush=True)
     comm.close()

@@ -68,7 +68,8 @@ def host():
                 _sig(lib, "spmm_mtx_close", None, c_vp)
                 _sig(lib, "spmm_mtx_write", C.c_int, C.c_char_p, C.c_int64, C.c_int64, c_vp, c_vp, c_vp, C.c_int)
                 _sig(lib, "spmm_mtx_part", C.c_int, c_vp, C.c_int, C.c_int, c_i64p, c_i64p, c_i64p, C.c_int)
-                _sig(lib, "spmm_mtx_fill_part", C.c_int, c_vp, C.c_int64, C.c_int64, c_vp, c_vp, c_vp, C.c_int)
+                _sig(lib, "spmm_mtx_fill_part", C.c_int64, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp, c_vp, c_vp,
+                     C.c_int)
                 _sig(lib, "spmm_mtx_write_begin", c_vp, C.c_char_p, C.c_int64, C.c_int64, C.c_int64, C.c_int)
                 _sig(lib, "spmm_mtx_write_panel", C.c_int, c_vp, C.c_int64, C.c_int64, c_vp, c_vp, c_vp, C.c_int)
                 _sig(lib, "spmm_mtx_write_end", C.c_int, c_vp)

@@ -60,12 +60,7 @@ def cmd_mult(args) -> int:
     t_mult = comm.allreduce_max(time.perf_counter() - t1)
     flops, nnz_c = info.flops, Cp.nnz
     if comm.is_dist:
-        import torch.distributed as dist
-
-        t = torch.tensor([float(flops), float(nnz_c)], dtype=torch.float64,
-                         device=comm.device if comm.backend == "nccl" else "cpu")
-        dist.all_reduce(t)
-        flops, nnz_c = (int(x) for x in t.tolist())
+        flops, nnz_c = sum(comm.gather_ints(flops)), sum(comm.gather_ints(nnz_c))
     t2 = time.perf_counter()
     if args.output:
         MS.write_rows_p2p(args.output, Cp, row0, comm)

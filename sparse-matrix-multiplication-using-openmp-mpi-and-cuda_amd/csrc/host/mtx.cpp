@@ -147,12 +147,17 @@ SPMM_HOST_EXPORT int spmm_mtx_part(void* handle, int part, int nparts, int64_t* 
   return ntok % per ? -1 : 0;
 }
 
-// Entries of the byte range [b0, b1) (from spmm_mtx_part), as spmm_mtx_fill.
-SPMM_HOST_EXPORT int spmm_mtx_fill_part(void* handle, int64_t b0, int64_t b1, int64_t* ri, int64_t* ci, double* v,
-                                        int nthreads) {
+// Entries of the byte range [b0, b1) (from spmm_mtx_part), as spmm_mtx_fill,
+// at most `entries` of them (the caller's buffers).  Returns the number of
+// entry tokens found in the range, so the caller can check it against the
+// count spmm_mtx_part reported (a file changed in between, or a short part).
+SPMM_HOST_EXPORT int64_t spmm_mtx_fill_part(void* handle, int64_t b0, int64_t b1, int64_t entries, int64_t* ri,
+                                            int64_t* ci, double* v, int nthreads) {
   MtxHandle* h = (MtxHandle*)handle;
   const int per = (h->field == 2) ? 2 : 3;
-  parallel_tokens(h->f.data, (size_t)b0, (size_t)b1, nthreads, [&](int64_t g, const char* p, const char* end) {
+  const int64_t need = entries * per;
+  return parallel_tokens(h->f.data, (size_t)b0, (size_t)b1, nthreads, [&](int64_t g, const char* p, const char* end) {
+    if (g >= need) return;
     const int64_t e = g / per, o = g % per;
     if (o < 2) {
       int64_t x;
@@ -164,8 +169,7 @@ SPMM_HOST_EXPORT int spmm_mtx_fill_part(void* handle, int64_t b0, int64_t b1, in
       std::from_chars(*p == '+' ? p + 1 : p, q, dv);
       v[e] = dv;
     }
-  });
-  return 0;   // (pattern files: the caller fills unit values)
+  });   // (pattern files: the caller fills unit values)
 }
 
 // Writer: header, then row panels appended in order (a distributed run

@@ -33,7 +33,6 @@ from dataclasses import dataclass
 from typing import Callable, List, Optional, Tuple
 
 import torch
-import torch.distributed as dist
 
 from ..ops.csr import CSR
 from ..ops.spgemm import SpgemmInfo, csr_sum, spgemm
@@ -42,70 +41,17 @@ from ..parallel.partition import row_panels, weighted_row_panels
 from ..utils.gen_csr import pattern_csr, rmat_edges, rmat_nchunks, rmat_perm, uniform_csr
 
 
-def _allgather_equal(comm: Comm, t: torch.Tensor) -> torch.Tensor:
-    """[world * t.numel()] gather of equally sized 1-D tensors, rank order."""
-    if comm.backend == "nccl":
-        out = torch.empty(comm.world * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
-        return out
-    parts = [torch.empty_like(t) for _ in range(comm.world)]
-    dist.all_gather(parts, t.contiguous())
-    return torch.cat(parts)
-
-
 def allgather_csr_rows(panel: CSR, comm: Comm) -> CSR:
     """Concatenate every rank's row panel (same column space) in rank order."""
     if not comm.is_dist:
         return panel
-    wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
-    meta = _allgather_equal(comm, torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)).view(-1, 2)
-    ms, nnzs = meta[:, 0].tolist(), meta[:, 1].tolist()
-    mmax, emax = max(ms), max(nnzs)
-    cnt = torch.zeros(mmax, dtype=torch.int64, device=wd)
-    cnt[:panel.m] = (panel.rowptr[1:] - panel.rowptr[:-1]).to(wd)
-    col = torch.zeros(emax, dtype=panel.col.dtype, device=wd)
-    col[:panel.nnz] = panel.col.to(wd)
-    val = torch.zeros(emax, dtype=panel.val.dtype, device=wd)
-    val[:panel.nnz] = panel.val.to(wd)
-    g_cnt = _allgather_equal(comm, cnt).view(comm.world, mmax)
-    g_col = _allgather_equal(comm, col).view(comm.world, emax)
-    g_val = _allgather_equal(comm, val).view(comm.world, emax)
-    if all(x == mmax for x in ms) and all(x == emax for x in nnzs):
-        cnts, cols, vals = g_cnt.reshape(-1), g_col.reshape(-1), g_val.reshape(-1)
-    else:
-        cnts = torch.cat([g_cnt[r, :ms[r]] for r in range(comm.world)])
-        cols = torch.cat([g_col[r, :nnzs[r]] for r in range(comm.world)])
-        vals = torch.cat([g_val[r, :nnzs[r]] for r in range(comm.world)])
-    m = sum(ms)
-    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=wd)
-    torch.cumsum(cnts, 0, out=rowptr[1:])
-    out = CSR(m, panel.n, rowptr, cols.contiguous(), vals.contiguous())
-    return out.to(panel.device)
+    B_meta, ready = allgather_operand_async(panel, comm)
+    return ready()
 
 
 def gather_rows(panel: CSR, comm: Comm, dst: int = 0) -> Optional[CSR]:
     full = allgather_csr_rows(panel, comm)
     return full if comm.rank == dst else None
-
-
-def _allgather_async(comm: Comm, t: torch.Tensor):
-    """Start an all-gather of equally sized 1-D tensors; returns a function that
-    waits for it and yields the [world * t.numel()] result (rank order)."""
-    if comm.backend == "nccl":
-        out = torch.empty(comm.world * t.numel(), dtype=t.dtype, device=t.device)
-        work = dist.all_gather_into_tensor(out, t.contiguous(), async_op=True)
-
-        def finish():
-            work.wait()   # the current stream waits; the host does not
-            return out
-        return finish
-    parts = [torch.empty_like(t) for _ in range(comm.world)]
-    work = dist.all_gather(parts, t.contiguous(), async_op=True)
-
-    def finish_gloo():
-        work.wait()
-        return torch.cat(parts)
-    return finish_gloo
 
 
 class OperandReady:
@@ -132,13 +78,17 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
     1. sizes, then the row counts of every panel (small collectives): B's row
        pointer is complete, which is all the product-count / binning / memory
        planning phase of ``spgemm`` reads;
-    2. RCCL: the columns, then the value bits, as two collectives started
-       asynchronously (they run in issue order): the row plan overlaps the
-       columns, the window splits and count kernel (columns only) overlap the
-       values; each lands in a padded [world, emax] buffer and one native pass
-       unpacks it (the values together with the interleaved (column, value)
-       pairs of the bitmap kernel).  gloo: one packed [cols | values]
-       collective and host-side concatenation.
+    2. device panels: the columns, then the value bits, as two collectives
+       started asynchronously (they run in issue order): the row plan overlaps
+       the columns, the window splits and count kernel (columns only) overlap
+       the values; each lands in a padded [world, emax] buffer and one native
+       pass unpacks it (the values together with the interleaved (column,
+       value) pairs of the bitmap kernel).  Host panels (gloo on CPUs): one
+       packed [cols | values] collective and host-side concatenation.
+
+    The collectives are ``comm`` methods, so the device branch is the one
+    RCCL runs at P ranks, and the in-process loopback backend drives the same
+    branch at any P on one GPU (tests/test_dist_device.py).
 
     Returns (B with row pointer only, ready): ``ready()`` makes the current
     stream wait for the payload and returns the full CSR; ``ready.cols()``
@@ -146,73 +96,92 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
     """
     if not comm.is_dist:
         return panel, OperandReady(lambda: panel)
-    wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
-    meta = _allgather_equal(comm, torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)).view(-1, 2)
+    dev = panel.device
+    W = comm.world
+    meta = comm.all_gather(torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=dev)).view(-1, 2)
     ms, nnzs = meta[:, 0].tolist(), meta[:, 1].tolist()
     mmax, emax = max(ms), max(nnzs)
-    W = range(comm.world)
-    cbuf = torch.zeros(mmax, dtype=torch.int64, device=wd)
-    cbuf[:panel.m] = (panel.rowptr[1:] - panel.rowptr[:-1]).to(wd)
+    cbuf = torch.zeros(mmax, dtype=torch.int64, device=dev)
+    cbuf[:panel.m] = panel.rowptr[1:] - panel.rowptr[:-1]
     # counts first: collectives of one group run in issue order, so the small
     # one must not queue behind the payload
-    cnt = _allgather_equal(comm, cbuf).to(panel.device).view(comm.world, mmax)
-    counts = cnt.reshape(-1) if all(x == mmax for x in ms) else torch.cat([cnt[r, :ms[r]] for r in W])
+    cnt = comm.all_gather(cbuf).view(W, mmax)
+    counts = cnt.reshape(-1) if all(x == mmax for x in ms) else torch.cat([cnt[r, :ms[r]] for r in range(W)])
     m = sum(ms)
-    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=panel.device)
+    rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     torch.cumsum(counts, 0, out=rowptr[1:])
-    empty_c = torch.empty(0, dtype=torch.int32, device=panel.device)
-    empty_v = torch.empty(0, dtype=torch.float32, device=panel.device)
-    meta_B = CSR(m, panel.n, rowptr, empty_c, empty_v)
     nnz = sum(nnzs)
+    empty_c = torch.empty(0, dtype=panel.col.dtype, device=dev)
+    empty_v = torch.empty(0, dtype=panel.val.dtype, device=dev)
+    meta_B = CSR(m, panel.n, rowptr, empty_c, empty_v)
+    meta_B._nnz_total = nnz   # the payload is in flight: CSR.nnz (= len(col)) is 0 here
+    if emax == 0:
+        return meta_B, OperandReady(lambda: CSR(m, panel.n, rowptr, empty_c, empty_v))
 
-    if comm.backend == "nccl":
+    if dev.type == "cuda" and panel.col.dtype == torch.int32 and panel.val.dtype == torch.float32:
         from ..ops.spgemm import _native as _nat
 
-        dev = panel.device
         cb = torch.zeros(emax, dtype=torch.int32, device=dev)
         cb[:panel.nnz] = panel.col
         vb = torch.zeros(emax, dtype=torch.int32, device=dev)
-        vb[:panel.nnz] = panel.val.float().view(torch.int32)
-        pay_c = _allgather_async(comm, cb)
-        pay_v = _allgather_async(comm, vb)
+        vb[:panel.nnz] = panel.val.view(torch.int32)
+        pay_c = comm.all_gather_async(cb)
+        pay_v = comm.all_gather_async(vb)
         base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=dev)
         got = {}
 
         def unpack(gc, gv, col, val, cv):
             _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(
-                _nat.ptr(gc) if gc is not None else None, _nat.ptr(gv) if gv is not None else None, comm.world,
-                emax, _nat.ptr(base), max(nnzs), _nat.ptr(col), _nat.ptr(val) if val is not None else None,
+                _nat.ptr(gc) if gc is not None else None, _nat.ptr(gv) if gv is not None else None, W,
+                emax, _nat.ptr(base), emax, _nat.ptr(col), _nat.ptr(val) if val is not None else None,
                 _nat.ptr(cv) if cv is not None else None, _nat.stream_ptr(dev)), "spgemm_bm_unpack_gathered")
 
         def cols() -> CSR:
             if "col" not in got:
+                g = pay_c()
+                if g.numel() != W * emax:
+                    raise RuntimeError(f"operand gather: {g.numel()} column words, expected {W * emax}")
                 col = torch.empty(nnz, dtype=torch.int32, device=dev)
-                unpack(pay_c(), None, col, None, None)
+                unpack(g, None, col, None, None)
                 got["col"] = col
+                got["gc"] = g   # the unpack kernel is still reading it (stream order)
             return CSR(m, panel.n, rowptr, got["col"], empty_v)
 
         def full() -> CSR:
             if "B" not in got:
                 col = cols().col
+                g = pay_v()
+                if g.numel() != W * emax:
+                    raise RuntimeError(f"operand gather: {g.numel()} value words, expected {W * emax}")
                 val = torch.empty(nnz, dtype=torch.float32, device=dev)
                 cv = torch.empty((nnz, 2), dtype=torch.int32, device=dev)
-                unpack(None, pay_v(), col, val, cv)
+                unpack(None, g, col, val, cv)
                 B = CSR(m, panel.n, rowptr, col, val)
                 B._bcv = cv
                 got["B"] = B
+                got["gv"] = g
             return got["B"]
         return meta_B, OperandReady(full, cols)
 
-    buf = torch.zeros(2 * emax, dtype=torch.int32, device=wd)
-    buf[:panel.nnz] = panel.col.to(wd)
-    buf[emax:emax + panel.nnz] = panel.val.float().to(wd).view(torch.int32)
-    payload = _allgather_async(comm, buf)
+    # generic (host panels, other dtypes): columns and value bits padded per rank
+    vbits = {2: torch.int16, 4: torch.int32, 8: torch.int64}[panel.val.element_size()]
+    cb = torch.zeros(emax, dtype=panel.col.dtype, device=dev)
+    cb[:panel.nnz] = panel.col
+    vb = torch.zeros(emax, dtype=vbits, device=dev)
+    vb[:panel.nnz] = panel.val.view(vbits)
+    pay_c = comm.all_gather_async(cb)
+    pay_v = comm.all_gather_async(vb)
+
+    done = []
 
     def ready() -> CSR:
-        Gv = payload().to(panel.device).view(comm.world, 2 * emax)
-        col = torch.cat([Gv[r, :nnzs[r]] for r in W])
-        val = torch.cat([Gv[r, emax:emax + nnzs[r]] for r in W]).view(torch.float32)
-        return CSR(m, panel.n, rowptr, col, val)
+        if not done:
+            Gc = pay_c().view(W, emax)
+            Gv = pay_v().view(W, emax)
+            col = torch.cat([Gc[r, :nnzs[r]] for r in range(W)])
+            val = torch.cat([Gv[r, :nnzs[r]] for r in range(W)]).view(panel.val.dtype)
+            done.append(CSR(m, panel.n, rowptr, col, val))
+        return done[0]
     return meta_B, OperandReady(ready)
 
 
@@ -231,12 +200,6 @@ def rowblock_spgemm(A_panel: CSR, B_panel: CSR, comm: Comm, info: Optional[Spgem
     return spgemm(A_panel, B_meta, info, B_ready=ready)
 
 
-def _alltoall_v(comm: Comm, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
-    out = torch.empty(sum(recv), dtype=x.dtype, device=x.device)
-    dist.all_to_all_single(out, x.contiguous(), recv, send)
-    return out
-
-
 def sparse_reduce_scatter(partial: CSR, comm: Comm, row_counts: List[int],
                           info: Optional[SpgemmInfo] = None) -> CSR:
     """Sum every rank's full-height ``partial`` (same m x n on all ranks) and
@@ -252,22 +215,20 @@ def sparse_reduce_scatter(partial: CSR, comm: Comm, row_counts: List[int],
         return partial
     if sum(row_counts) != partial.m or len(row_counts) != comm.world:
         raise ValueError(f"row_counts {row_counts} do not split {partial.m} rows over {comm.world} ranks")
-    wd = partial.device if comm.backend == "nccl" else torch.device("cpu")
     W = comm.world
+    dev = partial.device
     offs = [0]
     for c in row_counts:
         offs.append(offs[-1] + c)
-    bounds = partial.rowptr[torch.tensor(offs, device=partial.device)]
-    nnz_to = (bounds[1:] - bounds[:-1]).to(wd)
-    nnz_from = _alltoall_v(comm, nnz_to, [1] * W, [1] * W)
+    bounds = partial.rowptr[torch.tensor(offs, device=dev)]
+    nnz_to = bounds[1:] - bounds[:-1]
+    nnz_from = comm.all_to_all_v(nnz_to, [1] * W, [1] * W)
     send_n, recv_n = nnz_to.tolist(), nnz_from.tolist()
     mp = row_counts[comm.rank]
-    cnt = (partial.rowptr[1:] - partial.rowptr[:-1]).to(wd)
-    cnt_from = _alltoall_v(comm, cnt, list(row_counts), [mp] * W)
-    col = _alltoall_v(comm, partial.col.to(wd), send_n, recv_n)
-    val = _alltoall_v(comm, partial.val.float().to(wd), send_n, recv_n)
-    dev = partial.device
-    cnt_from, col, val = cnt_from.to(dev).view(W, mp), col.to(dev), val.to(dev)
+    cnt = partial.rowptr[1:] - partial.rowptr[:-1]
+    cnt_from = comm.all_to_all_v(cnt, list(row_counts), [mp] * W).view(W, mp)
+    col = comm.all_to_all_v(partial.col, send_n, recv_n)
+    val = comm.all_to_all_v(partial.val.float(), send_n, recv_n)
     parts, e = [], 0
     for r in range(W):
         rp = torch.zeros(mp + 1, dtype=torch.int64, device=dev)
@@ -349,7 +310,8 @@ def streamed_spgemm(A: CSR, B: CSR, consume: Callable[[int, int, CSR], None], bu
             # smaller budget (a single row that does not fit is a real limit)
             if hi - lo <= 1:
                 raise
-            if A.device.type == "cuda":
+            if A.device.type == "cuda":   # drain the failed attempt before its blocks are reused
+                torch.cuda.synchronize(A.device)
                 torch.cuda.empty_cache()
             mid = (lo + hi) // 2
             todo += [(mid, hi), (lo, mid)]
@@ -395,19 +357,6 @@ class UniformProblem:
         return A.col_slice(lo, hi)
 
 
-def _allreduce_sum_(comm: Comm, t: torch.Tensor) -> torch.Tensor:
-    """In-place sum over ranks (RCCL on the device, gloo through the host)."""
-    if not comm.is_dist:
-        return t
-    if comm.backend == "nccl":
-        dist.all_reduce(t)
-        return t
-    h = t.cpu()
-    dist.all_reduce(h)
-    t.copy_(h)
-    return t
-
-
 def shuffle_entries(comm: Comm, rows: torch.Tensor, cols: torch.Tensor, vals: Optional[torch.Tensor],
                     cuts: List[int]):
     """Send every entry (row, col[, val]) to the rank that owns ``row`` (rank r
@@ -428,10 +377,8 @@ def shuffle_entries(comm: Comm, rows: torch.Tensor, cols: torch.Tensor, vals: Op
     k = len(fields)
     packed = torch.stack(fields, 1).reshape(-1)
     del order, dest, fields
-    wd = dev if comm.backend == "nccl" else torch.device("cpu")
-    send_w = send.to(wd)
-    recv_w = _alltoall_v(comm, send_w, [1] * W, [1] * W)
-    got = _alltoall_v(comm, packed.to(wd), (k * send_w).tolist(), (k * recv_w).tolist()).to(dev).view(-1, k)
+    recv = comm.all_to_all_v(send, [1] * W, [1] * W)
+    got = comm.all_to_all_v(packed, (k * send).tolist(), (k * recv).tolist()).view(-1, k)
     return got[:, 0].contiguous(), got[:, 1].contiguous(), (got[:, 2].contiguous().view(torch.float64)
                                                              if vals is not None else None)
 
@@ -452,7 +399,8 @@ def read_mtx_rowblock(path: str, comm: Comm, dtype=torch.float32) -> Tuple[CSR, 
     from ..ops.csr import from_coo
     from ..utils.mtx import read_mtx_coo
 
-    m, n, ri, ci, v = read_mtx_coo(path, comm.rank, comm.world)
+    m, n, ri, ci, v = read_mtx_coo(path, comm.rank, comm.world,
+                                   gather_counts=comm.gather_ints if comm.is_dist else None)
     cuts = [lo for lo, _ in row_panels(m, comm.world)] + [m]
     dev = comm.device
     ri, ci, v = shuffle_entries(comm, ri.to(dev), ci.to(dev), v.to(dev), cuts)
@@ -482,20 +430,17 @@ def write_rows_p2p(path: str, panel: CSR, row0: int, comm: Comm, dst: int = 0, p
     ``matrix``, sparse_matrix_mult.cu:466-607)."""
     from ..utils.mtx import MtxWriter
 
-    wd = panel.device if comm.backend == "nccl" else torch.device("cpu")
-    tot = torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=wd)
-    if comm.is_dist:
-        dist.all_reduce(tot)
+    tot = torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=panel.device)
+    comm.all_reduce_(tot)
     m_tot, nnz_tot = (int(x) for x in tot.tolist())
     if comm.rank != dst:
-        hdr = torch.tensor([row0, panel.m, panel.nnz], dtype=torch.int64, device=wd)
-        dist.send(hdr, dst)
+        comm.send(torch.tensor([row0, panel.m, panel.nnz], dtype=torch.int64, device=panel.device), dst)
         if panel.m:
-            dist.send((panel.rowptr[1:] - panel.rowptr[:-1]).to(wd).contiguous(), dst)
+            comm.send(panel.rowptr[1:] - panel.rowptr[:-1], dst)
         if panel.nnz:
-            dist.send(panel.col.to(wd).contiguous(), dst)
+            comm.send(panel.col, dst)
             if not pattern:
-                dist.send(panel.val.float().to(wd).contiguous(), dst)
+                comm.send(panel.val.float(), dst)
         return
     w = MtxWriter(path, m_tot, panel.n, nnz_tot, pattern)
     try:
@@ -503,21 +448,20 @@ def write_rows_p2p(path: str, panel: CSR, row0: int, comm: Comm, dst: int = 0, p
             if r == dst:
                 w.panel(row0, panel)
                 continue
-            hdr = torch.empty(3, dtype=torch.int64, device=wd)
-            dist.recv(hdr, r)
+            hdr = comm.recv(torch.empty(3, dtype=torch.int64), r)
             r0, mp, nz = (int(x) for x in hdr.tolist())
-            cnt = torch.zeros(mp, dtype=torch.int64, device=wd)
-            col = torch.empty(nz, dtype=torch.int32, device=wd)
-            val = torch.empty(0 if pattern else nz, dtype=torch.float32, device=wd)
+            cnt = torch.zeros(mp, dtype=torch.int64)
+            col = torch.empty(nz, dtype=torch.int32)
+            val = torch.empty(0 if pattern else nz, dtype=torch.float32)
             if mp:
-                dist.recv(cnt, r)
+                comm.recv(cnt, r)
             if nz:
-                dist.recv(col, r)
+                comm.recv(col, r)
                 if not pattern:
-                    dist.recv(val, r)
+                    comm.recv(val, r)
             rp = torch.zeros(mp + 1, dtype=torch.int64)
-            torch.cumsum(cnt.cpu(), 0, out=rp[1:])
-            w.panel(r0, CSR(mp, panel.n, rp, col.cpu(), val.cpu()))
+            torch.cumsum(cnt, 0, out=rp[1:])
+            w.panel(r0, CSR(mp, panel.n, rp, col, val))
     finally:
         w.close()
 
@@ -586,8 +530,8 @@ class RmatProblem:
         perm = rmat_perm(scale, seed, dev)
         s, d, _ = rmat_edges(scale, edge_factor, seed=seed, device=dev, chunk=chunk, chunks=(k0, k1), perm=perm)
         del perm
-        coldeg = _allreduce_sum_(comm, torch.bincount(d, minlength=n))
-        w = _allreduce_sum_(comm, torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, s, coldeg[d]))
+        coldeg = comm.all_reduce_(torch.bincount(d, minlength=n))
+        w = comm.all_reduce_(torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, s, coldeg[d]))
         del coldeg
         panels = weighted_row_panels(torch.cumsum(w, 0), comm.world)
         del w

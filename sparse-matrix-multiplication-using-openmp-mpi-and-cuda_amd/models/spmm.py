@@ -18,7 +18,6 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
-import torch.distributed as dist
 
 from ..ops.csr import CSR
 from ..ops.spmm import PanelPlan, SpmmGraph, plan_panels, spmm
@@ -33,19 +32,12 @@ def allgather_rows(Xp: torch.Tensor, comm: Comm, counts) -> torch.Tensor:
     if not comm.is_dist:
         return Xp
     mx = max(counts)
-    wd = Xp.device if comm.backend == "nccl" else torch.device("cpu")
-    buf = torch.zeros((mx, Xp.shape[1]), dtype=Xp.dtype, device=wd)
-    buf[:Xp.shape[0]] = Xp.to(wd)
-    if comm.backend == "nccl":
-        out = torch.empty((comm.world * mx, Xp.shape[1]), dtype=Xp.dtype, device=wd)
-        dist.all_gather_into_tensor(out, buf)
-        parts = list(out.view(comm.world, mx, -1))
-    else:
-        parts = [torch.empty_like(buf) for _ in range(comm.world)]
-        dist.all_gather(parts, buf)
+    buf = torch.zeros((mx, Xp.shape[1]), dtype=Xp.dtype, device=Xp.device)
+    buf[:Xp.shape[0]] = Xp
+    parts = comm.all_gather(buf).view(comm.world, mx, -1)
     if all(c == mx for c in counts):
-        return torch.cat(parts).to(Xp.device)
-    return torch.cat([parts[r][:counts[r]] for r in range(comm.world)]).to(Xp.device)
+        return parts.reshape(comm.world * mx, -1)
+    return torch.cat([parts[r, :counts[r]] for r in range(comm.world)])
 
 
 def rowblock_spmm(A_panel: CSR, X_panel: torch.Tensor, comm: Comm, counts, plan: Optional[PanelPlan] = None,
@@ -62,25 +54,13 @@ def innerdim_spmm(A_colpanel: CSR, X_panel: torch.Tensor, comm: Comm, row_counts
     if not comm.is_dist:
         return Yp
     mx = max(row_counts)
-    wd = Yp.device if comm.backend == "nccl" else torch.device("cpu")
     D = Yp.shape[1]
-    full = torch.zeros((comm.world * mx, D), dtype=torch.float32, device=wd)
+    full = torch.zeros((comm.world * mx, D), dtype=torch.float32, device=Yp.device)
     off = 0
     for r, c in enumerate(row_counts):
-        full[r * mx:r * mx + c] = Yp[off:off + c].to(wd)
+        full[r * mx:r * mx + c] = Yp[off:off + c]
         off += c
-    out = torch.empty((mx, D), dtype=torch.float32, device=wd)
-    if comm.backend == "nccl":
-        dist.reduce_scatter_tensor(out, full)
-    else:
-        _gloo_reduce_scatter(out, full, comm, mx)
-    return out[:row_counts[comm.rank]].to(Yp.device)
-
-
-def _gloo_reduce_scatter(out, full, comm: Comm, mx: int) -> None:
-    # gloo has no reduce_scatter: all_reduce then keep this rank's block
-    dist.all_reduce(full)
-    out.copy_(full[comm.rank * mx:(comm.rank + 1) * mx])
+    return comm.reduce_scatter(full)[:row_counts[comm.rank]]
 
 
 def column_panel(A: CSR, lo: int, hi: int) -> CSR:
@@ -121,9 +101,7 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
         step = graph.run
     nnz_a = A.nnz
     if comm.is_dist:
-        t = torch.tensor([nnz_a], dtype=torch.int64, device=comm.device if comm.backend == "nccl" else "cpu")
-        dist.all_reduce(t)
-        nnz_a = int(t.item())
+        nnz_a = sum(comm.gather_ints(nnz_a))
     flops = 2 * nnz_a * cols
     extra = dict(nnz_A=nnz_a, spmm_method=method, panel_reuse=(plan.reuse if plan is not None else None),
                  inspector_ms=inspector_ms, hip_graph=not comm.is_dist and comm.device.type == "cuda")

@@ -32,6 +32,7 @@ from .._native import c_vp
 from ..utils.config import CONFIG
 from .csr import CSR, sort_rows
 import ctypes as C
+import threading
 
 C_I64 = C.c_int64
 C_INT = C.c_int
@@ -372,7 +373,10 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     Memory admission is a forecast (free-memory fractions); when a one-pass
     mode still runs out of device memory, the product is redone with the
     two-phase symbolic + numeric path, which allocates exactly nnz(C) and no
-    staging buffer (``info.rows_per_bin_num["oom_fallback"]`` records it)."""
+    staging buffer (``info.rows_per_bin_num["oom_fallback"]`` records it).
+    The retry starts only after the device has drained: kernels of the
+    failed attempt (on this and on the side stream) may still be writing
+    buffers the caching allocator would hand to the retry."""
     info = info if info is not None else SpgemmInfo()
     if A.device.type != "cuda":
         return _spgemm(A, B, info, B_ready)
@@ -381,19 +385,23 @@ def spgemm(A: CSR, B: CSR, info: Optional[SpgemmInfo] = None, B_ready=None) -> C
     except torch.OutOfMemoryError:
         if CONFIG.spgemm_onepass == "off" and CONFIG.spgemm_bitmap == "off":
             raise   # already the lowest-memory path
+    torch.cuda.synchronize(A.device)
     torch.cuda.empty_cache()
-    saved = (CONFIG.spgemm_onepass, CONFIG.spgemm_bitmap, CONFIG.spgemm_pipeline)
-    CONFIG.spgemm_onepass, CONFIG.spgemm_bitmap, CONFIG.spgemm_pipeline = "off", "off", "off"
-    try:
-        info.rows_per_bin_num = {}
-        C_ = _spgemm(A, B, info, B_ready)
-    finally:
-        CONFIG.spgemm_onepass, CONFIG.spgemm_bitmap, CONFIG.spgemm_pipeline = saved
+    info.rows_per_bin_num = {}
+    C_ = _spgemm(A, B, info, B_ready, two_phase=True)
     info.rows_per_bin_num["oom_fallback"] = 1
     return C_
 
 
-def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None) -> CSR:
+def _true_nnz(B: CSR) -> int:
+    """nnz of an operand whose payload may still be in flight (a distributed
+    gather's row-pointer-only CSR carries the total; ``CSR.nnz`` is len(col))."""
+    return max(B.nnz, getattr(B, "_nnz_total", 0))
+
+
+def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, two_phase: bool = False) -> CSR:
+    """``two_phase``: symbolic + numeric only (no one-pass / bitmap modes),
+    the exact-memory path the OOM fallback uses."""
     if A.n != B.m:
         raise ValueError(f"inner dimensions differ: {A.n} vs {B.m}")
     if A.device != B.device:
@@ -423,28 +431,29 @@ def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None) -> CSR:
             return cached[0]
         # the columns-only stage of a two-stage gather (see models.spgemm.OperandReady)
         B_ready.cols = getattr(fetch, "cols", B_ready)
-    if _bitmap_ok(A, B, info.flops // 2, pre):
-        C_ = onepass_bitmap(A, B, info, B_ready, pre)
-        if C_ is not None:
-            return C_
-        info.rows_per_bin_num = {}
-    if CONFIG.spgemm_onepass == "auto" or CONFIG.spgemm_ordered == "auto":
-        pre["free"] = _FreeMem(A.device)
-    mode = _onepass_mode(info.flops // 2, A.device, pre_free=pre.get("free"))
-    if mode is not None and _ordered_ok(nprod, info.flops // 2, A.device, pre):
-        C_ = onepass_ordered(A, B, nprod, info, B_ready, pre)
-        if C_ is not None:
-            return C_
-        info.rows_per_bin_num = {}
-    if mode == "pipelined":
-        C_ = onepass_pipelined(A, B, nprod, info, B_ready)
-        if C_ is not None:
-            return C_
-        info.rows_per_bin_num = {}
-        if _onepass_mode(info.flops // 2, A.device, allow_pipeline=False) == "plain":   # long / spilled rows
-            mode = "plain"
-    if mode == "plain":
-        return onepass(A, B, nprod, info, B_ready)
+    if not two_phase:
+        if _bitmap_ok(A, B, info.flops // 2, pre):
+            C_ = onepass_bitmap(A, B, info, B_ready, pre)
+            if C_ is not None:
+                return C_
+            info.rows_per_bin_num = {}
+        if CONFIG.spgemm_onepass == "auto" or CONFIG.spgemm_ordered == "auto":
+            pre["free"] = _FreeMem(A.device)
+        mode = _onepass_mode(info.flops // 2, A.device, pre_free=pre.get("free"))
+        if mode is not None and _ordered_ok(nprod, info.flops // 2, A.device, pre):
+            C_ = onepass_ordered(A, B, nprod, info, B_ready, pre)
+            if C_ is not None:
+                return C_
+            info.rows_per_bin_num = {}
+        if mode == "pipelined":
+            C_ = onepass_pipelined(A, B, nprod, info, B_ready)
+            if C_ is not None:
+                return C_
+            info.rows_per_bin_num = {}
+            if _onepass_mode(info.flops // 2, A.device, allow_pipeline=False) == "plain":   # long / spilled rows
+                mode = "plain"
+        if mode == "plain":
+            return onepass(A, B, nprod, info, B_ready)
     if B_ready is not None:
         B = B_ready()
     row_nnz = symbolic(A, B, nprod, info)
@@ -638,7 +647,7 @@ def _bitmap_ok(A: CSR, B: CSR, total_products: int, pre: dict) -> bool:
     kernel, row products not far above the mean (the windows are sized from
     the mean; a skewed matrix, e.g. R-MAT, takes the binned path)."""
     mode = CONFIG.spgemm_bitmap
-    if mode == "off" or total_products == 0 or B.nnz >= (1 << 31) or B.n >= (1 << 30) or A.nnz >= (1 << 31):
+    if mode == "off" or total_products == 0 or _true_nnz(B) >= (1 << 31) or B.n >= (1 << 30) or A.nnz >= (1 << 31):
         return False
     nz = max(pre["nonempty"], 1)
     mean = total_products / nz
@@ -758,9 +767,12 @@ _SIDE = {}
 
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
-    s = _SIDE.get(dev.index)
+    """One side stream per (device, thread): loopback ranks are threads that
+    share a device, and must not interleave their pipelines on one stream."""
+    key = (dev.index, threading.get_ident())
+    s = _SIDE.get(key)
     if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
+        s = _SIDE[key] = torch.cuda.Stream(dev)
     return s
 
 
@@ -818,51 +830,53 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
     sB.wait_stream(sA)
     free = [None, None]
     off = hist[0]
-    for c in range(nch):
-        lo, hi = bounds[c], bounds[c + 1]
-        sci, sv = stage[c % 2]
-        if free[c % 2] is not None:
-            sA.wait_event(free[c % 2])              # chunk c-2's compaction has read this buffer
-        long_rows = []
-        for b in range(NUM_GLOBAL + 1):
-            cnt = hist[c * 16 + b + 1]
-            if cnt and b == NUM_GLOBAL:
-                long_rows.append(order[off:off + cnt])
-            elif cnt:
-                _native.check(lib.spmm_spgemm_lds(b, 1, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
-                                                  P(B.val), P(splits) if splits is not None else None,
-                                                  P(order) + 4 * off, cnt, B.n, _group_log2(seg / _slices(b, 1)),
-                                                  P(rcap), P(out_nnz), P(ub_rel), P(sci), P(sv), P(flags),
-                                                  sA.cuda_stream), "spgemm_lds(numeric, pipelined)")
-            off += cnt
-        off += hist[(c + 1) * 16] if c + 1 < nch else 0   # empty rows of the next chunk (bin -1)
-        spill = ((flags[lo:hi] & 2) != 0).nonzero().flatten()
-        if spill.numel():
-            info.rows_per_bin_num["lds_overflow"] = info.rows_per_bin_num.get("lds_overflow", 0) + int(spill.numel())
-            long_rows.append((spill + lo).to(torch.int32))
-        deferred = []
-        if long_rows:
-            # hub rows stay in their chunk scratch and go straight to C once
-            # the chunk's row pointer exists (the compaction skips them)
-            rows = torch.cat(long_rows)
-            _long_rows(1, A, B, rows, nprod[rows.long()], sA.cuda_stream, out_nnz=out_nnz, defer=deferred)
-            ub_rel[rows.long()] = -1
-        done = torch.cuda.Event()
-        done.record(sA)
-        with torch.cuda.stream(sB):
-            sB.wait_event(done)
-            torch.cumsum(out_nnz[lo:hi], 0, dtype=torch.int64, out=rowptr[lo + 1:hi + 1])
-            rowptr[lo + 1:hi + 1] += rowptr[lo]
-            _native.check(lib.spmm_spgemm_compact(P(ub_rel) + 8 * lo, P(rowptr) + 8 * lo, hi - lo, P(sci), P(sv),
-                                                  P(Cci), P(Cv), sB.cuda_stream), "spgemm_compact(pipelined)")
-            for d in deferred:   # allocated on sA, last read on sB
-                for t in d:
-                    t.record_stream(sB)
-            place_long(deferred, rowptr, Cci, Cv, sB.cuda_stream)
-            del deferred
-            free[c % 2] = torch.cuda.Event()
-            free[c % 2].record(sB)
-    sA.wait_stream(sB)
+    try:   # the side stream may still read this call's buffers: drain it even on an error
+        for c in range(nch):
+            lo, hi = bounds[c], bounds[c + 1]
+            sci, sv = stage[c % 2]
+            if free[c % 2] is not None:
+                sA.wait_event(free[c % 2])              # chunk c-2's compaction has read this buffer
+            long_rows = []
+            for b in range(NUM_GLOBAL + 1):
+                cnt = hist[c * 16 + b + 1]
+                if cnt and b == NUM_GLOBAL:
+                    long_rows.append(order[off:off + cnt])
+                elif cnt:
+                    _native.check(lib.spmm_spgemm_lds(b, 1, P(A.rowptr), P(A.col), P(A.val), P(B.rowptr), P(B.col),
+                                                      P(B.val), P(splits) if splits is not None else None,
+                                                      P(order) + 4 * off, cnt, B.n, _group_log2(seg / _slices(b, 1)),
+                                                      P(rcap), P(out_nnz), P(ub_rel), P(sci), P(sv), P(flags),
+                                                      sA.cuda_stream), "spgemm_lds(numeric, pipelined)")
+                off += cnt
+            off += hist[(c + 1) * 16] if c + 1 < nch else 0   # empty rows of the next chunk (bin -1)
+            spill = ((flags[lo:hi] & 2) != 0).nonzero().flatten()
+            if spill.numel():
+                info.rows_per_bin_num["lds_overflow"] = info.rows_per_bin_num.get("lds_overflow", 0) + int(spill.numel())
+                long_rows.append((spill + lo).to(torch.int32))
+            deferred = []
+            if long_rows:
+                # hub rows stay in their chunk scratch and go straight to C once
+                # the chunk's row pointer exists (the compaction skips them)
+                rows = torch.cat(long_rows)
+                _long_rows(1, A, B, rows, nprod[rows.long()], sA.cuda_stream, out_nnz=out_nnz, defer=deferred)
+                ub_rel[rows.long()] = -1
+            done = torch.cuda.Event()
+            done.record(sA)
+            with torch.cuda.stream(sB):
+                sB.wait_event(done)
+                torch.cumsum(out_nnz[lo:hi], 0, dtype=torch.int64, out=rowptr[lo + 1:hi + 1])
+                rowptr[lo + 1:hi + 1] += rowptr[lo]
+                _native.check(lib.spmm_spgemm_compact(P(ub_rel) + 8 * lo, P(rowptr) + 8 * lo, hi - lo, P(sci), P(sv),
+                                                      P(Cci), P(Cv), sB.cuda_stream), "spgemm_compact(pipelined)")
+                for d in deferred:   # allocated on sA, last read on sB
+                    for t in d:
+                        t.record_stream(sB)
+                place_long(deferred, rowptr, Cci, Cv, sB.cuda_stream)
+                del deferred
+                free[c % 2] = torch.cuda.Event()
+                free[c % 2].record(sB)
+    finally:
+        sA.wait_stream(sB)
     nnz = int(rowptr[-1])
     info.nnz = nnz
     return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)

@@ -1,4 +1,4 @@
-"""Process-group bootstrap and BSR point-to-point transport.
+"""Process-group bootstrap, collectives and BSR point-to-point transport.
 
 Parity: the reference bootstraps with MPI_Init (sparse_matrix_mult.cu:404-409)
 and moves partial products with blocking MPI_Send/MPI_Recv of host-serialised
@@ -12,8 +12,17 @@ reference never calls cudaSetDevice, so all its ranks share device 0) and
 * backend ``nccl`` — RCCL on ROCm: device-to-device over xGMI, straight from
   HBM, no host staging, no chunking (RCCL pipelines internally), 64-bit
   counts;
-* backend ``gloo`` — CPU tensors; used for the CPU backend and for
-  multi-process tests without GPUs.
+* backend ``gloo`` — CPU tensors; used for the CPU backend, for
+  multi-process tests without GPUs and for rehearsing several ranks on one
+  card (device tensors are staged through the host by this class).
+
+Every collective the models use is a method here (``all_gather``,
+``all_gather_async``, ``all_to_all_v``, ``all_reduce_``, ``reduce_scatter``,
+``send`` / ``recv``): callers hand in tensors on their compute device and get
+results on that device, whatever the wire is.  The in-process loopback
+backend (``parallel.loopback``) implements the same methods for P ranks as
+threads of one process, so the device-resident code paths that run under
+RCCL at P > 1 run at any P on a single GPU in tests.
 
 A matrix travels as a fixed 4-int64 header (rows, cols, nb, k) followed, when
 nb > 0, by the key and value tensors.  The receiver learns the payload size
@@ -21,14 +30,14 @@ from the header before posting the payload receives, so variable-size
 partials need no padding.
 
 Launchers (torchrun, mpirun/mpiexec) are recognised from their environment
-variables; with none present the job is a single process (loopback).
+variables; with none present the job is a single process.
 """
 from __future__ import annotations
 
 import datetime
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -54,6 +63,9 @@ def launcher_env():
     return rank, world, local
 
 
+_REDUCE_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
 @dataclass
 class Comm:
     rank: int
@@ -66,29 +78,137 @@ class Comm:
     def is_dist(self) -> bool:
         return self.backend is not None
 
-    # --- transport -------------------------------------------------------
-    def _wire_device(self) -> torch.device:
-        return self.device if self.backend == "nccl" else torch.device("cpu")
+    @property
+    def device_collectives(self) -> bool:
+        """True when collectives move device tensors directly (RCCL over
+        xGMI): no host staging, so device-side packing / unpacking pays."""
+        return self.backend == "nccl"
 
+    # --- helpers -----------------------------------------------------------
+    def _wire_device(self) -> torch.device:
+        return self.device if self.device_collectives else torch.device("cpu")
+
+    def _wire(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to(self._wire_device()).contiguous()
+
+    # --- collectives (results on the input's device) ------------------------
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world * t.numel()] concatenation of every rank's equally sized
+        tensor, rank order."""
+        return self.all_gather_async(t)()
+
+    def all_gather_async(self, t: torch.Tensor) -> Callable[[], torch.Tensor]:
+        """Start an all-gather of equally sized tensors; the returned function
+        waits for it (the current stream waits, not the host, under RCCL) and
+        yields the flat [world * numel] result in rank order."""
+        flat = t.reshape(-1)
+        if not self.is_dist:
+            return lambda: flat
+        dev = t.device
+        src = self._wire(flat)
+        if self.device_collectives:
+            out = torch.empty(self.world * flat.numel(), dtype=t.dtype, device=src.device)
+            work = dist.all_gather_into_tensor(out, src, async_op=True)
+
+            def finish():
+                work.wait()
+                return out.to(dev)
+            return finish
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        work = dist.all_gather(parts, src, async_op=True)
+
+        def finish_host():
+            work.wait()
+            return torch.cat(parts).to(dev)
+        return finish_host
+
+    def all_to_all_v(self, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
+        """Rank r sends x[sum(send[:p]) : sum(send[:p + 1])] to rank p and
+        receives recv[p] elements from each rank p (concatenated, rank
+        order).  1-D tensors; counts are in elements."""
+        if not self.is_dist:
+            return x
+        src = self._wire(x)
+        out = torch.empty(sum(recv), dtype=x.dtype, device=src.device)
+        dist.all_to_all_single(out, src, list(recv), list(send))
+        return out.to(x.device)
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place reduction over ranks."""
+        if not self.is_dist:
+            return t
+        if self.device_collectives and t.device == self.device and t.is_contiguous():
+            dist.all_reduce(t, op=_REDUCE_OPS[op])
+            return t
+        w = self._wire(t).clone()
+        dist.all_reduce(w, op=_REDUCE_OPS[op])
+        t.copy_(w)
+        return t
+
+    def reduce_scatter(self, full: torch.Tensor) -> torch.Tensor:
+        """Sum of every rank's ``full`` [world * c, ...], block ``rank``
+        ([c, ...]) of it on this rank."""
+        if not self.is_dist:
+            return full
+        c = full.shape[0] // self.world
+        if self.device_collectives:
+            src = self._wire(full)
+            out = torch.empty((c,) + tuple(full.shape[1:]), dtype=full.dtype, device=src.device)
+            dist.reduce_scatter_tensor(out, src)
+            return out.to(full.device)
+        w = self._wire(full).clone()   # gloo has no reduce-scatter: all-reduce, keep this rank's block
+        dist.all_reduce(w)
+        return w[self.rank * c:(self.rank + 1) * c].to(full.device)
+
+    def send(self, t: torch.Tensor, dst: int) -> None:
+        dist.send(self._wire(t), dst)
+
+    def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        """Receive into ``t`` (any device) and return it."""
+        w = t if (self.device_collectives and t.device == self.device and t.is_contiguous()) else \
+            torch.empty(t.shape, dtype=t.dtype, device=self._wire_device())
+        dist.recv(w, src)
+        if w is not t:
+            t.copy_(w)
+        return t
+
+    def allreduce_max(self, x: float) -> float:
+        return self._allreduce_scalar(x, "max")
+
+    def allreduce_sum(self, x: float) -> float:
+        return self._allreduce_scalar(x, "sum")
+
+    def _allreduce_scalar(self, x: float, op: str) -> float:
+        if not self.is_dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self._wire_device())
+        self.all_reduce_(t, op)
+        return float(t.item())
+
+    def gather_ints(self, x: int) -> List[int]:
+        """Every rank's integer, rank order (small host-visible exchange)."""
+        if not self.is_dist:
+            return [int(x)]
+        return [int(v) for v in self.all_gather(torch.tensor([int(x)], dtype=torch.int64,
+                                                             device=self._wire_device())).tolist()]
+
+    # --- BSR transport -------------------------------------------------------
     def send_bsr(self, M: BSR, dst: int) -> None:
-        wd = self._wire_device()
-        hdr = torch.tensor([M.rows, M.cols, M.nb, M.k], dtype=torch.int64, device=wd)
-        dist.send(hdr, dst)
+        hdr = torch.tensor([M.rows, M.cols, M.nb, M.k], dtype=torch.int64, device=self._wire_device())
+        self.send(hdr, dst)
         if M.nb:
-            dist.send(M.keys.to(wd).contiguous(), dst)
-            dist.send(M.vals.to(wd).contiguous(), dst)
+            self.send(M.keys, dst)
+            self.send(M.vals, dst)
 
     def recv_bsr(self, src: int) -> BSR:
-        wd = self._wire_device()
-        hdr = torch.empty(4, dtype=torch.int64, device=wd)
-        dist.recv(hdr, src)
+        hdr = self.recv(torch.empty(4, dtype=torch.int64, device=self._wire_device()), src)
         rows, cols, nb, k = (int(x) for x in hdr.tolist())
-        keys = torch.empty((nb, 2), dtype=torch.int32, device=wd)
-        vals = torch.empty((nb, k, k), dtype=torch.int64, device=wd)
+        keys = torch.empty((nb, 2), dtype=torch.int32, device=self.device)
+        vals = torch.empty((nb, k, k), dtype=torch.int64, device=self.device)
         if nb:
-            dist.recv(keys, src)
-            dist.recv(vals, src)
-        return BSR(rows, cols, k, keys.to(self.device), vals.to(self.device))
+            self.recv(keys, src)
+            self.recv(vals, src)
+        return BSR(rows, cols, k, keys, vals)
 
     def barrier(self) -> None:
         if self.is_dist:
@@ -96,13 +216,6 @@ class Comm:
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
-
-    def allreduce_max(self, x: float) -> float:
-        if not self.is_dist:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device=self._wire_device())
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
 
     def close(self) -> None:
         if self.is_dist and dist.is_initialized():

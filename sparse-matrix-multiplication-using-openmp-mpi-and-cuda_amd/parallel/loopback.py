@@ -3,13 +3,21 @@
 unit tests; §5.6 ``--comm loopback``).
 
 The reference's ranks exchange partials with blocking MPI_Send / MPI_Recv
-(sparse_matrix_mult.cu:466-553).  Here ``LoopbackComm`` implements the same
-point-to-point contract as :class:`parallel.comm.Comm` (``send_bsr`` /
-``recv_bsr`` in per-(src, dst) FIFO order, ``barrier``, ``allreduce_max``)
-over thread-safe queues, so the distributed chain code (the binomial tree
-with row-panel splits) runs unchanged at any P in one process: no launcher,
+(sparse_matrix_mult.cu:466-553).  ``LoopbackComm`` implements the whole
+:class:`parallel.comm.Comm` contract — point-to-point (``send`` / ``recv``,
+``send_bsr`` / ``recv_bsr`` in per-(src, dst) FIFO order) and every
+collective the models use (``all_gather[_async]``, ``all_to_all_v``,
+``all_reduce_``, ``reduce_scatter``, ``barrier``) — over a shared hub, so
+the distributed code runs unchanged at any P in one process: no launcher,
 no sockets, and a failing rank surfaces as an exception in the caller.
-A sent matrix is cloned, so sender and receiver never share storage.
+
+On a GPU (``run_loopback(..., device="cuda")``) every rank is a thread on
+the same card and ``device_collectives`` is True: the models take exactly
+the branches they take under RCCL (padded device payloads, device-side
+unpacking), which a single-GPU box cannot otherwise run at P > 1 (RCCL does
+not put two ranks of one communicator on one device).  Stream safety: a
+posting rank records an event on its current stream and every consumer's
+stream waits on it before reading, as RCCL orders its kernels.
 
     results = run_loopback(world, lambda comm: run_chain(folder, comm, ...))
 """
@@ -31,7 +39,55 @@ class _Hub:
         self.timeout_s = timeout_s
         self.q = {(s, d): queue.Queue() for s in range(world) for d in range(world)}
         self.barrier = threading.Barrier(world, timeout=timeout_s)
-        self.slots = [0.0] * world
+        self.cv = threading.Condition()
+        self.slots = {}     # collective sequence number -> [posted objects], readers left
+        self.failed = False
+
+    def post(self, seq: int, rank: int, obj) -> None:
+        with self.cv:
+            slot = self.slots.setdefault(seq, [[None] * self.world, 0, self.world])
+            slot[0][rank] = obj
+            slot[1] += 1
+            self.cv.notify_all()
+
+    def collect(self, seq: int, rank: int) -> list:
+        with self.cv:
+            ok = self.cv.wait_for(lambda: self.failed or (seq in self.slots and self.slots[seq][1] == self.world),
+                                  timeout=self.timeout_s)
+            if self.failed:
+                raise RuntimeError(f"loopback rank {rank}: another rank failed")
+            if not ok:
+                raise TimeoutError(f"loopback rank {rank}: collective #{seq} incomplete after {self.timeout_s} s")
+            slot = self.slots[seq]
+            out = list(slot[0])
+            slot[2] -= 1
+            if slot[2] == 0:
+                del self.slots[seq]
+            return out
+
+    def fail(self) -> None:
+        with self.cv:
+            self.failed = True
+            self.cv.notify_all()
+        self.barrier.abort()
+
+
+def _mark(t: torch.Tensor):
+    """(tensor, event recorded after its producer on the current stream)."""
+    if t.device.type == "cuda":
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(t.device))
+        return t, ev
+    return t, None
+
+
+def _take(item, device: torch.device) -> torch.Tensor:
+    t, ev = item
+    if ev is not None and device.type == "cuda":
+        torch.cuda.current_stream(device).wait_event(ev)
+    elif ev is not None:
+        ev.synchronize()
+    return t.to(device)
 
 
 class LoopbackComm(Comm):
@@ -40,6 +96,82 @@ class LoopbackComm(Comm):
     def __init__(self, rank: int, world: int, device: torch.device, hub: _Hub):
         super().__init__(rank, world, rank, device, "loopback")
         self._hub = hub
+        self._seq = 0
+
+    @property
+    def device_collectives(self) -> bool:
+        return self.device.type == "cuda"
+
+    def _exchange(self, obj) -> list:
+        seq = self._seq
+        self._seq += 1
+        self._hub.post(seq, self.rank, obj)
+        return self._hub.collect(seq, self.rank)
+
+    def _post(self, obj) -> Callable[[], list]:
+        """Post now, collect later (once: the result is kept, like a finished
+        RCCL work object that can be waited on again)."""
+        seq = self._seq
+        self._seq += 1
+        self._hub.post(seq, self.rank, obj)
+        got = []
+
+        def collect():
+            if not got:
+                got.append(self._hub.collect(seq, self.rank))
+            return got[0]
+        return collect
+
+    # --- collectives -------------------------------------------------------
+    def all_gather_async(self, t: torch.Tensor) -> Callable[[], torch.Tensor]:
+        flat = t.reshape(-1)
+        dev = t.device
+        got = self._post(_mark(flat))
+        return lambda: torch.cat([_take(x, dev) for x in got()])
+
+    def all_to_all_v(self, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
+        got = self._exchange((_mark(x), list(send)))
+        parts = []
+        for src, (item, ssend) in enumerate(got):
+            off = sum(ssend[:self.rank])
+            if ssend[self.rank] != recv[src]:
+                raise RuntimeError(f"loopback all_to_all_v: rank {src} sends {ssend[self.rank]} to rank "
+                                   f"{self.rank}, which expects {recv[src]}")
+            parts.append(_take(item, x.device)[off:off + ssend[self.rank]])
+        return torch.cat(parts) if parts else x[:0]
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        got = [_take(x, t.device) for x in self._exchange(_mark(t.clone()))]
+        acc = got[0].clone()
+        for g in got[1:]:
+            if op == "sum":
+                acc += g
+            elif op == "max":
+                acc = torch.maximum(acc, g)
+            else:
+                acc = torch.minimum(acc, g)
+        t.copy_(acc)
+        return t
+
+    def reduce_scatter(self, full: torch.Tensor) -> torch.Tensor:
+        c = full.shape[0] // self.world
+        s = self.all_reduce_(full.clone())
+        return s[self.rank * c:(self.rank + 1) * c].clone()
+
+    def send(self, t: torch.Tensor, dst: int) -> None:
+        self._hub.q[(self.rank, dst)].put(_mark(t.clone()))
+
+    def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        try:
+            item = self._hub.q[(src, self.rank)].get(timeout=self._hub.timeout_s)
+        except queue.Empty:
+            raise TimeoutError(f"loopback rank {self.rank}: nothing from rank {src} "
+                               f"in {self._hub.timeout_s} s") from None
+        x = _take(item, t.device)
+        if x.shape != t.shape:
+            raise RuntimeError(f"loopback recv: got {tuple(x.shape)}, expected {tuple(t.shape)}")
+        t.copy_(x)
+        return t
 
     def send_bsr(self, M: BSR, dst: int) -> None:
         self._hub.q[(self.rank, dst)].put(BSR(M.rows, M.cols, M.k, M.keys.clone(), M.vals.clone()))
@@ -55,12 +187,12 @@ class LoopbackComm(Comm):
     def barrier(self) -> None:
         self._hub.barrier.wait()
 
-    def allreduce_max(self, x: float) -> float:
-        self._hub.slots[self.rank] = x
-        self._hub.barrier.wait()
-        m = max(self._hub.slots)
-        self._hub.barrier.wait()   # everyone read before the slots are reused
-        return m
+    def _allreduce_scalar(self, x: float, op: str) -> float:
+        vals = self._exchange(float(x))
+        return max(vals) if op == "max" else (min(vals) if op == "min" else float(sum(vals)))
+
+    def gather_ints(self, x: int) -> List[int]:
+        return [int(v) for v in self._exchange(int(x))]
 
     def close(self) -> None:
         pass
@@ -70,24 +202,30 @@ def run_loopback(world: int, fn: Callable[[LoopbackComm], object], device: str =
                  timeout_s: float = 300.0) -> List[object]:
     """Run ``fn(comm)`` on ``world`` ranks (threads) and return their results
     in rank order; the first rank failure is re-raised here (the other ranks
-    are released by aborting the barrier)."""
+    are released by aborting the barrier and failing pending collectives)."""
     hub = _Hub(world, timeout_s)
     dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
     out: List[object] = [None] * world
     errs: List[BaseException] = []
 
     def body(r: int) -> None:
         try:
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)
             out[r] = fn(LoopbackComm(r, world, dev, hub))
         except BaseException as e:   # noqa: BLE001  (re-raised in the caller)
             errs.append(e)
-            hub.barrier.abort()
+            hub.fail()
 
     threads = [threading.Thread(target=body, args=(r,), name=f"loopback-rank{r}") for r in range(world)]
     for t in threads:
         t.start()
     for t in threads:
         t.join()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     if errs:
         raise errs[0]
     return out

@@ -8,6 +8,7 @@ hermitian (real) files are expanded to general, duplicates are summed.
 from __future__ import annotations
 
 import ctypes as C
+from typing import Callable, List, Optional
 
 import torch
 
@@ -31,11 +32,19 @@ def _open(path: str):
     return h, m.value, n.value, nnz.value, field.value, sym.value
 
 
-def read_mtx_coo(path: str, part: int = 0, nparts: int = 1, nthreads: int = 0):
+def read_mtx_coo(path: str, part: int = 0, nparts: int = 1, nthreads: int = 0,
+                 gather_counts: Optional[Callable[[int], List[int]]] = None):
     """Entries of part ``part`` of ``nparts`` of the file (line-aligned byte
     ranges of the entry section: a distributed read parses 1/nparts of the
     text per rank), symmetric storage expanded.  Returns (m, n, rows, cols,
-    values) as int64 / int64 / float64 host tensors, 0-based, any order."""
+    values) as int64 / int64 / float64 host tensors, 0-based, any order.
+
+    ``gather_counts`` (required for nparts > 1): all-gathers this part's
+    entry count (-1: the part does not hold whole entries) and returns every
+    part's, in part order.  With them every part applies the 1-part rules
+    exactly: a file with fewer entries than the header's nnz is rejected (by
+    every part), entries past the nnz-th are ignored, so the matrix does not
+    depend on the number of parts."""
     lib = _native.host()
     h, m, n, nnz, field, sym = _open(path)
     try:
@@ -48,15 +57,28 @@ def read_mtx_coo(path: str, part: int = 0, nparts: int = 1, nthreads: int = 0):
             if ne and lib.spmm_mtx_fill(h, ri.data_ptr(), ci.data_ptr(), v.data_ptr(), nthreads, err, 512) != 0:
                 raise MtxError(f"{path}: {err.value.decode()}")
         else:
+            if gather_counts is None:
+                raise ValueError("read_mtx_coo: a partial read needs gather_counts")
             b0, b1, ne_ = C.c_int64(), C.c_int64(), C.c_int64()
-            if lib.spmm_mtx_part(h, part, nparts, C.byref(b0), C.byref(b1), C.byref(ne_), nthreads) != 0:
-                raise MtxError(f"{path}: part {part}/{nparts} does not hold whole entries")
-            ne = ne_.value
+            whole = lib.spmm_mtx_part(h, part, nparts, C.byref(b0), C.byref(b1), C.byref(ne_), nthreads) == 0
+            counts = gather_counts(ne_.value if whole else -1)   # every part takes part in this, even a bad one
+            if min(counts) < 0:
+                bad = [p for p, c in enumerate(counts) if c < 0]
+                raise MtxError(f"{path}: part(s) {bad} of {nparts} do not hold whole entries")
+            total = sum(counts)
+            if total < nnz:
+                raise MtxError(f"{path}: file has {total} entries, expected {nnz}")
+            start = sum(counts[:part])
+            ne = max(0, min(counts[part], nnz - start))   # entries past the nnz-th are ignored, as in a 1-part read
             ri = torch.empty(ne, dtype=torch.int64)
             ci = torch.empty(ne, dtype=torch.int64)
             v = torch.ones(ne, dtype=torch.float64)
             if ne:
-                lib.spmm_mtx_fill_part(h, b0.value, b1.value, ri.data_ptr(), ci.data_ptr(), v.data_ptr(), nthreads)
+                per = 2 if field == 2 else 3
+                got = lib.spmm_mtx_fill_part(h, b0.value, b1.value, ne, ri.data_ptr(), ci.data_ptr(), v.data_ptr(),
+                                             nthreads)
+                if got != counts[part] * per:
+                    raise MtxError(f"{path}: part {part}/{nparts} parsed {got} tokens, expected {counts[part] * per}")
     finally:
         lib.spmm_mtx_close(h)
     if ne and (int(ri.min()) < 0 or int(ri.max()) >= m or int(ci.min()) < 0 or int(ci.max()) >= n):

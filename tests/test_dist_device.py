@@ -1,0 +1,274 @@
+"""Distributed code paths at P > 1 inside ONE process (VERDICT r2 missing #1-2).
+
+A one-GPU box cannot run RCCL at P > 1 (one communicator cannot put two ranks
+on one device), so the device-resident branches that run at 8 GPUs — padded
+[world, emax] operand payloads, the native unpack kernel with grid.y = world,
+device all-to-all-v shuffles, device reduce-scatter — are driven here by the
+in-process loopback backend (``parallel.loopback``): P ranks are threads on
+one device and ``comm.device_collectives`` is True, exactly as under RCCL.
+Every result is compared against the single-process product.  Panels are
+uneven and include EMPTY ones.  CPU variants of the same tests run in the
+default (no-GPU) suite; the GPU ones are marked ``gpu``.
+
+Also here: the Matrix Market partial read applies the 1-rank rules at any P
+(truncated files rejected by every rank, entries past the header's nnz
+ignored: ADVICE r2 medium), and ``bench.py --gpus N`` self-launches N ranks.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import spmm_amd  # noqa: F401
+from spmm_amd.models import spgemm as MS
+from spmm_amd.models import spmm as MM
+from spmm_amd.ops import csr as CS
+from spmm_amd.ops import spgemm as SG
+from spmm_amd.parallel.loopback import run_loopback
+from spmm_amd.utils import gen_csr, mtx
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M, K, N, D = 230, 190, 260, 8
+
+
+def _cuts(total: int, world: int, seed: int):
+    """Uneven panel boundaries; panels 1 and world-1 empty (world >= 3)."""
+    g = torch.Generator().manual_seed(seed)
+    w = torch.rand(world, generator=g) + 0.2
+    if world >= 3:
+        w[1] = 0.0
+        w[world - 1] = 0.0
+    sizes = (w / w.sum() * total).floor().long()
+    sizes[0] += total - int(sizes.sum())
+    cuts = [0]
+    for s in sizes.tolist():
+        cuts.append(cuts[-1] + s)
+    return cuts
+
+
+def _stack(parts, n):
+    rps, cols, vals, base = [torch.zeros(1, dtype=torch.int64)], [], [], 0
+    for C in parts:
+        rps.append(C.rowptr.cpu()[1:] + base)
+        base += int(C.rowptr[-1])
+        cols.append(C.col.cpu())
+        vals.append(C.val.cpu())
+    rp = torch.cat(rps)
+    return CS.CSR(rp.numel() - 1, n, rp, torch.cat(cols), torch.cat(vals))
+
+
+def _all_decompositions(world: int, device: str):
+    dev = torch.device(device)
+    A = gen_csr.uniform_csr(M, K, 0.05, seed=11)
+    B = gen_csr.uniform_csr(K, N, 0.05, seed=12)
+    X = (torch.arange(K * D, dtype=torch.float32).view(K, D) % 5 - 2).to(torch.bfloat16)
+    Ab = A.with_values((torch.round(A.val * 4) / 4).to(torch.bfloat16))
+    rc, kc = _cuts(M, world, 1), _cuts(K, world, 2)
+    row_counts = [rc[r + 1] - rc[r] for r in range(world)]
+    k_counts = [kc[r + 1] - kc[r] for r in range(world)]
+
+    def body(comm):
+        r = comm.rank
+        lo, hi, klo, khi = rc[r], rc[r + 1], kc[r], kc[r + 1]
+        Bp = B.row_slice(klo, khi).to(dev)
+        out = {}
+        # operand gather stages (columns first, then values + interleaved pairs)
+        meta, ready = MS.allgather_operand_async(Bp, comm)
+        out["meta_rowptr"] = meta.rowptr.cpu()
+        out["nnz_total"] = getattr(meta, "_nnz_total", meta.nnz)
+        cols_only = ready.cols()
+        out["cols"] = cols_only.col.cpu()
+        full = ready()
+        out["full"] = (full.rowptr.cpu(), full.col.cpu(), full.val.cpu())
+        cv = getattr(full, "_bcv", None)
+        out["cv"] = cv.cpu() if cv is not None else None
+        out["rb_spgemm"] = MS.rowblock_spgemm(A.row_slice(lo, hi).to(dev), Bp, comm)
+        out["in_spgemm"] = MS.innerdim_spgemm(A.col_slice(klo, khi).to(dev), Bp, comm, row_counts)
+        out["rb_spmm"] = MM.rowblock_spmm(Ab.row_slice(lo, hi).to(dev), X[klo:khi].to(dev), comm, k_counts).cpu()
+        out["in_spmm"] = MM.innerdim_spmm(MM.column_panel(Ab, klo, khi).to(dev), X[klo:khi].to(dev), comm,
+                                          row_counts).cpu()
+        return out
+
+    got = run_loopback(world, body, device=device, timeout_s=300)
+    if world >= 3:
+        assert rc[2] - rc[1] == 0 and kc[2] - kc[1] == 0   # empty panels really exercised
+    for g in got:   # every rank holds the same gathered operand = B
+        assert torch.equal(g["meta_rowptr"], B.rowptr) and g["nnz_total"] == B.nnz
+        assert torch.equal(g["cols"], B.col)
+        rp, col, val = g["full"]
+        assert torch.equal(rp, B.rowptr) and torch.equal(col, B.col) and torch.equal(val, B.val)
+        if g["cv"] is not None:
+            assert torch.equal(g["cv"][:, 0], B.col) and torch.equal(g["cv"][:, 1], B.val.view(torch.int32))
+    C = SG.spgemm(A, B)
+    Cd = C.to_dense().double()
+    for key in ("rb_spgemm", "in_spgemm"):
+        parts = [g[key] for g in got]
+        for r in range(world):
+            assert parts[r].m == rc[r + 1] - rc[r], (key, r)
+        S = _stack(parts, N)
+        assert S.is_sorted(), key
+        assert torch.allclose(S.to_dense().double(), Cd, atol=1e-5), key
+        if key == "rb_spgemm":
+            assert torch.equal(S.rowptr, C.rowptr) and torch.equal(S.col, C.col)
+    Y = Ab.to_dense(torch.float32) @ X.float()
+    for key in ("rb_spmm", "in_spmm"):
+        Yg = torch.cat([g[key] for g in got])
+        assert Yg.shape == Y.shape and torch.allclose(Yg, Y, atol=1e-3), key
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_loopback_cpu_all_decompositions(world):
+    _all_decompositions(world, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 7, 8])
+def test_loopback_gpu_device_branches(world):
+    """The RCCL code path (device payloads, native unpack over world ranks)
+    at W = 2 / 7 / 8 on one GPU."""
+    _all_decompositions(world, "cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_gpu_bench_problem(world):
+    """The bench's own problem construction and step (``UniformProblem`` +
+    ``rowblock_spgemm``) at 65536^2 @ 0.1 % (config 2: every rank's panel
+    product takes the bitmap-rank kernels) on W loopback ranks equals the
+    one-process product: same row pointer and columns, same values up to
+    fp32 summation order, same FLOP and nnz totals."""
+    n, dens = 65536, 1e-3
+
+    def body(comm):
+        prob = MS.UniformProblem.build(n, dens, comm, seed=1)
+        info = SG.SpgemmInfo()
+        C = MS.rowblock_spgemm(prob.A, prob.B, comm, info)
+        return (C.rowptr.cpu(), C.col.cpu(), C.val.cpu(), info.flops, info.nnz,
+                info.rows_per_bin_num.get("bitmap_units", 0))
+
+    got = run_loopback(world, body, device="cuda", timeout_s=600)
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(n, n, dens, seed=1, device=dev)
+    B = gen_csr.uniform_csr(n, n, dens, seed=2, device=dev)
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, B, info)
+    S = _stack([CS.CSR(rp.numel() - 1, n, rp, c, v) for rp, c, v, *_ in got], n)
+    assert all(g[5] > 0 for g in got), "bitmap path not taken on some rank"
+    assert sum(g[3] for g in got) == info.flops and sum(g[4] for g in got) == info.nnz
+    assert torch.equal(S.rowptr, C.rowptr.cpu()) and torch.equal(S.col, C.col.cpu())
+    assert torch.allclose(S.val, C.val.cpu(), rtol=1e-5, atol=1e-6)
+
+
+def _rmat_build(world: int, device: str, scale: int = 10):
+    def body(comm):
+        p = MS.RmatProblem.build(scale, 8, comm, seed=3, chunk=1 << 11)
+        Bt = p.right_operand(comm)
+        return p.rows, p.A.to("cpu"), p.At.to("cpu"), Bt.to("cpu")
+
+    return run_loopback(world, body, device=device, timeout_s=300)
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_loopback_rmat_build_device_shuffles(device):
+    """R-MAT build (all-to-all-v edge shuffle to product-balanced panels,
+    distributed transpose, all-gathered A^T) at W = 4 equals W = 1."""
+    one = _rmat_build(1, device)[0]
+    four = _rmat_build(4, device)
+    A1 = one[1]
+    A4 = _stack([g[1] for g in four], A1.n)
+    assert torch.equal(A4.rowptr, A1.rowptr) and torch.equal(A4.col, A1.col)
+    At4 = _stack([g[2] for g in four], A1.n)
+    At1 = one[2]
+    assert torch.equal(At4.rowptr, At1.rowptr) and torch.equal(At4.col, At1.col)
+    for g in four:   # every rank's gathered right operand is the whole A^T
+        assert torch.equal(g[3].rowptr, At1.rowptr) and torch.equal(g[3].col, At1.col)
+    assert torch.equal(At1.to_dense(), A1.to_dense().t())
+
+
+def _write_lines(path, header, lines):
+    with open(path, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n" + header + "\n" + "\n".join(lines) + "\n")
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_mtx_partial_read_same_rules_as_one_rank(tmp_path, world):
+    """Loopback ranks: a file with trailing entries past the header's nnz
+    gives the same matrix at any P; a truncated file is rejected by every
+    rank (not accepted silently at P > 1)."""
+    g = torch.Generator().manual_seed(5)
+    lines = [f"{int(r) + 1} {int(c) + 1} {float(v)!r}" for r, c, v in
+             zip(torch.randint(0, 40, (120,), generator=g), torch.randint(0, 30, (120,), generator=g),
+                 torch.rand(120, generator=g))]
+    extra = str(tmp_path / "extra.mtx")
+    _write_lines(extra, "40 30 100", lines)          # 20 entries past nnz: ignored
+    short = str(tmp_path / "short.mtx")
+    _write_lines(short, "40 30 130", lines)          # 10 entries missing: rejected
+    ref = mtx.read_mtx(extra)
+
+    def body(comm):
+        A, row0, cuts = MS.read_mtx_rowblock(extra, comm)
+        return row0, A
+
+    parts = run_loopback(world, body, timeout_s=60)
+    S = _stack([A for _, A in parts], 30)
+    assert torch.equal(S.rowptr, ref.rowptr) and torch.equal(S.col, ref.col) and torch.equal(S.val, ref.val)
+
+    def bad(comm):
+        try:
+            MS.read_mtx_rowblock(short, comm)
+        except mtx.MtxError as e:
+            return str(e)
+        return None
+
+    with pytest.raises(mtx.MtxError, match="expected 390"):   # (tokens: 3 per entry)
+        mtx.read_mtx(short)
+    errs = run_loopback(world, bad, timeout_s=60)
+    assert all(e is not None and "expected 130" in e for e in errs), errs
+
+
+def test_mtx_truncated_gloo_four_ranks(tmp_path):
+    """The same rejection on 4 gloo processes through the command line."""
+    g = torch.Generator().manual_seed(6)
+    lines = [f"{int(r) + 1} {int(c) + 1} 1.5" for r, c in
+             zip(torch.randint(0, 50, (200,), generator=g), torch.randint(0, 50, (200,), generator=g))]
+    a = str(tmp_path / "A.mtx")
+    _write_lines(a, "50 50 260", lines)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr=127.0.0.1", "--master-port=29731", "-m", "spmm_amd.apps.spgemm", "mult", a, "--aat",
+           "-o", str(tmp_path / "C.mtx"), "--device", "cpu", "--comm", "gloo"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode != 0
+    assert "expected 260" in r.stderr
+
+
+def test_bench_self_launch_two_ranks():
+    """``bench.py --gpus 2`` with no launcher starts two ranks itself and
+    reports n_gpus 2 with the same whole-job work as one rank (here on CPUs
+    with gloo and a small problem; on a GPU box the same flags rehearse two
+    ranks on one card)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    recs = {}
+    for n in (1, 2):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--backend", "gloo",
+                            "--steps", "1", "--warmup", "0", "--matrix-n", "4096", "--matrix-density", "0.004"],
+                           env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(js) == 1, r.stdout   # exactly one JSON line (rank 0)
+        recs[n] = json.loads(js[0])
+    assert recs[2]["n_gpus"] == 2 and recs[1]["n_gpus"] == 1
+    assert recs[2]["flops_per_step"] == recs[1]["flops_per_step"] and recs[2]["nnz_C"] == recs[1]["nnz_C"]
+
+
+def test_bench_world_mismatch_fails():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", WORLD_SIZE="3", RANK="0",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "world size 3 != --gpus 2" in r.stderr

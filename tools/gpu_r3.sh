@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-3 GPU check: distributed-device tests (loopback ranks on one GPU), the
+# full GPU suite, smoke, the headline bench at 1 rank and at 2 gloo ranks on the
+# one card (self-launched by bench.py --gpus 2).  STEPS selects what runs.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out/${TAG:-r3}
+mkdir -p $O
+cd $R
+for st in ${STEPS:-dist gpu smoke bench bench2}; do
+  case $st in
+    dist)
+      echo "== pytest dist-device"
+      timeout -k 10 600 python -u -m pytest tests/test_dist_device.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_dist.log 2>&1 || { tail -30 $O/pytest_dist.log; exit 1; }
+      grep -E "passed|failed" $O/pytest_dist.log | tail -2 ;;
+    gpu)
+      echo "== pytest gpu (all)"
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYARGS} > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error|passed|failed" $O/pytest_gpu.log | tail -20; exit 1; }
+      grep -E "passed|failed" $O/pytest_gpu.log | tail -2 ;;
+    smoke)
+      echo "== smoke"
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    bench)
+      echo "== bench 1 rank"
+      timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/bench1.log 2>&1 || { tail -20 $O/bench1.log; exit 1; }
+      grep '"metric"' $O/bench1.log > $O/bench1.json; cut -c1-300 $O/bench1.json ;;
+    bench2)
+      echo "== bench 2 gloo ranks, self-launched"
+      timeout -k 10 600 python -u bench.py --gpus 2 --backend gloo --steps 2 --warmup 1 ${BENCH_ARGS} > $O/bench2.log 2>&1 || { tail -20 $O/bench2.log; exit 1; }
+      grep '"metric"' $O/bench2.log > $O/bench2.json; cut -c1-300 $O/bench2.json ;;
+    wl)
+      for wl in ${WLS:-spgemm64k spmm rmat chain}; do
+        echo "== bench $wl"
+        args="--steps 5 --warmup 2"
+        [ $wl = rmat ] && args="--steps 2 --warmup 1"
+        timeout -k 10 600 python -u bench.py --workload $wl $args > $O/bench_$wl.log 2>&1 || { tail -20 $O/bench_$wl.log; exit 1; }
+        grep '"metric"' $O/bench_$wl.log > $O/bench_$wl.json; cut -c1-300 $O/bench_$wl.json
+      done ;;
+  esac
+done
