@@ -54,14 +54,42 @@ def _run(cmd: list[str]) -> None:
 
 def build_hip(force: bool = False, verbose: bool = False, out: str = HIP_LIB, extra=()) -> str:
     """``out`` / ``extra``: a diagnostic variant (e.g. ``-DSPMM_BM_STAMPS``)
-    built next to the real library; load it with ``SPMM_HIP_LIB=<path>``."""
+    built next to the real library; load it with ``SPMM_HIP_LIB=<path>``.
+
+    Every kernel file is compiled to its own object in parallel (one device
+    code object per translation unit), objects are reused while their source
+    and the shared headers are older, then one link."""
+    from concurrent.futures import ThreadPoolExecutor
+
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    deps = srcs + glob.glob(os.path.join(CSRC, "kernels", "*.hpp"))
+    hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.hpp"))
+    deps = srcs + hdrs
     if force or _stale(out, deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
+        tag = "" if out == HIP_LIB else "_" + os.path.splitext(os.path.basename(out))[0]
+        obj_dir = os.path.join(LIB_DIR, "obj" + tag)
+        os.makedirs(obj_dir, exist_ok=True)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+                 "-munsafe-fp-atomics", *extra]
+        flag_file = os.path.join(obj_dir, "flags")
+        same_flags = os.path.exists(flag_file) and open(flag_file).read() == " ".join(flags)
+
+        def obj(src):
+            o = os.path.join(obj_dir, os.path.basename(src) + ".o")
+            if force or not same_flags or _stale(o, [src] + hdrs):
+                cmd = [_hipcc(), *flags, "-c", src, "-o", o + ".tmp"]
+                if verbose:
+                    print(" ".join(cmd))
+                _run(cmd)
+                os.replace(o + ".tmp", o)
+            return o
+
+        with ThreadPoolExecutor(max_workers=min(len(srcs), max(1, (os.cpu_count() or 4) - 1))) as ex:
+            objs = list(ex.map(obj, srcs))
+        with open(flag_file, "w") as f:
+            f.write(" ".join(flags))
         tmp = out + ".tmp"
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-fvisibility=hidden", "-munsafe-fp-atomics", *extra, "-o", tmp] + srcs
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
         if verbose:
             print(" ".join(cmd))
         _run(cmd)

@@ -146,6 +146,60 @@ __device__ unsigned long long g_bm_stamps[8];
 #define BM_STAMP_FLUSH() do {} while (0)
 #endif
 
+// ---- deterministic mode (DET kernels) ---------------------------------------
+// The fast path folds a column's products into its output slot with LDS float
+// atomics, so with three or more products per slot the fp32 sum depends on
+// the atomics' order.  One product needs no add, and two commute exactly
+// (fl(a + b) = fl(b + a)), so only slots of >= 3 products are order-
+// sensitive; they are rare (~0.03 per unit at the 1M config).  DET kernels
+// mark them in the slot's column word (columns < 2^30: bits 30 / 31 free):
+//   bit 31 (kDupBit): the slot has received a duplicate; a duplicate that
+//          finds it already set means >= 3 products -> the unit is "fixed";
+//   bit 30 (kOwnBit): reload kernel only (no owner store): a product has
+//          claimed the slot.
+// Fix: every product of a marked slot appends {slot << 17 | key, value} to a
+// small LDS list (key = its position in the unit's Gustavson order: chunk
+// index << lg | lane in chunk, < 2^17), and wave 0 re-sums each listed slot
+// in key order.  The result is then the sequential Gustavson sum
+// (A entries in order, B entries in order), bit for bit: the CPU engine's
+// order.  A unit whose list would overflow is deferred (fast kernels) or
+// flagged (reload: err bit 4 -> the host recomputes the product on the CPU
+// engine, same order).
+constexpr uint32_t kDupBit = 1u << 31, kOwnBit = 1u << 30, kColMask = (1u << 30) - 1u;
+constexpr uint32_t kKeyBits = 17, kKeyMask = (1u << kKeyBits) - 1u;
+
+// wave-level: re-sum the n listed products per slot in key order into items
+__device__ __forceinline__ void bm_det_sum(const uint2* list, int n, unsigned long long* items, int lane) {
+  for (int i = lane; i < n; i += 64) {
+    const uint2 e = list[i];
+    const uint32_t slot = e.x >> kKeyBits, key = e.x & kKeyMask;
+    bool head = true;   // the slot's first product in key order sums the slot
+    for (int j = 0; j < n; ++j) {
+      const uint32_t f = list[j].x;
+      head &= !((f >> kKeyBits) == slot && (f & kKeyMask) < key);
+    }
+    if (!head) continue;
+    float s = __uint_as_float(e.y);
+    uint32_t cur = key;
+    for (;;) {
+      uint32_t best = 0xFFFFFFFFu;
+      float bv = 0.f;
+      for (int j = 0; j < n; ++j) {
+        const uint2 f = list[j];
+        const uint32_t fk = f.x & kKeyMask;
+        if ((f.x >> kKeyBits) == slot && fk > cur && fk < best) {
+          best = fk;
+          bv = __uint_as_float(f.y);
+        }
+      }
+      if (best == 0xFFFFFFFFu) break;
+      s += bv;
+      cur = best;
+    }
+    reinterpret_cast<float*>(&items[slot])[1] = s;
+  }
+}
+
 // One instantiation's geometry.  MODE 0: count (NSUB windows per unit);
 // 1: numeric, products held in R register rounds; 2: numeric reload
 // (deferred units, B re-read in pass 2).
@@ -187,13 +241,18 @@ struct BmArgs {
                            // bit 2: deferred list full (host falls back)
 };
 
-template <int LGW, int NSUB, int NT, int PCAP, int R, int CCAP, int MODE>
+template <int LGW, int NSUB, int NT, int PCAP, int R, int CCAP, int MODE, bool DET = false>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   using Gm = BmGeom<LGW, NSUB, NT, PCAP, R, CCAP, MODE>;
   constexpr int NW = NT / 64;
   constexpr bool VALUES = MODE != 0;
   constexpr int NWORD = Gm::NWORD, WPW = Gm::WPW, WPT = Gm::WPT;
   constexpr int RR = MODE == 1 ? R : (MODE == 0 ? 16 : 8);   // rounds of loads in flight per block
+  // deterministic fix-up list: the fast kernel defers a unit that overflows
+  // it to the reload kernel, whose list is larger (it has one CU's LDS)
+  constexpr int LCAP = !DET ? 1 : (MODE == 2 ? 1024 : 64);
+  static_assert(!DET || MODE != 0, "DET: numeric kernels only");
+  static_assert(!DET || (CCAP << 6) <= (1 << kKeyBits), "DET keys fit 17 bits");
 
   // LDS.  bm: the window's column bitmap.  pre16: exclusive rank prefix of
   // every 64-bit word.  items: (column, value) of every output slot.
@@ -203,9 +262,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned long long items[VALUES ? PCAP : 1];
   using Desc = typename std::conditional<VALUES, uint4, uint2>::type;
   __shared__ __attribute__((aligned(16))) Desc desc[CCAP];
+  __shared__ __attribute__((aligned(8))) uint2 dlist[LCAP];
   __shared__ int wsum[2 * NW];
   __shared__ int scnt[NSUB];
-  __shared__ int sdup;
+  __shared__ int sdup, sfix, snl;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -231,7 +291,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   };
   clear_bm();
   if (tid < NSUB) scnt[tid] = 0;
-  if (tid == 0) sdup = 0;
+  if (tid == 0) {
+    sdup = 0;
+    sfix = 0;
+    snl = 0;
+  }
 
   // Unit schedule.  Count / numeric: static and persistent; iteration k of
   // workgroup g takes unit k * gridDim + perm(g), perm putting consecutive
@@ -636,37 +700,101 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         }
         if (any_dup) {   // uniform
           __syncthreads();
+          if constexpr (DET) {   // duplicates mark their slot; a second duplicate flags the unit
+            bool tri = false;
 #pragma unroll
-          for (int d = 0; d < RR; ++d)
-            if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+            for (int d = 0; d < RR; ++d)
+              if ((dupm >> d) & 1u) {
+                unsigned long long* it = &items[rank(c[d])];
+                tri |= (atomicOr(reinterpret_cast<uint32_t*>(it), kDupBit) & kDupBit) != 0u;
+                atomicAdd(reinterpret_cast<float*>(it) + 1, v[d]);
+              }
+            if (tri) sfix = 1;
+          } else {
+#pragma unroll
+            for (int d = 0; d < RR; ++d)
+              if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+          }
         }
       } else {
         // reload: B re-read; every product adds into a zeroed slot
         for (int i = tid; i < total; i += NT) items[i] = 0ull;
         __syncthreads();
+        bool tri = false;
         for (int i0 = 0; i0 < nr; i0 += RR) {
           fetch(i0, nr, TC, clo);
 #pragma unroll
           for (int d = 0; d < RR; ++d) {
             if (c[d] >= 0) {
               const int rr = rank(c[d]);
-              reinterpret_cast<uint32_t*>(&items[rr])[0] = (uint32_t)(c[d] + clo);
+              uint32_t* cw = reinterpret_cast<uint32_t*>(&items[rr]);
+              if constexpr (DET) {   // first product claims the slot, a third one flags the unit
+                if (atomicOr(cw, (uint32_t)(c[d] + clo) | kOwnBit) & kOwnBit)
+                  tri |= (atomicOr(cw, kDupBit) & kDupBit) != 0u;
+              } else {
+                cw[0] = (uint32_t)(c[d] + clo);
+              }
               atomicAdd(reinterpret_cast<float*>(&items[rr]) + 1, v[d]);
             }
           }
         }
+        if (DET && tri) sfix = 1;
       }
       __syncthreads();
+      bool skip = false;
+      if constexpr (DET) {
+        if (sfix) {   // uniform, rare: re-sum the slots of >= 3 products in Gustavson order
+          auto append = [&](int i0) {
+#pragma unroll
+            for (int d = 0; d < RR; ++d) {
+              if (c[d] >= 0) {
+                const int rr = rank(c[d]);
+                if (reinterpret_cast<const uint32_t*>(&items[rr])[0] & kDupBit) {
+                  const int at = atomicAdd(&snl, 1);
+                  const uint32_t key = ((uint32_t)(gid + (i0 + d) * ngrp) << lg) | (uint32_t)gl;
+                  if (at < LCAP) dlist[at] = make_uint2(((uint32_t)rr << kKeyBits) | key, __float_as_uint(v[d]));
+                }
+              }
+            }
+          };
+          if constexpr (MODE == 1) {
+            append(0);
+          } else {
+            for (int i0 = 0; i0 < nr; i0 += RR) {   // the products again (B re-read)
+              fetch(i0, nr, TC, clo);
+              append(i0);
+            }
+          }
+          __syncthreads();
+          const int nl = snl;
+          if (nl <= LCAP && w == 0) bm_det_sum(dlist, nl, items, lane);
+          skip = nl > LCAP;
+          if (skip && tid == 0) {
+            if (MODE == 1) {   // the reload kernel redoes the unit with a larger list
+              const uint32_t at = atomicAdd(p.novf, 1u);
+              if ((int64_t)at < p.ovf_cap) p.ovf[at] = h.u;
+              else atomicOr(p.err, 4);
+            } else {
+              atomicOr(p.err, 16);   // the host recomputes the product on the CPU engine
+            }
+          }
+          __syncthreads();
+          if (tid == 0) {
+            sfix = 0;
+            snl = 0;
+          }
+        }
+      }
       BM_STAMP(3);
       // ---- the unit's slots to C at its final offset; clear the bitmap -----
-      int lim = total;
-      if (want != total || off < 0 || off + total > p.cap) {   // never write outside the unit or C
+      int lim = skip ? 0 : total;
+      if (!skip && (want != total || off < 0 || off + total > p.cap)) {   // never write outside the unit or C
         if (tid == 0) atomicOr(p.err, 2);
         lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : (int)want);
       }
       for (int i = tid; i < lim; i += NT) {
         const unsigned long long it = items[i];
-        p.Cci[off + i] = (int32_t)(uint32_t)it;
+        p.Cci[off + i] = (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu));
         p.Cv[off + i] = __uint_as_float((uint32_t)(it >> 32));
       }
       clear_bm();
@@ -707,21 +835,24 @@ __device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb
   return b;
 }
 
-template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV>
+template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int RR = R;
+  constexpr int LCAP = DET ? 256 : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
   static_assert(WPW % 64 == 0 && PCAP < 65536, "geometry");
+  static_assert(!DET || (CCAP << 6) <= (1 << kKeyBits), "DET keys fit 17 bits");
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
   __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];   // chunk: {first B index, valid lanes}
   __shared__ float dval[CCAP];                                 //        a(i, j)
+  __shared__ __attribute__((aligned(8))) uint2 dlist[LCAP];
   __shared__ int wsum[2 * NW];
-  __shared__ int sdup;
+  __shared__ int sdup, sfix, snl;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -740,7 +871,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
     for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
   };
   clear_bm();
-  if (tid == 0) sdup = 0;
+  if (tid == 0) {
+    sdup = 0;
+    sfix = 0;
+    snl = 0;
+  }
 
   const int64_t NG = gridDim.x;
   const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
@@ -1016,21 +1151,63 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       }
       if (any_dup) {   // uniform
         __syncthreads();
+        if constexpr (DET) {   // duplicates mark their slot; a second duplicate flags the unit
+          bool tri = false;
 #pragma unroll
-        for (int d = 0; d < RR; ++d)
-          if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+          for (int d = 0; d < RR; ++d)
+            if ((dupm >> d) & 1u) {
+              unsigned long long* it = &items[rank(c[d])];
+              tri |= (atomicOr(reinterpret_cast<uint32_t*>(it), kDupBit) & kDupBit) != 0u;
+              atomicAdd(reinterpret_cast<float*>(it) + 1, v[d]);
+            }
+          if (tri) sfix = 1;
+        } else {
+#pragma unroll
+          for (int d = 0; d < RR; ++d)
+            if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+        }
       }
       __syncthreads();
+      bool skip = false;
+      if constexpr (DET) {
+        if (sfix) {   // uniform, rare: re-sum the slots of >= 3 products in Gustavson order
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            if (c[d] >= 0) {
+              const int rr = rank(c[d]);
+              if (reinterpret_cast<const uint32_t*>(&items[rr])[0] & kDupBit) {
+                const int at = atomicAdd(&snl, 1);
+                const uint32_t key = ((uint32_t)(gid + d * ngrp) << lg) | (uint32_t)gl;
+                if (at < LCAP) dlist[at] = make_uint2(((uint32_t)rr << kKeyBits) | key, __float_as_uint(v[d]));
+              }
+            }
+          }
+          __syncthreads();
+          const int nl = snl;
+          if (nl <= LCAP && w == 0) bm_det_sum(dlist, nl, items, lane);
+          skip = nl > LCAP;   // too many: the reload kernel redoes the unit
+          if (skip && tid == 0) {
+            const uint32_t at = atomicAdd(p.novf, 1u);
+            if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
+            else atomicOr(p.err, 4);
+          }
+          __syncthreads();
+          if (tid == 0) {
+            sfix = 0;
+            snl = 0;
+          }
+        }
+      }
       BM_STAMP(3);
       // ---- write-out -----------------------------------------------------
-      int lim = total;
-      if (want != total || off < 0 || off + total > p.cap) {   // never write outside the unit or C
+      int lim = skip ? 0 : total;
+      if (!skip && (want != total || off < 0 || off + total > p.cap)) {   // never write outside the unit or C
         if (tid == 0) atomicOr(p.err, 2);
         lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : want);
       }
       for (int i = tid; i < lim; i += NT) {
         const unsigned long long it = items[i];
-        p.Cci[off + i] = (int32_t)(uint32_t)it;
+        p.Cci[off + i] = (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu));
         p.Cv[off + i] = __uint_as_float((uint32_t)(it >> 32));
       }
       clear_bm();
@@ -1684,6 +1861,9 @@ struct BmKernels {
                                          K.rounds_fast * (kFastNT / 16), 1>;
   static constexpr int kReloadNT = reload_nt(K.lgw);
   static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, kReloadPcap, 8, kReloadCcap, 2>;
+  static constexpr auto fast_det = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
+                                             K.rounds_fast * (kFastNT / 16), 1, true>;
+  static constexpr auto reload_det = spgemm_bm<K.lgw, 1, kReloadNT, kReloadPcap, 8, kReloadCcap, 2, true>;
 };
 
 template <typename K>
@@ -1709,8 +1889,10 @@ template <int C>
 struct BmRowKernel {
   static constexpr BmCfg K = kCfgs[C];
   static constexpr int R = K.rounds_fast > SPMM_BM_ROWS_R ? SPMM_BM_ROWS_R : K.rounds_fast;   // (the row pipeline's registers cost rounds)
-  static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false>;
-  static constexpr auto kcv = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true>;
+  static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false, false>;
+  static constexpr auto kcv = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true, false>;
+  static constexpr auto k_det = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false, true>;
+  static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true, true>;
 };
 
 template <typename Kern>
@@ -1763,10 +1945,11 @@ struct BmPipeKernel {
 };
 
 
-// pipe: the software-pipelined kernel (needs nwin >= 4 for its row pipeline)
+// pipe: the software-pipelined kernel (needs nwin >= 4 for its row pipeline);
+// det: the deterministic kernels (fixed summation order; not with pipe)
 template <int C>
-int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, hipStream_t s) {
-  if (pipe) {
+int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, int det, hipStream_t s) {
+  if (pipe && !det) {
     const int rc = launch_rows(BmPipeKernel<C>::k, ra, s);
     if (rc) return rc;
   } else {   // passes > 0: window-major, one launch per `passes` windows
@@ -1775,17 +1958,23 @@ int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, hipStream_t s) {
     for (int q = 0; q < nwin; q += step) {
       ra.q0 = q;
       ra.q1 = q + step < nwin ? q + step : nwin;
-      const int rc = ra.a.Bcv ? launch_rows(BmRowKernel<C>::kcv, ra, s) : launch_rows(BmRowKernel<C>::k, ra, s);
+      using K = BmRowKernel<C>;
+      const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s) : launch_rows(K::k_det, ra, s))
+                         : (ra.a.Bcv ? launch_rows(K::kcv, ra, s) : launch_rows(K::k, ra, s));
       if (rc) return rc;
     }
   }
-  return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
+  return det ? launch_bm(BmKernels<C>::reload_det, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s)
+             : launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
 }
 
 template <int C>
-int bm_numeric(int64_t work, const BmArgs& a, hipStream_t s) {
-  const int rc = launch_bm(BmKernels<C>::fast, kFastNT, work, a, s);
-  return rc ? rc : launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, a, s);
+int bm_numeric(int64_t work, const BmArgs& a, int det, hipStream_t s) {
+  using K = BmKernels<C>;
+  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s);
+  if (rc) return rc;
+  return det ? launch_bm(K::reload_det, K::kReloadNT, int64_t(1) << 30, a, s)
+             : launch_bm(K::reload, K::kReloadNT, int64_t(1) << 30, a, s);
 }
 
 // integer knob from the environment (read once per name by the caller's static)
@@ -1840,19 +2029,22 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
 
 // Numeric: the fast kernel over every unit, then the reload kernel over the
 // units it deferred (novf must be zero; ovf has room for ovf_cap units).
+// det: fixed summation order (see "deterministic mode"); err bit 4 then
+// means a unit needs the CPU engine.
 SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                        const uint32_t* ws, const int32_t* Bci, const float* Bv, int64_t m, int nwin,
                                        int lg, const int64_t* uoff, int64_t cap, int32_t* Cci, float* Cv,
-                                       int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, void* stream) {
+                                       int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, int det,
+                                       void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
   BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, nullptr, err};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * nwin;
   switch (cfg) {
-    case 0: return bm_numeric<0>(work, a, s);
-    case 1: return bm_numeric<1>(work, a, s);
-    default: return bm_numeric<2>(work, a, s);
+    case 0: return bm_numeric<0>(work, a, det, s);
+    case 1: return bm_numeric<1>(work, a, det, s);
+    default: return bm_numeric<2>(work, a, det, s);
   }
 }
 
@@ -1892,7 +2084,7 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
                                             const void* Bcv,
                                             int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap,
                                             int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                                            int32_t* err, int pipe, void* stream) {
+                                            int32_t* err, int pipe, int det, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   if (pipe && (nwin < 4 || lg > 5)) return (int)hipErrorInvalidValue;   // (+ B.nnz < 2^27: host)
@@ -1902,9 +2094,9 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
   hipStream_t s = (hipStream_t)stream;
   const int passes = bm_env_int("SPMM_BM_NUM_PASS_WINDOWS", 0);
   switch (cfg) {
-    case 0: return bm_numeric_rows<0>(ra, pipe, passes, s);
-    case 1: return bm_numeric_rows<1>(ra, pipe, passes, s);
-    default: return bm_numeric_rows<2>(ra, pipe, passes, s);
+    case 0: return bm_numeric_rows<0>(ra, pipe, passes, det, s);
+    case 1: return bm_numeric_rows<1>(ra, pipe, passes, det, s);
+    default: return bm_numeric_rows<2>(ra, pipe, passes, det, s);
   }
 }
 

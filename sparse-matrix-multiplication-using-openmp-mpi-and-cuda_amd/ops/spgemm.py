@@ -60,14 +60,14 @@ _native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, 
 _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, C_INT, c_vp, c_vp,
                      c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
+                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp,
                      c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
-                     C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp)
+                     C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -98,6 +98,7 @@ class SpgemmInfo:
     rows_per_bin_num: Dict[int, int] = field(default_factory=dict)
     resorted_rows: int = 0
     partial_nnz: int = 0      # innerdim_spgemm: nnz of this rank's full-height partial before the merge
+    deterministic: bool = False   # C's fp32 sums were formed in a fixed (Gustavson) order
     mean_seg: float = 0.0     # mean B-row length per A entry (products / nnz(A)); picks the LDS lane groups
 
 
@@ -437,6 +438,9 @@ def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, two_phase: bool = Fa
             if C_ is not None:
                 return C_
             info.rows_per_bin_num = {}
+        if CONFIG.spgemm_deterministic >= 2:   # strict: no unordered GPU path
+            info.rows_per_bin_num["det_cpu_fallback"] = 1
+            return _det_cpu(A, B_ready() if B_ready is not None else B, info)
         if CONFIG.spgemm_onepass == "auto" or CONFIG.spgemm_ordered == "auto":
             pre["free"] = _FreeMem(A.device)
         mode = _onepass_mode(info.flops // 2, A.device, pre_free=pre.get("free"))
@@ -683,6 +687,7 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         return None
     if B_ready is not None:   # columns only: the values may still be in flight (two-stage gather)
         B = getattr(B_ready, "cols", B_ready)()
+    det = CONFIG.spgemm_deterministic > 0
     lib = _native.hip()
     P = _native.ptr
     st = _native.stream_ptr(dev)
@@ -741,24 +746,40 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
                                                       lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
-                                                      P(novf), ovf_cap, P(err), int(pipe), st),
+                                                      P(novf), ovf_cap, P(err), int(pipe and not det), int(det), st),
                       "spgemm_bm_numeric_rows")
-        info.rows_per_bin_num["bitmap_rows"] = 2 if pipe else 1
+        info.rows_per_bin_num["bitmap_rows"] = 2 if pipe and not det else 1
     else:
         _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
                                                  nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap,
-                                                 P(err), st), "spgemm_bm_numeric")
+                                                 P(err), int(det), st), "spgemm_bm_numeric")
     e, deferred = z.tolist()
     info.rows_per_bin_num["bitmap_units"] = nunits
     info.rows_per_bin_num["bitmap_cfg"] = cfg
     info.rows_per_bin_num["bitmap_deferred"] = deferred
     if e & 2:
         raise RuntimeError("spgemm bitmap: numeric and count kernels disagree (kernel invariant violated)")
+    if det and e & 21:
+        # a unit beyond every deterministic kernel's budget (adversarial column
+        # collisions): the CPU engine sums in the same (Gustavson) order
+        info.rows_per_bin_num["det_cpu_fallback"] = 1
+        del Cci, Cv
+        return _det_cpu(A, B, info)
     if e & 5:
         info.rows_per_bin_num["bitmap_fallback"] = 1
         return None
+    info.deterministic = bool(det)
     rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
     return CSR(m, B.n, rowptr, Cci, Cv)
+
+
+def _det_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:
+    """Deterministic product on the CPU engine (sequential Gustavson order,
+    the order the deterministic GPU kernels reproduce), back on A's device."""
+    dev = A.device
+    C_ = _spgemm_cpu(A.to("cpu"), B.to("cpu"), info)
+    info.deterministic = True
+    return C_.to(dev)
 
 
 PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper

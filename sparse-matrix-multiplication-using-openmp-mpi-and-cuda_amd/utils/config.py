@@ -51,6 +51,10 @@ class Config:
     spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
     # windows per row-major count unit (1: 16 KB bitmaps, 8 per CU; 2: 32 KB, 4 per CU)
     spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
+    # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU
+    # engine) on the bitmap-rank path: 0 = off, 1 = on (other GPU paths stay unordered), 2 = strict
+    # (a product no deterministic GPU kernel covers runs on the CPU engine)
+    spgemm_deterministic: int = field(default_factory=lambda: _env("SPMM_SPGEMM_DETERMINISTIC", 0, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     # long-row routing histogram reads a chunk-offset table for the long rows of B (1) or their columns (0)
     spgemm_long_btab: int = field(default_factory=lambda: _env("SPMM_SPGEMM_LONG_BTAB", 1, int))

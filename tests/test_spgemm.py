@@ -927,3 +927,109 @@ def test_spgemm_gpu_oom_falls_back_to_two_phase(monkeypatch):
     assert info.rows_per_bin_num.get("oom_fallback") == 1
     assert torch.equal(C.rowptr, ref.rowptr) and torch.equal(C.col, ref.col)
     assert torch.allclose(C.val, ref.val, atol=1e-5, rtol=1e-5)
+
+
+def _rows_subset(A, rows):
+    """CSR of the given rows of A (host)."""
+    Arp, Aci, Av = A.rowptr.cpu(), A.col.cpu(), A.val.cpu()
+    lens = Arp[rows + 1] - Arp[rows]
+    idx = torch.repeat_interleave(Arp[rows], lens) + (torch.arange(int(lens.sum())) -
+                                                       torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens))
+    rp = torch.zeros(rows.numel() + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=rp[1:])
+    return CS.CSR(rows.numel(), A.n, rp, Aci[idx], Av[idx])
+
+
+def _digest(t: torch.Tensor) -> int:
+    """Order-sensitive digest of a tensor's bits, chunked (C of the 1M product
+    is 46 GB of values)."""
+    bits = t.view(torch.int32)
+    acc = 0
+    step = 1 << 27
+    for s in range(0, bits.numel(), step):
+        x = bits[s:s + step].long()
+        w = (torch.arange(s, s + x.numel(), device=x.device) % 1000003) + 1
+        acc = (acc + int((x * w).sum())) & ((1 << 64) - 1)
+    return acc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["rows_cfg0", "rows_cfg1", "generic", "collide_fast", "collide_reload",
+                                  "collide_cpu"])
+def test_spgemm_gpu_deterministic_equals_cpu_order(monkeypatch, case):
+    """Deterministic mode (SPMM_SPGEMM_DETERMINISTIC=1): the bitmap kernels sum
+    every output in Gustavson order, so C equals the CPU engine's result value
+    for value, and two runs are bitwise equal.  Cases: the row-major kernel
+    (two window configurations), the per-unit kernel, heavy column collisions
+    (the >= 3-product fix-up in the fast kernel, in the reload kernel, and its
+    CPU fallback when even the reload list overflows)."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    monkeypatch.setattr(CONFIG, "spgemm_deterministic", 1)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap", "on")
+    cfg = {"rows_cfg1": 1}.get(case, 0)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_cfg", cfg)
+    if case == "generic":
+        monkeypatch.setattr(CONFIG, "spgemm_bitmap_rows", "off")
+    if case in ("rows_cfg0", "generic"):
+        A = gen_csr.uniform_csr(2000, 20000, 0.002, seed=191, device=dev)
+        B = gen_csr.uniform_csr(20000, 300000, 2.7e-4, seed=192, device=dev)
+    elif case == "rows_cfg1":
+        A = gen_csr.uniform_csr(3000, 10000, 0.006, seed=193, device=dev)
+        B = gen_csr.uniform_csr(10000, 65536, 0.001, seed=194, device=dev)
+    elif case == "collide_fast":    # ~1500 products per row into 20000 columns: pairs and a few triples
+        A = gen_csr.uniform_csr(1500, 4000, 0.01, seed=195, device=dev)
+        B = gen_csr.uniform_csr(4000, 20000, 0.00075, seed=196, device=dev)
+    elif case == "collide_reload":  # ~3000 products per row (> fast capacity) into 20000 columns
+        A = gen_csr.uniform_csr(800, 4000, 0.05, seed=197, device=dev)
+        B = gen_csr.uniform_csr(4000, 20000, 0.00075, seed=198, device=dev)
+    else:                           # ~1500 products into 300 columns: beyond every fix-up list
+        A = gen_csr.uniform_csr(300, 4000, 0.05, seed=199, device=dev)
+        B = gen_csr.uniform_csr(4000, 300, 0.025, seed=200, device=dev)
+    i1 = SG.SpgemmInfo()
+    C1 = SG.spgemm(A, B, i1)
+    C2 = SG.spgemm(A, B)
+    assert i1.deterministic
+    assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+    assert torch.equal(C1.val.view(torch.int32), C2.val.view(torch.int32))
+    R = SG.spgemm(A.to("cpu"), B.to("cpu"))
+    assert torch.equal(C1.rowptr.cpu(), R.rowptr) and torch.equal(C1.col.cpu(), R.col)
+    assert torch.equal(C1.val.cpu(), R.val)   # (value equality: +0.0 == -0.0)
+    bins = i1.rows_per_bin_num
+    if case == "collide_cpu":
+        assert bins.get("det_cpu_fallback") == 1
+    else:
+        assert "det_cpu_fallback" not in bins and bins.get("bitmap_cfg") == cfg
+    if case == "collide_reload":
+        assert bins.get("bitmap_deferred", 0) > 0
+
+
+@pytest.mark.gpu
+def test_spgemm_bench_scale_deterministic_bitwise(monkeypatch):
+    """BASELINE config 4 (1M^2 @ 0.01 %, the headline product) in
+    deterministic mode: two runs give bitwise-equal C, and 2048 sampled rows
+    equal the CPU engine's sequential Gustavson sums value for value."""
+    from spmm_amd.utils.config import CONFIG
+
+    monkeypatch.setattr(CONFIG, "spgemm_deterministic", 1)
+    dev = torch.device("cuda")
+    n, d = 1 << 20, 1e-4
+    A = gen_csr.uniform_csr(n, n, d, seed=1, device=dev)
+    B = gen_csr.uniform_csr(n, n, d, seed=2, device=dev)
+    info = SG.SpgemmInfo()
+    C = SG.spgemm(A, B, info)
+    assert info.deterministic and "bitmap_units" in info.rows_per_bin_num
+    d1, dc1, rp1 = _digest(C.val), _digest(C.col), C.rowptr.clone()
+    g = torch.Generator().manual_seed(3)
+    rows = torch.randint(0, n, (2048,), generator=g).unique()
+    R = SG.spgemm(_rows_subset(A, rows), B.to("cpu"))
+    Crp = C.rowptr.cpu()
+    for t, i in enumerate(rows.tolist()):
+        cs, ce = int(Crp[i]), int(Crp[i + 1])
+        rs, re = int(R.rowptr[t]), int(R.rowptr[t + 1])
+        assert torch.equal(C.col[cs:ce].cpu(), R.col[rs:re]) and torch.equal(C.val[cs:ce].cpu(), R.val[rs:re]), i
+    del C
+    torch.cuda.empty_cache()
+    C = SG.spgemm(A, B)
+    assert torch.equal(C.rowptr, rp1) and _digest(C.col) == dc1 and _digest(C.val) == d1

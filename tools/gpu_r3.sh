@@ -17,6 +17,14 @@ for st in ${STEPS:-dist gpu smoke bench bench2}; do
       echo "== pytest gpu (all)"
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYARGS} > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error|passed|failed" $O/pytest_gpu.log | tail -20; exit 1; }
       grep -E "passed|failed" $O/pytest_gpu.log | tail -2 ;;
+    det)
+      echo "== pytest deterministic"
+      timeout -k 10 600 python -u -m pytest tests/test_spgemm.py -m gpu -k deterministic -x -v --timeout 300 --timeout-method thread > $O/pytest_det.log 2>&1 || { grep -E "FAILED|Error|assert|passed|failed" $O/pytest_det.log | tail -20; exit 1; }
+      grep -E "passed|failed" $O/pytest_det.log | tail -2 ;;
+    benchdet)
+      echo "== bench 1 rank, deterministic"
+      SPMM_SPGEMM_DETERMINISTIC=1 timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/bench1_det.log 2>&1 || { tail -20 $O/bench1_det.log; exit 1; }
+      grep '"metric"' $O/bench1_det.log > $O/bench1_det.json; cut -c1-300 $O/bench1_det.json ;;
     smoke)
       echo "== smoke"
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
