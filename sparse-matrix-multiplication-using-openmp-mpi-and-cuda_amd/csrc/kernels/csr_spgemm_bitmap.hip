@@ -45,6 +45,20 @@
 #define SPMM_BM_SKIP_ROUNDS 1
 #endif
 
+#ifndef SPMM_BM_P1_SPLIT   // row-major numeric pass 1: straight-line bodies of RR/2, RR-2, RR rounds by the unit's need
+#define SPMM_BM_P1_SPLIT 0
+#endif
+
+#ifndef SPMM_BM_NT_STORE   // numeric write-out: non-temporal stores of C (C does not displace B in L2 / MALL;
+#define SPMM_BM_NT_STORE 1   // 1M step 76.55 -> 75.41 ms, 64k 1.755 -> 1.697 ms, same box)
+#endif
+
+#if SPMM_BM_NT_STORE
+#define BM_OUT(ptr, val) __builtin_nontemporal_store((val), (ptr))
+#else
+#define BM_OUT(ptr, val) (*(ptr) = (val))
+#endif
+
 namespace {
 
 // 64-lane inclusive prefix sum on the DPP network (VALU only; no LDS
@@ -794,8 +808,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       }
       for (int i = tid; i < lim; i += NT) {
         const unsigned long long it = items[i];
-        p.Cci[off + i] = (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu));
-        p.Cv[off + i] = __uint_as_float((uint32_t)(it >> 32));
+        BM_OUT(p.Cci + (off + i), (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu)));
+        BM_OUT(p.Cv + (off + i), __uint_as_float((uint32_t)(it >> 32)));
       }
       clear_bm();
       __syncthreads();   // cleared (and items read) before the next unit's pass 1
@@ -991,7 +1005,76 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       __syncthreads();
       BM_STAMP(0);
       // ---- pass 1 ----------------------------------------------------------
+      // (N = rounds compiled in: with SPMM_BM_P1_SPLIT the unit's round count
+      // picks a straight-line body of RR / 2, RR - 2 or RR rounds, so unused
+      // rounds cost no VALU; rounds >= N hold no product)
       const int nr = (TC + ngrp - 1) / ngrp;
+#if SPMM_BM_P1_SPLIT
+      auto pass1 = [&](auto NRc) -> uint32_t {
+        constexpr int N = decltype(NRc)::value;
+        uint2 ds[N];
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+          const int t = gid + d * ngrp;
+          ds[d] = desc[t < TC ? t : TC - 1];
+        }
+        uint32_t f[N];
+        uint32_t okm = 0;
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+          const int t = gid + d * ngrp;
+          const bool ok = (t < TC) & ((uint32_t)gl < ds[d].y);
+          okm |= (ok ? 1u : 0u) << d;
+          f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
+        }
+        int x[N];
+        float b[N];
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+          x[d] = 0;
+          b[d] = 0.f;
+          if (d < nr) {   // wave-uniform
+            if constexpr (CV) {   // one 8-byte load: a chunk's products share cache lines
+              const uint2 e = p.Bcv[f[d]];
+              x[d] = (int)e.x;
+              b[d] = __uint_as_float(e.y);
+            } else {
+              x[d] = p.Bci[f[d]];
+              b[d] = p.Bv[f[d]];
+            }
+          }
+        }
+        // A values while the B loads are in flight
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+          const int t = gid + d * ngrp;
+          v[d] = dval[t < TC ? t : TC - 1];
+        }
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+          c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
+          v[d] *= b[d];
+        }
+#pragma unroll
+        for (int d = N; d < RR; ++d) {
+          c[d] = -1;
+          v[d] = 0.f;
+        }
+        uint32_t dm = 0;
+        uint32_t old[N];
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+          old[d] = 0u;
+          if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
+        }
+#pragma unroll
+        for (int d = 0; d < N; ++d) dm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
+        return dm;
+      };
+      const uint32_t dupm = nr <= RR / 2 ? pass1(std::integral_constant<int, RR / 2>{})
+                            : nr <= RR - 2 ? pass1(std::integral_constant<int, RR - 2>{})
+                                           : pass1(std::integral_constant<int, RR>{});
+#else
       {
         uint2 ds[RR];
 #pragma unroll
@@ -1048,6 +1131,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
 #pragma unroll
         for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
       }
+#endif
       // this unit's B loads have landed, and with them every older load:
       // the next row's registers are ready to be taken
       if (last) take_next();
@@ -1207,8 +1291,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       }
       for (int i = tid; i < lim; i += NT) {
         const unsigned long long it = items[i];
-        p.Cci[off + i] = (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu));
-        p.Cv[off + i] = __uint_as_float((uint32_t)(it >> 32));
+        BM_OUT(p.Cci + (off + i), (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu)));
+        BM_OUT(p.Cv + (off + i), __uint_as_float((uint32_t)(it >> 32)));
       }
       clear_bm();
       __syncthreads();

@@ -31,6 +31,8 @@
 
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -144,6 +146,143 @@ __global__ __launch_bounds__(NT) void spmm_panel_mfma(
   }
 }
 
+// spmm_panel_mfma_db — the panel kernel software-pipelined over chunks
+// ("issue chunk c+1's X-row gather before chunk c's MFMAs, 2
+// barriers instead of 3").  Two A tiles and one X tile in LDS (32 KB: four
+// to five workgroups per CU); chunk c+1's X rows and entries are gathered
+// into registers while chunk c is multiplied:
+//   top of c:  At[c & 1] and Xt hold chunk c, chunk c+1's loads in flight
+//   zero At[(c+1) & 1] (its last reader, chunk c-1's MFMAs, passed the last
+//   barrier); MFMAs of chunk c;                                    barrier
+//   store chunk c+1's rows into Xt, scatter its entries into
+//   At[(c+1) & 1], issue chunk c+2's gathers;                      barrier
+struct ChunkRegs {
+  uint4 xv[4];
+  int rc[2];
+  unsigned short val[2];
+  int nent;
+};
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(NT, 4) void spmm_panel_mfma_db(
+    const int64_t* __restrict__ panel_chunk_ptr, const int32_t* __restrict__ chunk_cols,
+    const int64_t* __restrict__ chunk_ent_ptr, const int32_t* __restrict__ ent_rc,
+    const unsigned short* __restrict__ ent_val, const unsigned short* __restrict__ X, int64_t ldx, int64_t m,
+    void* __restrict__ Yv, int64_t ldy) {
+  __shared__ __attribute__((aligned(16))) unsigned short At[2][PR * CK];   // 2 x 8 KB
+  __shared__ __attribute__((aligned(16))) unsigned char Xt[CK * DB * 2];   // 16 KB, swizzled rows
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t panel = blockIdx.x;
+  const int64_t dcol0 = (int64_t)blockIdx.y * DB;
+  v4f acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int64_t c0 = panel_chunk_ptr[panel], c1 = panel_chunk_ptr[panel + 1];
+  const int gr = tid >> 2, gp = tid & 3;
+  const int sw = xswz(gr);
+
+  // chunk ch's gathers into registers (a chunk past the panel loads nothing)
+  auto issue = [&](int64_t ch, ChunkRegs& r) {
+    r.nent = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.xv[q] = make_uint4(0, 0, 0, 0);
+    if (ch < c1) {
+      const int xr = chunk_cols[ch * CK + gr];
+      if (xr >= 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(X + (int64_t)xr * ldx + dcol0) + gp * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r.xv[q] = src[q];
+      }
+      const int64_t e0 = chunk_ent_ptr[ch], e1 = chunk_ent_ptr[ch + 1];
+      const int64_t ne = e1 - e0;
+      r.nent = (int)(ne > 2 * NT ? 2 * NT : ne);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int64_t e = e0 + tid + k * NT;
+        r.rc[k] = e < e1 ? ent_rc[e] : -1;
+        r.val[k] = e < e1 ? ent_val[e] : (unsigned short)0;
+      }
+      // (> 512 entries in one chunk: the remainder is scattered from memory, see store)
+    }
+  };
+  // chunk ch into LDS: X rows into Xt, entries into tile a
+  auto store = [&](int64_t ch, const ChunkRegs& r, unsigned short* a) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int cbyte = gp * 64 + q * 16;
+      const int chunk = cbyte >> 5, within = cbyte & 31;
+      *reinterpret_cast<uint4*>(Xt + gr * 256 + ((chunk ^ sw) << 5) + within) = r.xv[q];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (r.rc[k] >= 0) a[r.rc[k]] = r.val[k];
+    if (r.nent == 2 * NT) {   // rare: more than 512 entries in the chunk
+      const int64_t e1 = chunk_ent_ptr[ch + 1];
+      for (int64_t e = chunk_ent_ptr[ch] + 2 * NT + tid; e < e1; e += NT) a[ent_rc[e]] = ent_val[e];
+    }
+  };
+  auto zero = [&](unsigned short* a) {
+    reinterpret_cast<uint4*>(a)[tid * 2 + 0] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4*>(a)[tid * 2 + 1] = make_uint4(0, 0, 0, 0);
+  };
+  auto mfma = [&](const unsigned short* a) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const v8bf av = *reinterpret_cast<const v8bf*>(&a[(16 * w + (lane & 15)) * CK + ks * 32 + 8 * (lane >> 4)]);
+      const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+      const int r0 = ks * 32 + 8 * g + q, r1 = r0 + 4;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const unsigned char* p0 = Xt + r0 * 256 + ((t ^ xswz(r0)) << 5) + pp * 8;
+        const unsigned char* p1 = Xt + r1 * 256 + ((t ^ xswz(r1)) << 5) + pp * 8;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p0));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p1));
+        const v8s bs = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const v8bf b = __builtin_bit_cast(v8bf, bs);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b, acc[t], 0, 0, 0);
+      }
+    }
+  };
+
+  ChunkRegs r;
+  // prologue: chunk c0 into LDS (tile 0), chunk c0 + 1's gathers in flight
+  if (c0 < c1) {
+    issue(c0, r);
+    zero(At[0]);
+    __syncthreads();
+    store(c0, r, At[0]);
+    issue(c0 + 1, r);
+    __syncthreads();
+  }
+  for (int64_t ch = c0; ch < c1; ++ch) {
+    const int par = (int)((ch - c0) & 1);
+    zero(At[par ^ 1]);
+    mfma(At[par]);
+    __syncthreads();   // chunk ch's MFMAs done: Xt and tile par free
+    if (ch + 1 < c1) {
+      store(ch + 1, r, At[par ^ 1]);
+      issue(ch + 2, r);   // in flight across the next chunk's MFMAs
+    }
+    __syncthreads();
+  }
+  // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + i
+  const int64_t rbase = panel * PR + 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = rbase + i;
+    if (row >= m) break;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int64_t col = dcol0 + 16 * t + (lane & 15);
+      if (OUT_BF16)
+        reinterpret_cast<unsigned short*>(Yv)[row * ldy + col] = f2bf(acc[t][i]);
+      else
+        reinterpret_cast<float*>(Yv)[row * ldy + col] = acc[t][i];
+    }
+  }
+}
+
 // One wave per row; lane owns columns 2*lane, 2*lane+1 of each 128-column
 // block.  The row's column indices and values are read once, coalesced, 64
 // per lane-round; each entry's X row address is then a readlane (scalar) and
@@ -203,7 +342,241 @@ __global__ __launch_bounds__(NT) void spmm_rowwise(const int64_t* __restrict__ r
   }
 }
 
+// ---- inspector: the panel plan on the device -------------------------------
+// (ops/spmm.py plan_panels; was a chain of torch sort / unique / bincount
+// launches, ~37 ms for the 65536^2 config.)  Per 64-row panel, one workgroup:
+//   count: the size of the panel's column union (an LDS bitmap of a 2^16-
+//          column window, popcounts), per window of the columns it touches;
+//   fill:  the union's sorted columns in chunks of 64 slots (chunk_cols, -1
+//          padding), the entries' (row in panel, slot) grouped by chunk
+//          (chunk_ent_ptr: an LDS count + scan per chunk; inside a chunk the
+//          order is arbitrary: the MFMA kernel scatters into a tile), and the
+//          values as bf16.  A panel's entries keep the index range they have
+//          in A (rp[p*64] ..), so no global scan over entries is needed; the
+//          chunk ranges come from one scan of the union sizes (host side).
+constexpr int PL_LG = 16, PL_W = 1 << PL_LG, PL_WORDS = PL_W / 64;   // 8 KB bitmap window
+constexpr int PL_MAXCH = 1024;                                       // chunks per panel (65536 union columns)
+
+// block-wide exclusive scan of one int per thread (256 threads), + total
+__device__ __forceinline__ int pl_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    pre += i < w ? wsum[i] : 0;
+    tot += wsum[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+struct PlanArgs {
+  const int64_t* rp;
+  const int32_t* ci;
+  const void* av;          // A values: bf16 or fp32
+  int val_f32;
+  int64_t m, n;
+  int64_t* nunion;         // count: [npanels]
+  const int64_t* pcp;      // fill: panel_chunk_ptr [npanels + 1]
+  int32_t* chunk_cols;
+  int64_t* chunk_ent_ptr;  // [nchunks + 1]
+  int32_t* ent_rc;
+  unsigned short* ent_val;
+  int32_t* err;            // bit 0: a panel has more than PL_MAXCH chunks
+};
+
+// One panel per workgroup.  FILL = false: union size only.
+template <bool FILL>
+__global__ __launch_bounds__(NT) void spmm_plan(PlanArgs a) {
+  __shared__ unsigned long long bm[PL_WORDS];
+  __shared__ int pre[PL_WORDS];
+  __shared__ int64_t srp[PR + 1];
+  __shared__ int chcnt[FILL ? PL_MAXCH : 1], chpre[FILL ? PL_MAXCH : 1], chfill[FILL ? PL_MAXCH : 1];
+  __shared__ int wsum[NT / 64];
+  __shared__ int snext;
+
+  const int tid = threadIdx.x;
+  const int64_t panel = blockIdx.x;
+  const int64_t r0 = panel * PR;
+  const int nrows = (int)(a.m - r0 < PR ? a.m - r0 : PR);
+  if (tid <= nrows) srp[tid] = a.rp[r0 + tid];
+  __syncthreads();
+  const int64_t e0 = srp[0], e1 = srp[nrows];
+  const int64_t nwin = (a.n + PL_W - 1) >> PL_LG;
+  int64_t chunk0 = 0;
+  int nch = 0;
+  if constexpr (FILL) {
+    chunk0 = a.pcp[panel];
+    nch = (int)(a.pcp[panel + 1] - chunk0);
+    if (nch > PL_MAXCH) {   // uniform; the host falls back to the torch inspector
+      if (tid == 0) atomicOr(a.err, 1);
+      return;
+    }
+    for (int k = tid; k < nch; k += NT) {
+      chcnt[k] = 0;
+      chfill[k] = 0;
+    }
+  }
+  auto row_of = [&](int64_t e) {   // row in panel of entry e (binary search over the panel's row pointers)
+    int lo = 0, hi = nrows - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (srp[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  // one window: OR its columns, exclusive rank prefix per word (base = union
+  // slots before the window); returns the window's union size
+  auto window = [&](int64_t w, int base) {
+    for (int i = tid; i < PL_WORDS; i += NT) bm[i] = 0ull;
+    __syncthreads();
+    const int64_t lo = w << PL_LG, hi = lo + PL_W;
+    for (int64_t e = e0 + tid; e < e1; e += NT) {
+      const int64_t c = a.ci[e];
+      if (c >= lo && c < hi) {
+        const int cc = (int)(c - lo);
+        atomicOr(&bm[cc >> 6], 1ull << (cc & 63));
+      }
+    }
+    __syncthreads();
+    constexpr int WPT = PL_WORDS / NT;   // 4 words per thread
+    int cnt[WPT], s = 0;
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      cnt[i] = __popcll(bm[tid * WPT + i]);
+      s += cnt[i];
+    }
+    int tot;
+    int p = pl_scan(s, wsum, &tot);
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      pre[tid * WPT + i] = base + p;
+      p += cnt[i];
+    }
+    __syncthreads();
+    return tot;
+  };
+  // next window holding a column of the panel at or after window w (or nwin)
+  auto next_window = [&](int64_t w) {
+    if (tid == 0) snext = 0x7fffffff;
+    __syncthreads();
+    const int64_t lo = w << PL_LG;
+    int best = 0x7fffffff;
+    for (int64_t e = e0 + tid; e < e1; e += NT) {
+      const int64_t c = a.ci[e];
+      if (c >= lo) best = min(best, (int)(c >> PL_LG));
+    }
+    if (best != 0x7fffffff) atomicMin(&snext, best);
+    __syncthreads();
+    const int r = snext;
+    __syncthreads();
+    return r == 0x7fffffff ? nwin : (int64_t)r;
+  };
+  auto rank = [&](int cc) { return pre[cc >> 6] + __popcll(bm[cc >> 6] & ((1ull << (cc & 63)) - 1ull)); };
+
+  int total = 0, nwt = 0;
+  for (int64_t w = next_window(0); w < nwin; w = next_window(w + 1)) {
+    const int base = total;
+    total += window(w, base);
+    ++nwt;
+    if constexpr (FILL) {
+      // the union's columns of this window in slot order
+      constexpr int WPT = PL_WORDS / NT;
+      for (int i = 0; i < WPT; ++i) {
+        const int wd = tid * WPT + i;
+        unsigned long long bits = bm[wd];
+        int slot = pre[wd];
+        while (bits) {
+          const int b = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          a.chunk_cols[chunk0 * 64 + slot] = (int32_t)((w << PL_LG) + wd * 64 + b);
+          ++slot;
+        }
+      }
+      // entries per chunk
+      const int64_t lo = w << PL_LG, hi = lo + PL_W;
+      for (int64_t e = e0 + tid; e < e1; e += NT) {
+        const int64_t c = a.ci[e];
+        if (c >= lo && c < hi) atomicAdd(&chcnt[rank((int)(c - lo)) >> 6], 1);
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (!FILL) {
+    if (tid == 0) a.nunion[panel] = total;
+    return;
+  } else {
+    for (int s = total + tid; s < nch * 64; s += NT) a.chunk_cols[chunk0 * 64 + s] = -1;   // last chunk's padding
+    // chunk entry ranges: the panel's entries keep A's index range [e0, e1)
+    int run = 0;
+    for (int k0 = 0; k0 < nch; k0 += NT) {
+      const int k = k0 + tid;
+      const int v = k < nch ? chcnt[k] : 0;
+      int tot;
+      const int p = pl_scan(v, wsum, &tot);
+      if (k < nch) {
+        chpre[k] = run + p;
+        a.chunk_ent_ptr[chunk0 + k] = e0 + run + p;
+      }
+      run += tot;
+    }
+    if (panel == (int64_t)gridDim.x - 1 && tid == 0) a.chunk_ent_ptr[chunk0 + nch] = e1;
+    __syncthreads();
+    // scatter the entries (the bitmap of the last window is still valid when
+    // the panel touches one window; otherwise every window is rebuilt)
+    int acc = 0;   // rank base of the window: union slots of the windows before it
+    for (int64_t w = next_window(0); w < nwin; w = next_window(w + 1)) {
+      if (nwt > 1) acc += window(w, acc);
+      const int64_t lo = w << PL_LG, hi = lo + PL_W;
+      for (int64_t e = e0 + tid; e < e1; e += NT) {
+        const int64_t c = a.ci[e];
+        if (c >= lo && c < hi) {
+          const int slot = rank((int)(c - lo));
+          const int k = slot >> 6;
+          const int64_t pos = e0 + chpre[k] + atomicAdd(&chfill[k], 1);
+          a.ent_rc[pos] = row_of(e) * 64 + (slot & 63);
+          a.ent_val[pos] = a.val_f32 ? f2bf(reinterpret_cast<const float*>(a.av)[e])
+                                     : reinterpret_cast<const unsigned short*>(a.av)[e];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace
+
+// Inspector, count pass: nunion[p] = size of panel p's column union.
+SPMM_EXPORT int spmm_spmm_plan_count(const int64_t* rp, const int32_t* ci, int64_t m, int64_t n, int64_t* nunion,
+                                     void* stream) {
+  if (m <= 0) return 0;
+  PlanArgs a{rp, ci, nullptr, 0, m, n, nunion, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(spmm_plan<false>, dim3((unsigned)((m + PR - 1) / PR)), dim3(NT), 0, (hipStream_t)stream, a);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Inspector, fill pass (pcp = exclusive scan of ceil(nunion / 64)); err bit 0:
+// a panel has more than 1024 chunks (the host uses the torch inspector).
+SPMM_EXPORT int spmm_spmm_plan_fill(const int64_t* rp, const int32_t* ci, const void* av, int val_f32, int64_t m,
+                                    int64_t n, const int64_t* pcp, int32_t* chunk_cols, int64_t* chunk_ent_ptr,
+                                    int32_t* ent_rc, void* ent_val, int32_t* err, void* stream) {
+  if (m <= 0) return 0;
+  PlanArgs a{rp, ci, av, val_f32, m, n, nullptr, pcp, chunk_cols, chunk_ent_ptr, ent_rc, (unsigned short*)ent_val,
+             err};
+  hipLaunchKernelGGL(spmm_plan<true>, dim3((unsigned)((m + PR - 1) / PR)), dim3(NT), 0, (hipStream_t)stream, a);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
 
 SPMM_EXPORT int spmm_spmm_panel_mfma(const int64_t* panel_chunk_ptr, const int32_t* chunk_cols,
                                      const int64_t* chunk_ent_ptr, const int32_t* ent_rc, const void* ent_val,
@@ -213,14 +586,14 @@ SPMM_EXPORT int spmm_spmm_panel_mfma(const int64_t* panel_chunk_ptr, const int32
   if (D % DB != 0 || ldx % 8 != 0) return (int)hipErrorInvalidValue;
   const int64_t npanels = (m + PR - 1) / PR;
   dim3 grid((unsigned)npanels, (unsigned)(D / DB));
-  if (out_bf16)
-    hipLaunchKernelGGL(spmm_panel_mfma<true>, grid, dim3(NT), 0, (hipStream_t)stream, panel_chunk_ptr, chunk_cols,
-                       chunk_ent_ptr, ent_rc, (const unsigned short*)ent_val, (const unsigned short*)X, ldx, m, Y,
-                       ldy);
-  else
-    hipLaunchKernelGGL(spmm_panel_mfma<false>, grid, dim3(NT), 0, (hipStream_t)stream, panel_chunk_ptr, chunk_cols,
-                       chunk_ent_ptr, ent_rc, (const unsigned short*)ent_val, (const unsigned short*)X, ldx, m, Y,
-                       ldy);
+  static const int db = [] {   // SPMM_SPMM_MFMA_DB=0: the single-buffered kernel (A/B)
+    const char* e = getenv("SPMM_SPMM_MFMA_DB");
+    return e && *e ? atoi(e) : 1;
+  }();
+  auto k = db ? (out_bf16 ? spmm_panel_mfma_db<true> : spmm_panel_mfma_db<false>)
+              : (out_bf16 ? spmm_panel_mfma<true> : spmm_panel_mfma<false>);
+  hipLaunchKernelGGL(k, grid, dim3(NT), 0, (hipStream_t)stream, panel_chunk_ptr, chunk_cols, chunk_ent_ptr, ent_rc,
+                     (const unsigned short*)ent_val, (const unsigned short*)X, ldx, m, Y, ldy);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

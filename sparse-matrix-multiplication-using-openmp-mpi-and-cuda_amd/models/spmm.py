@@ -83,17 +83,39 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     g.manual_seed(seed * 31 + comm.rank)
     Xp = (torch.rand((hi - lo, cols), generator=g, device=comm.device) * 2 - 1).to(torch.bfloat16)
     counts = [b - a for a, b in panels]
-    plan, inspector_ms = None, None
-    if comm.device.type == "cuda" and method in ("auto", "mfma"):
-        import time
+    plan, inspector_ms, inspector_first_ms = None, None, None
+    import time
 
-        torch.cuda.synchronize(comm.device)
-        t0 = time.perf_counter()
-        plan = plan_panels(A)
-        torch.cuda.synchronize(comm.device)
-        inspector_ms = (time.perf_counter() - t0) * 1e3
+    if comm.device.type == "cuda" and method in ("auto", "mfma"):
+        times = []
+        for _ in range(2):   # first call: includes loading the kernels; second: the steady state
+            torch.cuda.synchronize(comm.device)
+            t0 = time.perf_counter()
+            plan = plan_panels(A)
+            torch.cuda.synchronize(comm.device)
+            times.append((time.perf_counter() - t0) * 1e3)
+        inspector_ms = times[1]
+        inspector_first_ms = times[0]
+    kernel_ms = {}
     if method == "auto":
         method = "mfma" if plan is not None and cols % 128 == 0 and plan.reuse >= CONFIG.spmm_mfma_min_reuse else "rowwise"
+        if method == "mfma" and comm.device.type == "cuda":
+            # executor choice at inspection time: near reuse 1 the two kernels
+            # gather the same X bytes, so time both on this operand (one local
+            # SpMM each, warm) and keep the faster one; both times are reported
+            Xfull = torch.zeros((n, cols), dtype=torch.bfloat16, device=comm.device)
+            for meth in ("mfma", "rowwise"):
+                spmm(A, Xfull, method=meth, plan=plan)
+                torch.cuda.synchronize(comm.device)
+                t0 = time.perf_counter()
+                for _ in range(10):
+                    spmm(A, Xfull, method=meth, plan=plan)
+                torch.cuda.synchronize(comm.device)
+                kernel_ms[meth] = (time.perf_counter() - t0) * 1e3 / 10
+            del Xfull
+            # the slowest rank's view decides, so every rank runs the same kernel
+            faster = comm.allreduce_max(kernel_ms["mfma"] - kernel_ms["rowwise"])
+            method = "mfma" if faster <= 0 else "rowwise"
     step = lambda: rowblock_spmm(A, Xp, comm, counts, plan=plan, method=method)  # noqa: E731
     if not comm.is_dist and comm.device.type == "cuda":
         # one GPU: the step is a single launch-bound SpMM -> replay it from a HIP graph
@@ -104,7 +126,8 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
         nnz_a = sum(comm.gather_ints(nnz_a))
     flops = 2 * nnz_a * cols
     extra = dict(nnz_A=nnz_a, spmm_method=method, panel_reuse=(plan.reuse if plan is not None else None),
-                 inspector_ms=inspector_ms, hip_graph=not comm.is_dist and comm.device.type == "cuda")
+                 inspector_ms=inspector_ms, inspector_first_ms=inspector_first_ms,
+                 autotune_ms=kernel_ms or None, hip_graph=not comm.is_dist and comm.device.type == "cuda")
     cfg = dict(model=f"{n}x{n} CSR SpMM (sparse x dense {cols}-col) at {density * 100:g}% density, bf16 MFMA",
                n=n, density=density, cols=cols, global_batch=1, seq_len=n, parallelism=f"rowblock{comm.world}")
     return step, flops, extra, cfg

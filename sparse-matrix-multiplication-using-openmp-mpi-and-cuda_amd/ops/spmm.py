@@ -30,6 +30,9 @@ _native.register_hip("spmm_spmm_panel_mfma", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                      c_vp, C.c_int64, C.c_int, c_vp)
 _native.register_hip("spmm_spmm_rowwise", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp,
                      C.c_int64, C.c_int, c_vp)
+_native.register_hip("spmm_spmm_plan_count", c_vp, c_vp, C.c_int64, C.c_int64, c_vp, c_vp)
+_native.register_hip("spmm_spmm_plan_fill", c_vp, c_vp, c_vp, C.c_int, C.c_int64, C.c_int64, c_vp, c_vp, c_vp, c_vp,
+                     c_vp, c_vp, c_vp)
 
 PANEL = 64
 CHUNK = 64
@@ -53,8 +56,49 @@ class PanelPlan:
         return self.nnz / max(self.union_cols, 1)
 
 
-def plan_panels(A: CSR) -> PanelPlan:
-    """Inspector for the MFMA kernel (device-side torch ops, done once)."""
+def plan_panels(A: CSR, device_kernel: bool = True) -> PanelPlan:
+    """Inspector for the MFMA kernel, done once per sparse operand.  On a GPU
+    it is two hand-written kernels (``csr_spmm.hip`` spmm_plan: per panel an
+    LDS column bitmap, union ranks, chunk counts and scan) with one read-back
+    of the chunk total; panels whose union exceeds 65536 columns, and CPU
+    tensors, use the torch formulation below (same plan up to the order of
+    entries inside a chunk)."""
+    if device_kernel and A.device.type == "cuda" and A.m > 0:
+        plan = _plan_panels_hip(A)
+        if plan is not None:
+            return plan
+    return _plan_panels_torch(A)
+
+
+def _plan_panels_hip(A: CSR) -> Optional[PanelPlan]:
+    dev = A.device
+    P = _native.ptr
+    lib = _native.hip()
+    st = _native.stream_ptr(dev)
+    npan = (A.m + PANEL - 1) // PANEL
+    col = A.col if A.col.dtype == torch.int32 else A.col.to(torch.int32)
+    val_f32 = A.val.dtype == torch.float32
+    av = A.val if val_f32 or A.val.dtype == torch.bfloat16 else A.val.float()
+    val_f32 = av.dtype == torch.float32
+    nunion = torch.empty(npan, dtype=torch.int64, device=dev)
+    _native.check(lib.spmm_spmm_plan_count(P(A.rowptr), P(col), A.m, A.n, P(nunion), st), "spmm_plan_count")
+    pcp = torch.zeros(npan + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.div(nunion + CHUNK - 1, CHUNK, rounding_mode="floor"), 0, out=pcp[1:])
+    total_ch, union_cols, widest = torch.stack([pcp[-1], nunion.sum(), nunion.max()]).tolist()   # one read-back
+    if widest > 1024 * CHUNK:
+        return None
+    chunk_cols = torch.empty(total_ch * CHUNK, dtype=torch.int32, device=dev)
+    chunk_ent_ptr = torch.zeros(total_ch + 1, dtype=torch.int64, device=dev)
+    ent_rc = torch.empty(A.nnz, dtype=torch.int32, device=dev)
+    ent_val = torch.empty(A.nnz, dtype=torch.bfloat16, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    _native.check(lib.spmm_spmm_plan_fill(P(A.rowptr), P(col), P(av), int(val_f32), A.m, A.n, P(pcp), P(chunk_cols),
+                                          P(chunk_ent_ptr), P(ent_rc), P(ent_val), P(err), st), "spmm_plan_fill")
+    return PanelPlan(A.m, A.n, pcp, chunk_cols, chunk_ent_ptr, ent_rc, ent_val, int(union_cols), A.nnz)
+
+
+def _plan_panels_torch(A: CSR) -> PanelPlan:
+    """The inspector as device-side torch ops (reference formulation)."""
     dev = A.device
     n = A.n
     npan = (A.m + PANEL - 1) // PANEL

@@ -151,3 +151,62 @@ def test_spmm_graph_replay_matches_eager():
     X2 = (torch.rand((2500, 128), device=dev) * 2 - 1).to(torch.bfloat16)
     g.X.copy_(X2)
     assert torch.equal(g.run(), spmm(A, X2, method="mfma", plan=plan))
+
+
+def _plan_chunks(P):
+    """(panel_chunk_ptr, chunk_cols, chunk_ent_ptr, per-chunk sorted (rc, val) lists) on the host."""
+    cep = P.chunk_ent_ptr.cpu()
+    rc, val = P.ent_rc.cpu(), P.ent_val.cpu().float()
+    per = []
+    for ch in range(cep.numel() - 1):
+        s, e = int(cep[ch]), int(cep[ch + 1])
+        k, o = torch.sort(rc[s:e])
+        per.append((k, val[s:e][o]))
+    return P.panel_chunk_ptr.cpu(), P.chunk_cols.cpu(), cep, per
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,d,dt", [(65536, 65536, 1e-3, torch.bfloat16), (1000, 300000, 2e-4, torch.float32),
+                                      (777, 5000, 0.02, torch.bfloat16), (64, 70000, 0.01, torch.bfloat16)])
+def test_plan_panels_device_kernel_matches_torch(m, n, d, dt):
+    """The HIP inspector (count + fill kernels, column windows of 2^16, empty
+    panels, fp32 or bf16 values) builds the torch inspector's plan: same
+    chunk layout and columns, same entries per chunk (the order inside a
+    chunk is free)."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, n, d, seed=7, device=dev, dtype=dt)
+    Pk = SM.plan_panels(A)
+    Pt = SM.plan_panels(A, device_kernel=False)
+    a, b = _plan_chunks(Pk), _plan_chunks(Pt)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert all(torch.equal(x[0], y[0]) and torch.equal(x[1], y[1]) for x, y in zip(a[3], b[3]))
+    assert Pk.union_cols == Pt.union_cols and Pk.nnz == Pt.nnz
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("db", ["0", "1"])
+def test_spmm_mfma_kernels_match_reference(monkeypatch, db):
+    """Single-buffered and double-buffered MFMA panel kernels (SPMM_SPMM_MFMA_DB,
+    read once per process: run in a subprocess) equal the fp32 reference, incl.
+    a chunk with more than 512 entries (dense panel columns)."""
+    import subprocess
+    import sys
+
+    code = """
+import torch, spmm_amd
+from spmm_amd.ops import spmm as SM
+from spmm_amd.utils import gen_csr
+dev = torch.device("cuda")
+for (m, n, d) in [(4096, 3000, 0.01), (300, 200, 0.9), (70, 65, 1.0)]:
+    A = gen_csr.uniform_csr(m, n, d, seed=3, device=dev, dtype=torch.bfloat16)
+    X = (torch.randn(n, 256, device=dev) * 0.5).to(torch.bfloat16)
+    Y = SM.spmm(A, X, method="mfma")
+    R = A.to_dense(torch.float32) @ X.float()
+    err = float((Y - R).abs().max()) / max(1.0, float(R.abs().max()))
+    assert err < 1e-3, (m, n, d, err)
+print("ok")
+"""
+    env = dict(os.environ, SPMM_SPMM_MFMA_DB=db,
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]

@@ -25,6 +25,23 @@ for st in ${STEPS:-dist gpu smoke bench bench2}; do
       echo "== bench 1 rank, deterministic"
       SPMM_SPGEMM_DETERMINISTIC=1 timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/bench1_det.log 2>&1 || { tail -20 $O/bench1_det.log; exit 1; }
       grep '"metric"' $O/bench1_det.log > $O/bench1_det.json; cut -c1-300 $O/bench1_det.json ;;
+    spmm)
+      echo "== pytest spmm"
+      timeout -k 10 600 python -u -m pytest tests/test_spmm.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_spmm.log 2>&1 || { grep -E "FAILED|Error|assert|passed|failed" $O/pytest_spmm.log | tail -20; exit 1; }
+      grep -E "passed|failed" $O/pytest_spmm.log | tail -2
+      for db in 0 1 0 1; do
+        SPMM_SPMM_MFMA_DB=$db timeout -k 10 300 python -u bench.py --workload spmm --steps 20 --warmup 5 > $O/bench_spmm_db$db.log 2>&1 || { tail -20 $O/bench_spmm_db$db.log; exit 1; }
+        echo "db=$db $(grep -o '"ms_per_step": [0-9.]*' $O/bench_spmm_db$db.log) $(grep -o '"value": [0-9.]*' $O/bench_spmm_db$db.log) $(grep -o '"spmm_method": "[a-z]*"' $O/bench_spmm_db$db.log) $(grep -o '"inspector_ms": [0-9.]*' $O/bench_spmm_db$db.log) $(grep -o '"inspector_first_ms": [0-9.]*' $O/bench_spmm_db$db.log)"
+      done
+      for meth in rowwise; do
+        SPMM_MFMA_MIN_REUSE=100 timeout -k 10 300 python -u bench.py --workload spmm --steps 20 --warmup 5 > $O/bench_spmm_row.log 2>&1 || { tail -20 $O/bench_spmm_row.log; exit 1; }
+        echo "rowwise $(grep -o '"ms_per_step": [0-9.]*' $O/bench_spmm_row.log) $(grep -o '"spmm_method": "[a-z]*"' $O/bench_spmm_row.log)"
+      done ;;
+    rows64k)
+      for v in auto on auto on; do
+        SPMM_SPGEMM_BITMAP_ROWS=$v timeout -k 10 300 python -u bench.py --workload spgemm64k --steps 20 --warmup 3 > $O/bench64k_rows_$v.log 2>&1 || { tail -20 $O/bench64k_rows_$v.log; exit 1; }
+        echo "rows=$v $(grep -o '"ms_per_step": [0-9.]*' $O/bench64k_rows_$v.log)"
+      done ;;
     smoke)
       echo "== smoke"
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
