@@ -17,6 +17,21 @@ if [ -n "${VARIANTS}" ]; then
     done
   done
 fi
+if [ -n "${ENVS}" ]; then
+  # ENVS="base;VAR=1;VAR=2,OTHER=3": one bench run per ';'-separated environment set
+  echo "== env A/B"
+  IFS=';' read -ra SETS <<< "${ENVS}"
+  i=0
+  for set in "${SETS[@]}"; do
+    i=$((i+1))
+    envs=""
+    [ "$set" = base ] || envs=$(echo "$set" | tr ',' ' ')
+    for wl in ${WLS:-spgemm}; do
+      env $envs timeout -k 10 300 python -u bench.py --workload $wl --steps ${NSTEPS:-5} --warmup 2 > $O/env_${i}_$wl.log 2>&1 || { tail -20 $O/env_${i}_$wl.log; exit 1; }
+      echo "[$set] $wl $(grep -o '"ms_per_step": [0-9.]*' $O/env_${i}_$wl.log) $(grep -o '"value": [0-9.]*' $O/env_${i}_$wl.log)"
+    done
+  done
+fi
 if [ -n "${STAMPS}" ]; then
   echo "== stamps ${STAMPS}"
   timeout -k 10 300 python -u tools/bm_stamps.py ${STAMPS} > $O/stamps.log 2>&1 || { tail -20 $O/stamps.log; exit 1; }
