@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU check: distributed-device tests (loopback ranks on one GPU), the
+# GPU check: distributed-device tests (loopback ranks on one GPU), the
 # full GPU suite, smoke, the headline bench at 1 rank and at 2 gloo ranks on the
 # one card (self-launched by bench.py --gpus 2).  STEPS selects what runs.
 set -o pipefail
