@@ -1012,13 +1012,15 @@ constexpr int LONG_W = 1 << LONG_LGW;
 constexpr int LONG_DNT = LONG_W / 32;  // long_dense: one occupancy word per thread
 constexpr int LONG_MAXCH = 4096;        // chunks per row (ncols <= 2^26)
 
+// SCATTER: wg_hist holds each workgroup's offset inside its (row, chunk)
+// regions (long_wg_scan), row_off[row * nch + t] the regions' scratch bases.
 template <bool SCATTER>
 __global__ __launch_bounds__(LONG_NT) void long_route(
     const int32_t* __restrict__ Aci, const float* __restrict__ Av, const int64_t* __restrict__ Brp,
     const int32_t* __restrict__ Bci, const float* __restrict__ Bv, const int64_t* __restrict__ wg_e0,
     const int64_t* __restrict__ wg_e1, int nch, int32_t* __restrict__ wg_hist,
-    const int64_t* __restrict__ wg_base, unsigned long long* __restrict__ scratch,
-    const int32_t* __restrict__ lidx, const uint32_t* __restrict__ btab) {
+    const int32_t* __restrict__ wg_row, const int64_t* __restrict__ row_off,
+    unsigned long long* __restrict__ scratch, const int32_t* __restrict__ lidx, const uint32_t* __restrict__ btab) {
   __shared__ unsigned long long cur[SCATTER ? LONG_MAXCH : 1];
   __shared__ int hist[SCATTER ? 1 : LONG_MAXCH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1030,8 +1032,9 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
 #else
   const int64_t wg = blockIdx.x;
 #endif
+  const int64_t ro = SCATTER ? (int64_t)wg_row[wg] * nch : 0;
   for (int t = tid; t < nch; t += LONG_NT) {
-    if constexpr (SCATTER) cur[t] = (unsigned long long)wg_base[wg * nch + t];
+    if constexpr (SCATTER) cur[t] = (unsigned long long)(row_off[ro + t] + wg_hist[wg * nch + t]);
     else hist[t] = 0;
   }
   __syncthreads();
@@ -1091,6 +1094,28 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
     __syncthreads();
     for (int t = tid; t < nch; t += LONG_NT) wg_hist[wg * nch + t] = hist[t];
   }
+}
+
+// Routing plan on the device (replaces a chain of torch ops over the
+// [workgroups x chunks] histogram: widening copies, a transpose, cumsums,
+// gathers; ~10 passes over arrays of ~2e9 entries per R-MAT 24 batch).  Per
+// (row, chunk): the histogram counts of the row's workgroups (consecutive:
+// wg0[r] .. wg0[r] + nwg[r]) become each workgroup's offset inside the
+// (row, chunk) scratch region, in place; the region sizes go to cnt.
+__global__ __launch_bounds__(256) void long_wg_scan(int32_t* __restrict__ hist, const int64_t* __restrict__ wg0,
+                                                   const int64_t* __restrict__ nwg, int nch,
+                                                   int64_t* __restrict__ cnt) {
+  const int64_t r = blockIdx.x;
+  const int k = blockIdx.y * 256 + threadIdx.x;
+  if (k >= nch) return;
+  const int64_t w0 = wg0[r], w1 = w0 + nwg[r];
+  int64_t run = 0;
+  for (int64_t w = w0; w < w1; ++w) {   // consecutive threads: consecutive chunks of one row (coalesced)
+    const int32_t v = hist[w * nch + k];
+    hist[w * nch + k] = (int32_t)run;
+    run += v;
+  }
+  cnt[r * nch + k] = run;
 }
 
 // Chunk offsets of the long rows of B (the routing histogram's shortcut):
@@ -1665,20 +1690,35 @@ SPMM_EXPORT int spmm_spgemm_esc_ordered(const int64_t* Arp, const int32_t* Aci, 
 SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp,
                                        const int32_t* Bci, const float* Bv, const int64_t* wg_e0,
                                        const int64_t* wg_e1, int64_t nwg, int nch, int32_t* wg_hist,
-                                       const int64_t* wg_base, void* scratch, const int32_t* lidx,
-                                       const uint32_t* btab, void* stream) {
-  // lidx / btab (histogram pass, optional): B row -> long-row index or -1,
-  // and the long rows' chunk offsets (spmm_spgemm_long_btab)
+                                       const int32_t* wg_row, const int64_t* row_off, void* scratch,
+                                       const int32_t* lidx, const uint32_t* btab, void* stream) {
+  // histogram pass: wg_hist out; lidx / btab (optional): B row -> long-row
+  // index or -1, and the long rows' chunk offsets (spmm_spgemm_long_btab).
+  // scatter pass: wg_hist = per-workgroup offsets (spmm_spgemm_long_wg_scan),
+  // wg_row = each workgroup's row in the batch, row_off = region bases.
   if (nwg <= 0) return 0;
   if (nch > LONG_MAXCH) return (int)hipErrorInvalidValue;
   if ((lidx == nullptr) != (btab == nullptr)) return (int)hipErrorInvalidValue;
+  if (scatter && (wg_row == nullptr || row_off == nullptr)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   if (scatter)
     hipLaunchKernelGGL(long_route<true>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0, wg_e1,
-                       nch, wg_hist, wg_base, (unsigned long long*)scratch, nullptr, nullptr);
+                       nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, nullptr, nullptr);
   else
     hipLaunchKernelGGL(long_route<false>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0,
-                       wg_e1, nch, wg_hist, wg_base, (unsigned long long*)scratch, lidx, btab);
+                       wg_e1, nch, wg_hist, nullptr, nullptr, (unsigned long long*)scratch, lidx, btab);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// In place: routing histogram -> per-workgroup offsets inside each (row,
+// chunk) region; cnt[r * nch + k] = region sizes.  wg0 / nwg: int64 [R].
+SPMM_EXPORT int spmm_spgemm_long_wg_scan(int32_t* wg_hist, const int64_t* wg0, const int64_t* nwg, int64_t R,
+                                         int nch, int64_t* cnt, void* stream) {
+  if (R <= 0) return 0;
+  if (nch > LONG_MAXCH || R > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(long_wg_scan, dim3((unsigned)R, (unsigned)((nch + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, wg_hist, wg0, nwg, nch, cnt);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -49,6 +49,10 @@
 #define SPMM_BM_P1_SPLIT 0
 #endif
 
+#ifndef SPMM_BM_PREFETCH   // row kernels: L2 prefetch of each entry's next-unit B segment (first + last line)
+#define SPMM_BM_PREFETCH 0
+#endif
+
 #ifndef SPMM_BM_NT_STORE   // numeric write-out: non-temporal stores of C (C does not displace B in L2 / MALL;
 #define SPMM_BM_NT_STORE 1   // 1M step 76.55 -> 75.41 ms, 64k 1.755 -> 1.697 ms, same box)
 #endif
@@ -956,12 +960,16 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
 
   int c[RR];
   float v[RR];
+  uint32_t pf0 = 0, pf1 = 0;   // prefetch sinks (SPMM_BM_PREFETCH)
   for (; row < m; row += NG) {
     const int na = cna;
     const int q0 = ra.q0, q1 = ra.q1;
     uint32_t bq = bm_window_start(cwa, cwb, q0);   // first B index of window q of this thread's entry
     for (int q = q0; q < q1; ++q) {
       const bool last = q == q1 - 1;
+#if SPMM_BM_PREFETCH
+      asm volatile("" ::"v"(pf0), "v"(pf1));   // the previous unit's prefetches: a use, so their registers stay reserved
+#endif
       // ---- pipeline hooks (every path) ---------------------------------
       if (q == q0) {
         ld_entries(row + NG, n1a, n1b);
@@ -977,6 +985,24 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       }
       const uint32_t b0 = bq;
       bq += (uint32_t)len;
+#if SPMM_BM_PREFETCH
+      // the next window's segment of this entry into L2 (its first and last
+      // lines): the next unit's B loads then hit L2 instead of HBM
+      if (!last && tid < na && tid < NT) {
+        const int qn = q + 1;
+        const uint32_t wn = qn < 2 ? cwa.y : qn < 4 ? cwa.z : qn < 6 ? cwa.w : cwb;
+        const uint32_t ln = (wn >> (16 * (qn & 1))) & 0xffffu;
+        if (ln) {
+          if constexpr (CV) {
+            pf0 = p.Bcv[bq].x;
+            pf1 = p.Bcv[bq + ln - 1].x;
+          } else {
+            pf0 = (uint32_t)p.Bci[bq] ^ __float_as_uint(p.Bv[bq]);
+            pf1 = (uint32_t)p.Bci[bq + ln - 1] ^ __float_as_uint(p.Bv[bq + ln - 1]);
+          }
+        }
+      }
+#endif
       const int clo = q << LGW;
       const int u = (int)(row * nwin + q);
       // (both halves zero-extended: offsets pass 2^31 on the 1M product)
@@ -1728,12 +1754,16 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
   take_next();
   __syncthreads();
 
+  uint32_t pf0 = 0, pf1 = 0;   // prefetch sinks (SPMM_BM_PREFETCH)
   for (; row < m; row += NG) {
     const int na = cna;
     const int q0 = ra.q0, q1 = ra.q1;   // (q0 a multiple of NSUB)
     uint32_t bq = bm_window_start(cwa, cwb, q0);
     for (int q = q0; q < q1; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
       const bool last = q + NSUB >= q1;
+#if SPMM_BM_PREFETCH
+      asm volatile("" ::"v"(pf0), "v"(pf1));
+#endif
       if (q == q0) {
         ld_entries(row + NG);
         ld_arp(row + 2 * NG, n2a, n2b);
@@ -1752,6 +1782,18 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
       }
       const uint32_t b0 = bq;
       bq += (uint32_t)len;
+#if SPMM_BM_PREFETCH
+      if (!last && tid < na && tid < NT) {   // the next unit's column segment of this entry into L2
+        const int qn = q + NSUB;
+        const uint32_t wn = qn < 2 ? cwa.y : qn < 4 ? cwa.z : qn < 6 ? cwa.w : cwb;
+        uint32_t ln = (wn >> (16 * (qn & 1))) & 0xffffu;
+        if (NSUB == 2 && qn + 1 < nwin) ln += wn >> 16;
+        if (ln) {
+          pf0 = (uint32_t)p.Bci[bq];
+          pf1 = (uint32_t)p.Bci[bq + ln - 1];
+        }
+      }
+#endif
       const int clo = q << LGW;
       const int64_t u = row * nwin + q;
       int pre, plen, TC, P;

@@ -46,7 +46,8 @@ _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_
                      C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_compact", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, c_vp,
-                     c_vp, c_vp, c_vp, c_vp, c_vp)
+                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_wg_scan", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_btab", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
@@ -302,32 +303,31 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         wg_hist = torch.empty(nwg * nch, dtype=torch.int32, device=dev)
         nil = None
         _native.check(lib.spmm_spgemm_long_route(0, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
-                                                 P(wg_e1), nwg, nch, P(wg_hist), nil, nil,
+                                                 P(wg_e1), nwg, nch, P(wg_hist), nil, nil, nil,
                                                  P(lidx) if lidx is not None else nil,
                                                  P(btab) if btab is not None else nil, stream), "long_route")
-        H = wg_hist.view(nwg, nch).long()
-        T = torch.zeros((R, nch), dtype=torch.int64, device=dev).index_add_(0, row_of_wg, H)
+        # the [workgroups x chunks] histogram becomes per-workgroup offsets in
+        # place (one kernel); only the [rows x chunks] region sizes go through
+        # torch
+        T = torch.empty((R, nch), dtype=torch.int64, device=dev)
+        _native.check(lib.spmm_spgemm_long_wg_scan(P(wg_hist), P(first_wg), P(nwg_r), R, nch, P(T), stream),
+                      "long_wg_scan")
         chunk_off = torch.cumsum(T, 1) - T
         row_tot = T.sum(1)
         row_base = torch.cumsum(row_tot, 0) - row_tot
-        # per-chunk running sum over workgroups; scanned along the inner
-        # dimension (torch's outer-dimension scan runs one thread per column:
-        # 480 ms per R-MAT step for this line before the transpose)
-        Hc = torch.cumsum(H.t().contiguous(), 1).t() - H
-        Hc = Hc - Hc[first_wg][row_of_wg]
-        wg_base = (row_base[row_of_wg, None] + chunk_off[row_of_wg] + Hc).contiguous()
         # the scatter pass writes exactly the histogram's slots: a histogram
         # that disagrees with the rows' product counts would overrun them
         ntot, nbad = torch.stack([row_tot.sum(), (row_tot != nprod_rows[start:end]).sum()]).tolist()
         if nbad:
             raise RuntimeError(f"spgemm long rows: routing histogram disagrees with the product counts ({nbad} rows)")
         scratch = torch.empty(ntot, dtype=torch.int64, device=dev)
+        rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()   # each (row, chunk) region's base
+        wg_row = row_of_wg.to(torch.int32)
         _native.check(lib.spmm_spgemm_long_route(1, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
-                                                 P(wg_e1), nwg, nch, nil, P(wg_base), P(scratch), nil, nil, stream),
-                      "long_route")
-        del wg_base, Hc, H, wg_hist
-        rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()
-        rt_cnt = T.reshape(-1).contiguous()
+                                                 P(wg_e1), nwg, nch, P(wg_hist), P(wg_row), P(rt_off), P(scratch), nil,
+                                                 nil, stream), "long_route")
+        del wg_hist, wg_row
+        rt_cnt = T.reshape(-1)
         if LONG_STATS is not None:
             _long_stats(rt_cnt)
         rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)

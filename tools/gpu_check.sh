@@ -42,6 +42,10 @@ for st in ${STEPS:-dist gpu smoke bench bench2}; do
         SPMM_SPGEMM_BITMAP_ROWS=$v timeout -k 10 300 python -u bench.py --workload spgemm64k --steps 20 --warmup 3 > $O/bench64k_rows_$v.log 2>&1 || { tail -20 $O/bench64k_rows_$v.log; exit 1; }
         echo "rows=$v $(grep -o '"ms_per_step": [0-9.]*' $O/bench64k_rows_$v.log)"
       done ;;
+    long)
+      echo "== pytest long rows / rmat"
+      timeout -k 10 900 python -u -m pytest tests/test_spgemm.py -m gpu -x -v --timeout 300 --timeout-method thread -k "long or rmat or streamed or onepass or column_sliced" > $O/pytest_long.log 2>&1 || { grep -E "FAILED|Error|assert|passed|failed" $O/pytest_long.log | tail -20; exit 1; }
+      grep -E "passed|failed" $O/pytest_long.log | tail -2 ;;
     smoke)
       echo "== smoke"
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
