@@ -23,6 +23,8 @@ Extra options (all optional; env equivalents SPMM_*):
                       process-group backend (default: nccl on GPU, gloo on CPU);
                       loopback runs --ranks P ranks as threads of this process
   --threads N         host parser/writer threads (default: all)
+  --streams N         concurrent products per tree level on the GPU (default 4,
+                      as the native a4)
   --quiet             suppress the "multiplying" lines
   --metrics-json PATH per-rank phase times, bytes moved and throughput
   --no-split          cross-rank tree products on one rank each (default: each
@@ -49,6 +51,7 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default=os.environ.get("SPMM_DEVICE", "auto"))
     ap.add_argument("--comm", default=os.environ.get("SPMM_COMM", "auto"))
     ap.add_argument("--threads", type=int, default=int(os.environ.get("SPMM_THREADS", "0")))
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("SPMM_STREAMS", "4")))
     ap.add_argument("--ranks", type=int, default=int(os.environ.get("SPMM_RANKS", "1")),
                     help="--comm loopback: in-process ranks")
     ap.add_argument("--quiet", action="store_true", default=bool(os.environ.get("SPMM_QUIET")))
@@ -81,7 +84,7 @@ def main(argv=None) -> int:
     try:
         log = None if args.quiet else (lambda s: print(s, flush=True))
         run_chain(args.folder, comm, out_path=args.out, log=log, nthreads=args.threads, stats=stats,
-                  split=not args.no_split, fast=args.fast)
+                  split=not args.no_split, fast=args.fast, streams=max(1, args.streams))
     except refio.FormatError as e:
         print(str(e), file=sys.stderr)
         rc = 1
@@ -117,7 +120,7 @@ def _main_loopback(args, t_start: float) -> int:
     def rank_main(comm):
         st = ChainStats()
         run_chain(args.folder, comm, out_path=args.out, log=log, nthreads=args.threads, stats=st,
-                  split=not args.no_split, fast=args.fast)
+                  split=not args.no_split, fast=args.fast, streams=max(1, args.streams))
         return st
 
     try:

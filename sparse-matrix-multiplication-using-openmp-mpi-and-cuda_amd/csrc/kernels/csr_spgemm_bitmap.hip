@@ -45,6 +45,10 @@
 #define SPMM_BM_SKIP_ROUNDS 1
 #endif
 
+#ifndef SPMM_BM_ROWS_WPS   // 512-thread row kernel: waves per SIMD its registers are sized for
+#define SPMM_BM_ROWS_WPS 6
+#endif
+
 #ifndef SPMM_BM_P1_SPLIT   // row-major numeric pass 1: straight-line bodies of RR/2, RR-2, RR rounds by the unit's need
 #define SPMM_BM_P1_SPLIT 0
 #endif
@@ -854,7 +858,7 @@ __device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb
 }
 
 template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET>
-__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
+__global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_bm_rows(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
@@ -1974,6 +1978,10 @@ struct BmCfg {
 constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12}, {15, 2, 3840, 16}, {16, 4, 3072, 16}};
 constexpr int kNumCfgs = 3;
 constexpr int kFastNT = 256, kReloadPcap = 12288, kReloadCcap = 2048;
+#ifndef SPMM_BM_ROWS_NT   // threads of the row-major numeric kernel's workgroups (256 or 512; 4 workgroups per CU)
+#define SPMM_BM_ROWS_NT 256
+#endif
+constexpr int kRowsNT = SPMM_BM_ROWS_NT;
 // reload workgroup: up to 1024 threads (the longest A row it can stage), at
 // most one wave per 64 bitmap words
 constexpr int reload_nt(int lgw) { return ((1 << lgw) / 64) < 1024 ? ((1 << lgw) / 64) : 1024; }
@@ -2014,11 +2022,15 @@ int bm_count(int64_t work, const BmArgs& a, hipStream_t s) {
 template <int C>
 struct BmRowKernel {
   static constexpr BmCfg K = kCfgs[C];
-  static constexpr int R = K.rounds_fast > SPMM_BM_ROWS_R ? SPMM_BM_ROWS_R : K.rounds_fast;   // (the row pipeline's registers cost rounds)
-  static constexpr auto k = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false, false>;
-  static constexpr auto kcv = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true, false>;
-  static constexpr auto k_det = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), false, true>;
-  static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16), true, true>;
+  static constexpr int NT = kRowsNT;
+  // register rounds: the same products per workgroup round at any width (the
+  // row pipeline's registers cost rounds)
+  static constexpr int R0 = K.rounds_fast > SPMM_BM_ROWS_R ? SPMM_BM_ROWS_R : K.rounds_fast;
+  static constexpr int R = (R0 * kFastNT + NT - 1) / NT;
+  static constexpr auto k = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, false>;
+  static constexpr auto kcv = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false>;
+  static constexpr auto k_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, true>;
+  static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, true>;
 };
 
 template <typename Kern>
@@ -2085,8 +2097,8 @@ int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, int det, hipStream_t s) 
       ra.q0 = q;
       ra.q1 = q + step < nwin ? q + step : nwin;
       using K = BmRowKernel<C>;
-      const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s) : launch_rows(K::k_det, ra, s))
-                         : (ra.a.Bcv ? launch_rows(K::kcv, ra, s) : launch_rows(K::k, ra, s));
+      const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
+                         : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT));
       if (rc) return rc;
     }
   }

@@ -29,6 +29,9 @@
 //   --load-partials DIR   resume from saved partials, skipping load + local tree
 //   --timeout S           RCCL transfer timeout (fail fast, default 600)
 //   --no-split            cross-rank products on one rank each (no row-panel split)
+//   --format ref|mtx      input format: the reference folder (default) or a
+//                         chain of Matrix Market files / a folder of them
+//                         (CSR engine, fp32; csr_chain.cpp; output ./matrix.mtx)
 #include <mpi.h>
 #include <sys/stat.h>
 
@@ -48,13 +51,15 @@
 #include <thread>
 
 #include "comm.hpp"
+#include "csr_chain.hpp"
 #include "rt.hpp"
 
 namespace a4 {
 namespace {
 
 struct Options {
-  std::string folder, out = "matrix", device = "auto", comm = "auto", metrics, save_dir, load_dir;
+  std::string folder, out, device = "auto", comm = "auto", metrics, save_dir, load_dir, format = "ref";
+  std::vector<std::string> inputs;
   int threads = 0, streams = 4;
   bool quiet = false, dump = false, split = true, fast = false;
   double timeout = 600.0;
@@ -62,7 +67,7 @@ struct Options {
 
 [[noreturn]] void usage(const char* why) {
   std::cerr << "a4: " << why << "\n"
-            << "usage: a4 <folder> [--out PATH] [--device auto|hip|cpu] [--comm auto|rccl|mpi] [--threads N]\n"
+            << "usage: a4 <folder> [--format ref|mtx] [--out PATH] [--device auto|hip|cpu] [--comm auto|rccl|mpi] [--threads N]\n"
                "          [--streams N] [--quiet] [--dump] [--metrics-json PATH] [--save-partials DIR]\n"
                "          [--load-partials DIR] [--timeout S] [--no-split] [--exact | --fast]\n";
   std::exit(2);
@@ -90,11 +95,15 @@ Options parse_args(int argc, char** argv) {
     else if (a == "--save-partials") o.save_dir = val();
     else if (a == "--load-partials") o.load_dir = val();
     else if (a == "--timeout") o.timeout = std::atof(val().c_str());
+    else if (a == "--format") o.format = val();
     else if (a.rfind("--", 0) == 0) usage(("unknown option " + a).c_str());
-    else if (o.folder.empty()) o.folder = a;
-    else usage(("unexpected argument " + a).c_str());
+    else o.inputs.push_back(a);
   }
-  if (o.folder.empty()) usage("missing <folder>");
+  if (o.format != "ref" && o.format != "mtx") usage("--format must be ref or mtx");
+  if (o.inputs.empty()) usage("missing <folder>");
+  if (o.format == "ref" && o.inputs.size() != 1) usage(("unexpected argument " + o.inputs[1]).c_str());
+  o.folder = o.inputs[0];
+  if (o.out.empty()) o.out = o.format == "mtx" ? "matrix.mtx" : "matrix";
   if (o.device != "auto" && o.device != "hip" && o.device != "cpu") usage("--device must be auto, hip or cpu");
   if (o.comm != "auto" && o.comm != "rccl" && o.comm != "mpi") usage("--comm must be auto, rccl or mpi");
   return o;
@@ -791,6 +800,17 @@ int local_rank() {
 }
 
 int run(const Options& o, int rank, int world, double t_start) {
+  if (o.format == "mtx") {
+    MtxOptions m;
+    m.inputs = o.inputs;
+    m.out = o.out;
+    m.device = o.device;
+    m.metrics = o.metrics;
+    m.threads = o.threads;
+    m.local_rank = local_rank();
+    m.quiet = o.quiet;
+    return run_mtx(m, rank, world);
+  }
   // size file: "N k" (:412-418)
   int64_t N = 0;
   int k = 0;

@@ -99,38 +99,81 @@ class _Loader(threading.Thread):
 
 
 def reduce_tree(mats: List[BSR], start: int, log: Optional[Log], stats: Optional[ChainStats] = None,
-                source=None) -> BSR:
+                source=None, streams: int = 1) -> BSR:
     """``helper2``: pairwise tree, level by level, odd tail carried.
 
     ``mats`` may be shorter than the chain when ``source`` (a loader) is given:
     level 0 pulls matrices from it as they land, so products start before the
-    last file is parsed.
+    last file is parsed.  ``streams`` > 1 (GPU): the independent products of a
+    level are issued round-robin on a pool of HIP streams (``a4 --streams``),
+    so one product's kernels overlap the next one's host-side planning.
     """
     n = len(mats) if source is None else (source.hi - source.lo + 1)
     arr: List[Optional[BSR]] = list(mats) if source is None else []
+    pool = _StreamPool(streams, mats[0].device if mats else (source.device if source is not None else None))
     if source is not None:
         level0: List[BSR] = []
-        for ind in range(0, n - 1, 2):
+        for j, ind in enumerate(range(0, n - 1, 2)):
             a = source.get()
             b = source.get()
             if log:
                 log(f"multiplying {start + ind} {start + ind + 1}")
-            level0.append(_mul(a, b, stats))
+            level0.append(pool.mul(j, a, b, stats))
         if n % 2 == 1:
             level0.append(source.get())
+        pool.join(level0)
         if n == 1:
             return level0[0]
         arr = level0
     while len(arr) > 1:
         nxt = []
-        for ind in range(0, len(arr) - 1, 2):
+        for j, ind in enumerate(range(0, len(arr) - 1, 2)):
             if log:
                 log(f"multiplying {start + ind} {start + ind + 1}")
-            nxt.append(_mul(arr[ind], arr[ind + 1], stats))
+            nxt.append(pool.mul(j, arr[ind], arr[ind + 1], stats))
         if len(arr) % 2 == 1:
             nxt.append(arr[-1])
+        pool.join(nxt)
         arr = nxt
     return arr[0]
+
+
+class _StreamPool:
+    """Round-robin HIP streams for the products of one tree level.  Every
+    product's stream waits for the issuing stream first; operands are recorded
+    on the stream that reads them and results on the issuing stream, so the
+    caching allocator never hands a block to one stream while another still
+    uses it."""
+
+    def __init__(self, streams: int, device):
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.on = streams > 1 and dev.type == "cuda"
+        self.dev = dev
+        self.pool = [torch.cuda.Stream(dev) for _ in range(streams)] if self.on else []
+        self.used = set()
+
+    def mul(self, j: int, a: BSR, b: BSR, stats: Optional[ChainStats]) -> BSR:
+        if not self.on:
+            return _mul(a, b, stats)
+        st = self.pool[j % len(self.pool)]
+        st.wait_stream(torch.cuda.current_stream(self.dev))
+        self.used.add(j % len(self.pool))
+        with torch.cuda.stream(st):
+            c = _mul(a, b, stats)
+        for t in (a.keys, a.vals, b.keys, b.vals):
+            t.record_stream(st)
+        return c
+
+    def join(self, results: List[BSR]) -> None:
+        if not self.on:
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        for i in sorted(self.used):
+            cur.wait_stream(self.pool[i])
+        self.used.clear()
+        for M in results:
+            M.keys.record_stream(cur)
+            M.vals.record_stream(cur)
 
 
 def _mul(a: BSR, b: BSR, stats: Optional[ChainStats]) -> BSR:
@@ -147,7 +190,7 @@ def _sync(dev: torch.device) -> None:
 
 def run_chain(folder: str, comm: Comm, out_path: Optional[str] = "matrix", log: Optional[Log] = print,
               nthreads: int = 0, stats: Optional[ChainStats] = None, split: bool = True,
-              fast: bool = False) -> Optional[BSR]:
+              fast: bool = False, streams: int = 1) -> Optional[BSR]:
     """The full reference pipeline on this rank.  Returns the final product on
     rank 0 (pruned), None elsewhere.  Writes ``out_path`` on rank 0 unless None.
     ``fast``: chain ranges balanced on the matrix files' sizes instead of the
@@ -169,7 +212,7 @@ def run_chain(folder: str, comm: Comm, out_path: Optional[str] = "matrix", log: 
         t0 = time.perf_counter()
         loader = _Loader(folder, my[0], my[1], k, dev, nthreads)
         loader.start()
-        part = reduce_tree([], my[0], log, stats, source=loader)
+        part = reduce_tree([], my[0], log, stats, source=loader, streams=streams)
         _sync(dev)
         loader.join()
         stats.bytes_h2d += loader.bytes
@@ -272,8 +315,8 @@ def _binomial_reduce(part: Optional[BSR], comm: Comm, log: Optional[Log], stats:
     return part if r == 0 else None
 
 
-def chain_product(mats: List[BSR], log: Optional[Log] = None) -> BSR:
+def chain_product(mats: List[BSR], log: Optional[Log] = None, streams: int = 1) -> BSR:
     """In-memory chain product with the single-rank tree (P = 1 association)."""
     if not mats:
         raise ValueError("empty chain")
-    return prune_zero_tiles(reduce_tree(mats, 0, log))
+    return prune_zero_tiles(reduce_tree(mats, 0, log, streams=streams))

@@ -184,3 +184,153 @@ def test_a4_gpu_k32_matches_cpu_engine(tmp_path, a4_bin):
     _run(a4_bin, 1, folder, "--device", "hip", "--out", str(tmp_path / "g"), "--quiet")
     _run(a4_bin, 1, folder, "--device", "cpu", "--out", str(tmp_path / "c"), "--quiet")
     assert open(tmp_path / "g").read() == open(tmp_path / "c").read()
+
+
+# ---- a4 --format mtx (csr_chain.cpp) ----------------------------------------
+
+def _mtx_chain(d, dims, density=0.03, seed=10):
+    from spmm_amd.utils import gen_csr, mtx
+
+    d.mkdir(exist_ok=True)
+    mats = [gen_csr.uniform_csr(dims[i], dims[i + 1], density, seed=seed + i) for i in range(len(dims) - 1)]
+    for i, M in enumerate(mats):
+        mtx.write_mtx(str(d / f"m{i + 1}.mtx"), M)
+    return mats
+
+
+def _python_mtx(tmp_path, inputs, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "spmm_amd.apps.a4", "--format", "mtx", *inputs, "--out", out,
+                        "--device", "cpu", "--comm", "gloo", "--quiet"], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 8])
+def test_a4_mtx_native_matches_python_cli(tmp_path, a4_bin, p):
+    """Native ``a4 --format mtx`` at P MPI ranks (each rank parses 1/P of every
+    file, entries shuffled to their row owners, B all-gathered, C written
+    through rank 0) writes the same bytes as the Python front-end's one-rank
+    run (both on the OpenMP Gustavson engine), with the reference's stdout."""
+    import torch
+
+    from spmm_amd.utils import mtx
+
+    mats = _mtx_chain(tmp_path / "chain", [300, 250, 280, 260, 310])
+    want = str(tmp_path / "py.mtx")
+    _python_mtx(tmp_path, [str(tmp_path / "chain")], want)
+    out, met = str(tmp_path / "n.mtx"), str(tmp_path / "met.json")
+    r = _run(a4_bin, p, str(tmp_path / "chain"), "--format", "mtx", "--device", "cpu", "--out", out, "--threads", "2",
+             "--metrics-json", met)
+    assert open(out, "rb").read() == open(want, "rb").read()
+    assert re.findall(r"multiplying \d+ \d+", r.stdout) == ["multiplying 1 2", "multiplying 2 3", "multiplying 3 4"]
+    assert len(re.findall(r"time taken [0-9.e+-]+ seconds", r.stdout)) == p
+    m = json.load(open(met))
+    assert m["format"] == "mtx" and m["ranks"] == p and m["n_files"] == 4
+    ref = mats[0].to_dense().double()
+    for M in mats[1:]:
+        ref = ref @ M.to_dense().double()
+    assert torch.allclose(mtx.read_mtx(out).to_dense().double(), ref, atol=1e-4)
+
+
+@pytest.mark.parametrize("p", [1, 4])
+def test_a4_mtx_symmetric_shuffled_natural_order(tmp_path, a4_bin, p):
+    """Symmetric storage expanded, entries in random line order, a folder of
+    11 files taken in natural order (m2 before m10: lexicographic order breaks
+    the chain's shapes), an explicit file list giving the same bytes."""
+    import torch
+
+    from spmm_amd.utils import gen_csr, mtx
+
+    d = tmp_path / "chain"
+    d.mkdir()
+    dims = [40 + 3 * i for i in range(12)]
+    mats = [gen_csr.uniform_csr(dims[i], dims[i + 1], 0.08, seed=30 + i) for i in range(11)]
+    for i, M in enumerate(mats):
+        mtx.write_mtx(str(d / f"m{i + 1}.mtx"), M)
+    S = gen_csr.uniform_csr(dims[-1], dims[-1], 0.05, seed=99)
+    S = _symmetrize(S)
+    lines = ["%%MatrixMarket matrix coordinate real symmetric", f"{S.m} {S.n} 0"]
+    r_, c_, v_ = S.row_ids().tolist(), S.col.tolist(), S.val.tolist()
+    ent = [(r_[i], c_[i], v_[i]) for i in range(len(r_)) if r_[i] >= c_[i]]
+    import random
+
+    random.Random(5).shuffle(ent)
+    lines[1] = f"{S.m} {S.n} {len(ent)}"
+    lines += [f"{a + 1} {b + 1} {v!r}" for a, b, v in ent]
+    (tmp_path / "sym.mtx").write_text("\n".join(lines) + "\n")
+    d2 = tmp_path / "chain2"
+    d2.mkdir()
+    for i in range(11):
+        shutil.copy(d / f"m{i + 1}.mtx", d2 / f"m{i + 1}.mtx")
+    shutil.copy(tmp_path / "sym.mtx", d2 / "m12.mtx")
+    out1, out2 = str(tmp_path / "a.mtx"), str(tmp_path / "b.mtx")
+    _run(a4_bin, p, str(d2), "--format", "mtx", "--device", "cpu", "--out", out1, "--quiet")
+    files = [str(d2 / f"m{i + 1}.mtx") for i in range(12)]
+    _run(a4_bin, p, *files[:1], *files[1:], "--format", "mtx", "--device", "cpu", "--out", out2, "--quiet")
+    assert open(out1, "rb").read() == open(out2, "rb").read()
+    ref = mats[0].to_dense().double()
+    for M in mats[1:]:
+        ref = ref @ M.to_dense().double()
+    ref = ref @ S.to_dense().double()
+    assert torch.allclose(mtx.read_mtx(out1).to_dense().double(), ref, rtol=1e-4, atol=1e-4)
+
+
+def _symmetrize(S):
+    """S + S^T."""
+    import torch
+
+    from spmm_amd.ops import csr as CS
+
+    St = S.transpose()
+    return CS.from_coo(torch.cat([S.row_ids(), St.row_ids()]), torch.cat([S.col.long(), St.col.long()]),
+                       torch.cat([S.val, St.val]), S.m, S.n)
+
+
+@pytest.mark.parametrize("p", [1, 3])
+def test_a4_mtx_truncated_and_overlong_files(tmp_path, a4_bin, p):
+    """The 1-rank rules at any P: a file short of its header's nnz is rejected
+    (every rank exits non-zero with the count), entries past it are ignored."""
+    d = tmp_path / "c"
+    _mtx_chain(d, [60, 50, 70], density=0.1)
+    good = str(tmp_path / "good.mtx")
+    _run(a4_bin, 1, str(d), "--format", "mtx", "--device", "cpu", "--out", good, "--quiet")
+    text = (d / "m2.mtx").read_text().splitlines()
+    hdr = next(i for i, l in enumerate(text) if not l.startswith("%"))
+    nnz = int(text[hdr].split()[2])
+    (d / "m2.mtx").write_text("\n".join(text + ["1 1 7.0", "2 2 3.0"]) + "\n")   # 2 entries past nnz
+    out = str(tmp_path / "long.mtx")
+    _run(a4_bin, p, str(d), "--format", "mtx", "--device", "cpu", "--out", out, "--quiet")
+    assert open(out, "rb").read() == open(good, "rb").read()
+    (d / "m2.mtx").write_text("\n".join(text[:-5]) + "\n")
+    r = _run(a4_bin, p, str(d), "--format", "mtx", "--device", "cpu", "--out", out, "--quiet", check=False)
+    assert r.returncode != 0
+    assert f"file has {nnz - 5} entries, expected {nnz}" in r.stderr
+
+
+def test_a4_mtx_bad_format_flag(tmp_path, a4_bin):
+    r = _run(a4_bin, 1, str(tmp_path), "--format", "coo", check=False)
+    assert r.returncode != 0 and "--format must be ref or mtx" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [1, 2])
+def test_a4_mtx_gpu_bitmap_matches_cpu(tmp_path, a4_bin, p):
+    """The products run on the GPU's bitmap-rank kernels through their C ABI:
+    same structure as the CPU engine, values to fp32 summation order."""
+    import numpy as np
+
+    from spmm_amd.utils import mtx
+
+    _mtx_chain(tmp_path / "c", [3000, 2500, 2800, 2600], density=0.004, seed=3)
+    g, c, met = str(tmp_path / "g.mtx"), str(tmp_path / "c.mtx"), str(tmp_path / "met.json")
+    _run(a4_bin, p, str(tmp_path / "c"), "--format", "mtx", "--device", "hip", "--out", g, "--quiet",
+         "--metrics-json", met)
+    _run(a4_bin, p, str(tmp_path / "c"), "--format", "mtx", "--device", "cpu", "--out", c, "--quiet")
+    assert json.load(open(met))["gpu_products"] == 2
+    G, C = mtx.read_mtx(g), mtx.read_mtx(c)
+    assert G.nnz == C.nnz and bool((G.rowptr == C.rowptr).all()) and bool((G.col == C.col).all())
+    np.testing.assert_allclose(G.val.numpy(), C.val.numpy(), rtol=1e-5, atol=1e-6)

@@ -257,16 +257,35 @@ def test_bsr_numeric_gpu_matches_golden_k32():
 
 
 @pytest.mark.gpu
-def test_run_chain_gpu_k32(tmp_path):
+@pytest.mark.parametrize("streams", [1, 4])
+def test_run_chain_gpu_k32(tmp_path, streams):
+    """Also with the products of each tree level on a pool of 4 HIP streams
+    (``a4 --streams 4``): same bytes as the golden model."""
     k = 32
-    mats = gen.random_chain(6, 5, k, 0.4, "adversarial", seed=21)
+    mats = gen.random_chain(11, 5, k, 0.4, "adversarial", seed=21)
     folder = _write_chain(tmp_path, mats, k)
     comm = CM.Comm(0, 1, 0, torch.device("cuda", 0), None)
     out = str(tmp_path / "matrix")
-    CH.run_chain(folder, comm, out_path=out, log=None)
+    lines = []
+    CH.run_chain(folder, comm, out_path=out, log=lines.append, streams=streams)
     want = golden.chain([golden.from_bsr(m) for m in mats], p=1)
     with open(out) as f:
         assert f.read() == golden.to_text(want)
+    assert len(lines) == 10
+
+
+def test_a4_cli_streams_flag_cpu(tmp_path):
+    """``--streams`` is accepted by the Python front-end as by the native one
+    (a no-op on the CPU engine)."""
+    k = 2
+    mats = gen.random_chain(5, 3, k, 0.6, "full", seed=12)
+    folder = _write_chain(tmp_path, mats, k)
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "spmm_amd.apps.a4", folder, "--device", "cpu", "--streams", "3"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    want = golden.chain([golden.from_bsr(m) for m in mats], p=1)
+    assert (tmp_path / "matrix").read_text() == golden.to_text(want)
 
 
 def test_weighted_row_panels_balance():
