@@ -992,6 +992,14 @@ __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict_
 //          column order over the chunk's region, count in rt_nnz
 //   place  chunk results copied to their final CSR positions
 // Traffic per product: 4 + 8 B of B reads, 8 B scratch write + 8 B read.
+//
+// Direct products (hub B rows, long_btab): an item of more than LR_CAP
+// products takes the products of the row's LONG B rows (>= LONG_BTAB_MIN
+// entries per chunk; R-MAT 24: ~85 % of the long-row products) straight from
+// B in long_dense, through their chunk segments in long_btab: no scratch
+// write, no scratch read.  The route passes histogram them apart (dhist),
+// skip them in the scatter, and list the row's long entries (dl) instead;
+// items of <= LR_CAP products still route them (long_rank reads the scratch).
 #ifndef SPMM_LONG_EPW                   // (diagnostic builds: tools/bm_variants.py)
 #define SPMM_LONG_EPW 64
 #endif
@@ -1012,17 +1020,86 @@ constexpr int LONG_W = 1 << LONG_LGW;
 constexpr int LONG_DNT = LONG_W / 32;  // long_dense: one occupancy word per thread
 constexpr int LONG_MAXCH = 4096;        // chunks per row (ncols <= 2^26)
 
+// 64-lane inclusive prefix sum on the DPP network (VALU; no LDS traffic):
+// row_shr 1/2/4/8 inside 16-lane rows, then row_bcast:15 / row_bcast:31.
+__device__ __forceinline__ int wave_incl_scan_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// 64-lane inclusive max scan on the DPP network (identity -1).
+__device__ __forceinline__ int wave_incl_max_dpp(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));
+  x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));
+  return x;
+}
+
+constexpr int LR_R = 16, LR_CAP = LR_R * 64, LR_WAVES = 4;
+constexpr int LR_WORDS = LONG_W / 64;   // 64-bit bitmap words per chunk
+static_assert(LR_WORDS % 64 == 0, "whole bitmap rows per lane");
+
+__device__ __forceinline__ void lr_wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-level expansion of 64 sources (lane = source, exclusive prefix `pre`
+// of the lengths `len`) into slots: the owner of slot qw + lane, the window
+// [qw, qw + 64) of the concatenated sources (any window, in any order).
+// `own` = 64 ints of this wave's LDS.  A source starting inside the window
+// marks its first slot; a max scan over the marks gives every slot the last
+// source starting at or before it, the sources starting before the window
+// (one ballot) the slots before the first mark.
+__device__ __forceinline__ int wave_slot_owner(int pre, int len, int qw, int lane, int* own) {
+  const unsigned long long before = __ballot(len > 0 && pre < qw);
+  const int carry = before ? 63 - __clzll((long long)before) : -1;
+  own[lane] = -1;
+  lr_wave_fence();
+  if (len > 0 && pre >= qw && pre < qw + 64) own[pre - qw] = lane;
+  lr_wave_fence();
+  const int o = max(wave_incl_max_dpp(own[lane]), carry);
+  lr_wave_fence();
+  return o;
+}
+
 // SCATTER: wg_hist holds each workgroup's offset inside its (row, chunk)
 // regions (long_wg_scan), row_off[row * nch + t] the regions' scratch bases.
-template <bool SCATTER>
+// Direct mode (wg_dhist / dl given; lidx / btab required):
+//   histogram  the long B rows' chunk counts go to wg_dhist (not wg_hist),
+//              wg_nlong = the workgroup's long entries
+//   scatter    rt_mode[row * nch + t] (long_wg_scan): 0 = the item routes its
+//              long products too (same cursor), 1 = direct (skipped), 2 = no
+//              long products; every long entry is listed in dl at
+//              dl_off[wg] + i as {B row start, btab row, a bits, 0}
+template <bool SCATTER, bool DIRECT>
 __global__ __launch_bounds__(LONG_NT) void long_route(
     const int32_t* __restrict__ Aci, const float* __restrict__ Av, const int64_t* __restrict__ Brp,
     const int32_t* __restrict__ Bci, const float* __restrict__ Bv, const int64_t* __restrict__ wg_e0,
     const int64_t* __restrict__ wg_e1, int nch, int32_t* __restrict__ wg_hist,
     const int32_t* __restrict__ wg_row, const int64_t* __restrict__ row_off,
-    unsigned long long* __restrict__ scratch, const int32_t* __restrict__ lidx, const uint32_t* __restrict__ btab) {
+    unsigned long long* __restrict__ scratch, const int32_t* __restrict__ lidx, const uint32_t* __restrict__ btab,
+    int32_t* __restrict__ wg_dhist, int32_t* __restrict__ wg_nlong, const uint8_t* __restrict__ rt_mode,
+    uint4* __restrict__ dl, const int64_t* __restrict__ dl_off) {
+  constexpr int NWV = LONG_NT / 64;
+  constexpr bool DS = SCATTER && DIRECT;
   __shared__ unsigned long long cur[SCATTER ? LONG_MAXCH : 1];
   __shared__ int hist[SCATTER ? 1 : LONG_MAXCH];
+  __shared__ int dhist[!SCATTER && DIRECT ? LONG_MAXCH : 1];
+  __shared__ int own_all[DS ? NWV : 1][64];
+  __shared__ uint2 seg_all[DS ? NWV : 1][64];                 // {first B index (low 32 bits), slot prefix}
+  __shared__ unsigned long long dst_all[DS ? NWV : 1][64];    // scratch slot of each chunk's first product
+  __shared__ int16_t m0list[DS ? LONG_MAXCH : 1];             // the row's mode-0 chunks
+  __shared__ int nlong, nm0;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // Neighbouring workgroups own neighbouring scratch runs of every chunk, so
   // they share cache lines: give them one XCD (one L2) so the partial lines
@@ -1033,24 +1110,79 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
   const int64_t wg = blockIdx.x;
 #endif
   const int64_t ro = SCATTER ? (int64_t)wg_row[wg] * nch : 0;
+  if (tid == 0) {
+    nlong = 0;
+    nm0 = 0;
+  }
+  __syncthreads();
   for (int t = tid; t < nch; t += LONG_NT) {
-    if constexpr (SCATTER) cur[t] = (unsigned long long)(row_off[ro + t] + wg_hist[wg * nch + t]);
-    else hist[t] = 0;
+    if constexpr (SCATTER) {
+      cur[t] = (unsigned long long)(row_off[ro + t] + wg_hist[wg * nch + t]);
+      if constexpr (DS)
+        if (rt_mode[ro + t] == 0) m0list[atomicAdd(&nm0, 1)] = (int16_t)t;   // (any order)
+    } else {
+      hist[t] = 0;
+      if constexpr (DIRECT) dhist[t] = 0;
+    }
   }
   __syncthreads();
   const int64_t e1 = wg_e1[wg];
-  for (int64_t e = wg_e0[wg] + w; e < e1; e += LONG_NT / 64) {
+  for (int64_t e = wg_e0[wg] + w; e < e1; e += NWV) {
     const int j = Aci[e];
     const float a = SCATTER ? Av[e] : 0.f;
+    const int k = lidx != nullptr ? lidx[j] : -1;
     if constexpr (!SCATTER) {
       // a long B row (long_btab): its chunk histogram is the difference of
       // its chunk offsets, nch + 1 words instead of its whole column list
-      const int k = lidx != nullptr ? lidx[j] : -1;
       if (k >= 0) {   // wave-uniform
         const uint32_t* tk = btab + (int64_t)k * (nch + 1);
+        int* hh = DIRECT ? dhist : hist;
         for (int t = lane; t < nch; t += 64) {
           const int n = (int)(tk[t + 1] - tk[t]);
-          if (n) atomicAdd(&hist[t], n);
+          if (n) atomicAdd(&hh[t], n);
+        }
+        if (DIRECT && lane == 0) atomicAdd(&nlong, 1);
+        continue;
+      }
+    } else {
+      if (DIRECT && k >= 0) {   // wave-uniform: listed for long_dense; routed only into mode-0 items
+        const int64_t b0 = Brp[j];
+        if (lane == 0) {
+          const int at = atomicAdd(&nlong, 1);
+          dl[dl_off[wg] + at] = make_uint4((uint32_t)b0, (uint32_t)k, __float_as_uint(a), 0u);
+        }
+        const int n0 = nm0;
+        if (n0 == 0) continue;   // uniform: every long product of this row is direct
+        const uint32_t* tk = btab + (int64_t)k * (nch + 1);
+        int* own = own_all[w];
+        uint2* sg = seg_all[w];
+        unsigned long long* dst = dst_all[w];
+        for (int t0 = 0; t0 < n0; t0 += 64) {   // lane = a mode-0 chunk: its segment of this B row
+          int len = 0, t = 0;
+          uint32_t s0 = 0;
+          if (t0 + lane < n0) {
+            t = m0list[t0 + lane];
+            s0 = tk[t];
+            len = (int)(tk[t + 1] - s0);
+          }
+          const int incl = wave_incl_scan_dpp(len);
+          const int tot = __builtin_amdgcn_readlane(incl, 63);
+          if (tot == 0) continue;   // uniform
+          const int pre = incl - len;
+          sg[lane] = make_uint2((uint32_t)b0 + s0, (uint32_t)pre);
+          dst[lane] = len ? atomicAdd(&cur[t], (unsigned long long)len) : 0ull;
+          for (int qw = 0; qw < tot; qw += 64) {
+            const int o = wave_slot_owner(pre, len, qw, lane, own);
+            const int q = qw + lane;
+            if (q < tot) {
+              const uint2 g = sg[o];
+              const uint32_t f = g.x + (uint32_t)(q - (int)g.y);
+              const int c = Bci[f];
+              scratch[dst[o] + (uint32_t)(q - (int)g.y)] = ((unsigned long long)__float_as_uint(a * Bv[f]) << 32) |
+                                                           (uint32_t)c;
+            }
+          }
+          lr_wave_fence();   // seg / dst reads done before the next block's writes
         }
         continue;
       }
@@ -1092,7 +1224,11 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
   }
   if constexpr (!SCATTER) {
     __syncthreads();
-    for (int t = tid; t < nch; t += LONG_NT) wg_hist[wg * nch + t] = hist[t];
+    for (int t = tid; t < nch; t += LONG_NT) {
+      wg_hist[wg * nch + t] = hist[t];
+      if constexpr (DIRECT) wg_dhist[wg * nch + t] = dhist[t];
+    }
+    if (DIRECT && tid == 0) wg_nlong[wg] = nlong;
   }
 }
 
@@ -1101,17 +1237,36 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
 // gathers; ~10 passes over arrays of ~2e9 entries per R-MAT 24 batch).  Per
 // (row, chunk): the histogram counts of the row's workgroups (consecutive:
 // wg0[r] .. wg0[r] + nwg[r]) become each workgroup's offset inside the
-// (row, chunk) scratch region, in place; the region sizes go to cnt.
+// (row, chunk) scratch region, in place; the routed counts go to cnt.
+// Direct mode (dhist given): T = short-row products, D = long-row products;
+// an item of more than LR_CAP products with D > 0 takes D directly (mode 1:
+// dcnt = D, cnt = T); otherwise its long products are routed with the short
+// ones under the same per-workgroup offsets (mode 0: cnt = T + D; mode 2
+// when D = 0).
 __global__ __launch_bounds__(256) void long_wg_scan(int32_t* __restrict__ hist, const int64_t* __restrict__ wg0,
                                                    const int64_t* __restrict__ nwg, int nch,
-                                                   int64_t* __restrict__ cnt) {
+                                                   int64_t* __restrict__ cnt, const int32_t* __restrict__ dhist,
+                                                   int64_t* __restrict__ dcnt, uint8_t* __restrict__ mode,
+                                                   int64_t dmin) {
   const int64_t r = blockIdx.x;
   const int k = blockIdx.y * 256 + threadIdx.x;
   if (k >= nch) return;
   const int64_t w0 = wg0[r], w1 = w0 + nwg[r];
+  bool with_long = false;
+  if (dhist != nullptr) {
+    int64_t T = 0, D = 0;
+    for (int64_t w = w0; w < w1; ++w) {
+      T += hist[w * nch + k];
+      D += dhist[w * nch + k];
+    }
+    const uint8_t md = D == 0 ? 2 : (T + D > dmin ? 1 : 0);
+    mode[r * nch + k] = md;
+    dcnt[r * nch + k] = md == 1 ? D : 0;
+    with_long = md == 0;
+  }
   int64_t run = 0;
   for (int64_t w = w0; w < w1; ++w) {   // consecutive threads: consecutive chunks of one row (coalesced)
-    const int32_t v = hist[w * nch + k];
+    const int32_t v = hist[w * nch + k] + (with_long ? dhist[w * nch + k] : 0);
     hist[w * nch + k] = (int32_t)run;
     run += v;
   }
@@ -1144,18 +1299,6 @@ __global__ __launch_bounds__(256) void long_btab(const int64_t* __restrict__ Brp
   tab[t] = (uint32_t)(lo - r0);
 }
 
-// 64-lane inclusive prefix sum on the DPP network (VALU; no LDS traffic):
-// row_shr 1/2/4/8 inside 16-lane rows, then row_bcast:15 / row_bcast:31.
-__device__ __forceinline__ int wave_incl_scan_dpp(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
-  return x;
-}
-
 // Persistent: a workgroup walks (row, chunk) items rt = blockIdx.x,
 // + gridDim.x, ...  At R-MAT scale 24 (2^24 columns = 1024 chunks per hub
 // row) an item averages ~500 products, so the fixed per-item LDS work of a
@@ -1165,18 +1308,35 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x) {
 // runs once per workgroup), the block scan runs on DPP instead of LDS
 // permutes, empty items cost nothing, and the next item's counts and first
 // scratch loads are in flight during the current write-back.
-template <bool VALUES>
+// Direct products (dt_cnt given): after an item's routed products, the row's
+// long entries (dl[dl_rp[r] .. dl_rp[r + 1]) are taken in blocks of 64 (lane
+// = entry: its B segment in this chunk from btab) and expanded into
+// 64-product windows (wave_slot_owner); DU windows at a time are folded into
+// the accumulator, their B loads in flight together.  A row of >= NW blocks
+// gives each wave whole blocks; a row of fewer spreads every block's windows
+// over all the waves (one hub B row can hold all of an item's products).
+constexpr int LONG_DU = 4;
+template <bool VALUES, bool DIRECT>
 __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restrict__ list,
                                                          const int32_t* __restrict__ nlist,
                                                          const int64_t* __restrict__ rt_off,
                                                          const int64_t* __restrict__ rt_cnt, int nch,
                                                          unsigned long long* __restrict__ scratch,
-                                                         int64_t* __restrict__ rt_nnz) {
+                                                         int64_t* __restrict__ rt_nnz,
+                                                         const int64_t* __restrict__ dt_cnt,
+                                                         const uint4* __restrict__ dl,
+                                                         const int64_t* __restrict__ dl_rp,
+                                                         const uint32_t* __restrict__ btab,
+                                                         const int32_t* __restrict__ Bci,
+                                                         const float* __restrict__ Bv) {
+  constexpr int NW = LONG_DNT / 64;
   __shared__ float vals[VALUES ? LONG_W : 1];
   __shared__ uint32_t bits[LONG_W / 32];
   __shared__ int wsum[LONG_DNT / 64];
+  __shared__ int own_all[DIRECT ? NW : 1][64];
+  __shared__ uint2 seg_all[DIRECT ? NW : 1][64];
+  __shared__ float sa_all[DIRECT ? NW : 1][64];
   static_assert(LONG_W / 32 == LONG_DNT, "one occupancy word per thread");
-  constexpr int NW = LONG_DNT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   bits[tid] = 0u;
   if constexpr (VALUES)
@@ -1213,6 +1373,82 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
       for (int u = 0; u < LONG_DL; ++u) {
         const int64_t i = i0 + u * LONG_DNT;
         x[u] = i < n ? scratch[base + i] : ~0ull;
+      }
+    }
+    if (DIRECT && dt_cnt[rt] > 0) {   // uniform: direct products
+      const int64_t r = rt / nch;
+      const int t = (int)(rt % nch);
+      const int64_t d0 = dl_rp[r], d1 = dl_rp[r + 1];
+      const int nb = (int)((d1 - d0 + 63) >> 6);
+      // >= NW blocks of 64 long entries: a wave per block; fewer: every wave
+      // expands every block and takes every NW-th of its 64-product windows
+      const bool share = nb < NW;
+      int* own = own_all[w];
+      uint2* sg = seg_all[w];
+      float* sa = sa_all[w];
+      int gwin = 0;   // (share) windows of the blocks before this one
+      for (int b = share ? 0 : w; b < nb; b += share ? 1 : NW) {
+        const int64_t i = d0 + ((int64_t)b << 6) + lane;
+        int len = 0;
+        uint32_t st = 0;
+        float a = 0.f;
+        if (i < d1) {
+          const uint4 e = dl[i];
+          const uint32_t* tk = btab + (int64_t)e.y * (nch + 1);
+          const uint32_t s0 = tk[t];
+          len = (int)(tk[t + 1] - s0);
+          st = e.x + s0;
+          a = __uint_as_float(e.z);
+        }
+        const int incl = wave_incl_scan_dpp(len);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        if (tot == 0) continue;   // uniform
+        const int pre = incl - len;
+        const int nwin = (tot + 63) >> 6;
+        sg[lane] = make_uint2(st, (uint32_t)pre);
+        sa[lane] = a;
+        // this wave's windows: j0, j0 + js, ... (all of them unless shared)
+        const int j0 = share ? (w - gwin % NW + NW) % NW : 0;
+        const int js = share ? NW : 1;
+        gwin += nwin;
+        for (int j = j0; j < nwin; j += js * LONG_DU) {
+          uint32_t f[LONG_DU];
+          float av[LONG_DU];
+          bool ok[LONG_DU];
+#pragma unroll
+          for (int u = 0; u < LONG_DU; ++u) {
+            const int q0 = (j + u * js) << 6;
+            ok[u] = false;
+            f[u] = 0u;
+            av[u] = 0.f;
+            if (q0 < tot) {   // uniform
+              const int o = wave_slot_owner(pre, len, q0, lane, own);
+              const int q = q0 + lane;
+              if (q < tot) {
+                const uint2 g = sg[o];
+                f[u] = g.x + (uint32_t)(q - (int)g.y);
+                av[u] = sa[o];
+                ok[u] = true;
+              }
+            }
+          }
+          int cc[LONG_DU];
+          float vv[LONG_DU];
+#pragma unroll
+          for (int u = 0; u < LONG_DU; ++u) {
+            cc[u] = ok[u] ? Bci[f[u]] : -1;
+            vv[u] = 0.f;
+            if constexpr (VALUES) vv[u] = ok[u] ? Bv[f[u]] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < LONG_DU; ++u) {
+            if (cc[u] < 0) continue;
+            const int c = cc[u] - c0;
+            atomicOr(&bits[c >> 5], 1u << (c & 31));
+            if constexpr (VALUES) atomicAdd(&vals[c], av[u] * vv[u]);
+          }
+        }
+        lr_wave_fence();   // seg / sa reads done before the next block's writes
       }
     }
     __syncthreads();
@@ -1267,16 +1503,6 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
 //   its bitmap and takes the next item (rt += waves in the grid).
 // LDS ops of one wave complete in issue order, so the phases only need the
 // compiler not to move LDS accesses across them (wave-scope fences).
-constexpr int LR_R = 16, LR_CAP = LR_R * 64, LR_WAVES = 4;
-constexpr int LR_WORDS = LONG_W / 64;   // 64-bit bitmap words per chunk
-static_assert(LR_WORDS % 64 == 0, "whole bitmap rows per lane");
-
-__device__ __forceinline__ void lr_wave_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <bool VALUES>
 __global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int32_t* __restrict__ list,
                                                            const int32_t* __restrict__ nlist,
@@ -1367,16 +1593,19 @@ __global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int32_t* __rest
 // Empty items get their zero count here.  The persistent kernels then walk
 // only their own items: a walk over all items costs a dependent count load
 // per skipped item (R-MAT 24: 82 % of the items are long_rank's).
+// Items with direct products (dt_cnt > 0) always go to long_dense.
 __global__ __launch_bounds__(256) void long_partition(const int64_t* __restrict__ rt_cnt, int64_t nrt, int64_t small,
                                                       int32_t* __restrict__ rank_list,
                                                       int32_t* __restrict__ dense_list, int32_t* __restrict__ nl,
-                                                      int64_t* __restrict__ rt_nnz) {
+                                                      int64_t* __restrict__ rt_nnz,
+                                                      const int64_t* __restrict__ dt_cnt) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t n = i < nrt ? rt_cnt[i] : 0;
-  if (i < nrt && n == 0) rt_nnz[i] = 0;
-  const bool r = n > 0 && n <= small;
-  const bool d = n > 0 && n > small;
+  const int64_t dn = (i < nrt && dt_cnt != nullptr) ? dt_cnt[i] : 0;
+  if (i < nrt && n == 0 && dn == 0) rt_nnz[i] = 0;
+  const bool r = dn == 0 && n > 0 && n <= small;
+  const bool d = dn > 0 || n > small;
   const unsigned long long mr = __ballot(r), md = __ballot(d);
   int br = 0, bd = 0;
   if (lane == 0) {
@@ -1691,34 +1920,60 @@ SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const fl
                                        const int32_t* Bci, const float* Bv, const int64_t* wg_e0,
                                        const int64_t* wg_e1, int64_t nwg, int nch, int32_t* wg_hist,
                                        const int32_t* wg_row, const int64_t* row_off, void* scratch,
-                                       const int32_t* lidx, const uint32_t* btab, void* stream) {
+                                       const int32_t* lidx, const uint32_t* btab, int32_t* wg_dhist,
+                                       int32_t* wg_nlong, const uint8_t* rt_mode, void* dl, const int64_t* dl_off,
+                                       void* stream) {
   // histogram pass: wg_hist out; lidx / btab (optional): B row -> long-row
   // index or -1, and the long rows' chunk offsets (spmm_spgemm_long_btab).
+  // Direct mode: wg_dhist / wg_nlong out (the long rows' counts apart).
   // scatter pass: wg_hist = per-workgroup offsets (spmm_spgemm_long_wg_scan),
-  // wg_row = each workgroup's row in the batch, row_off = region bases.
+  // wg_row = each workgroup's row in the batch, row_off = region bases;
+  // direct mode: lidx, btab, rt_mode, dl, dl_off (see long_route).
   if (nwg <= 0) return 0;
   if (nch > LONG_MAXCH) return (int)hipErrorInvalidValue;
   if ((lidx == nullptr) != (btab == nullptr)) return (int)hipErrorInvalidValue;
   if (scatter && (wg_row == nullptr || row_off == nullptr)) return (int)hipErrorInvalidValue;
+  if (!scatter && (wg_dhist != nullptr) && (lidx == nullptr || wg_nlong == nullptr)) return (int)hipErrorInvalidValue;
+  if (scatter && dl != nullptr && (lidx == nullptr || rt_mode == nullptr || dl_off == nullptr))
+    return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (scatter)
-    hipLaunchKernelGGL(long_route<true>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0, wg_e1,
-                       nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, nullptr, nullptr);
+  if (scatter && dl != nullptr)
+    hipLaunchKernelGGL((long_route<true, true>), dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0,
+                       wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, lidx, btab, nullptr, nullptr,
+                       rt_mode, (uint4*)dl, dl_off);
+  else if (scatter)
+    hipLaunchKernelGGL((long_route<true, false>), dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv,
+                       wg_e0, wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
+  else if (wg_dhist != nullptr)
+    hipLaunchKernelGGL((long_route<false, true>), dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv,
+                       wg_e0, wg_e1, nch, wg_hist, nullptr, nullptr, (unsigned long long*)scratch, lidx, btab,
+                       wg_dhist, wg_nlong, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(long_route<false>, dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0,
-                       wg_e1, nch, wg_hist, nullptr, nullptr, (unsigned long long*)scratch, lidx, btab);
+    hipLaunchKernelGGL((long_route<false, false>), dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv,
+                       wg_e0, wg_e1, nch, wg_hist, nullptr, nullptr, (unsigned long long*)scratch, lidx, btab,
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
 
 // In place: routing histogram -> per-workgroup offsets inside each (row,
-// chunk) region; cnt[r * nch + k] = region sizes.  wg0 / nwg: int64 [R].
+// chunk) region; cnt[r * nch + k] = routed counts.  wg0 / nwg: int64 [R].
+// Direct mode (dhist): dcnt = direct counts, mode = item modes (long_wg_scan).
 SPMM_EXPORT int spmm_spgemm_long_wg_scan(int32_t* wg_hist, const int64_t* wg0, const int64_t* nwg, int64_t R,
-                                         int nch, int64_t* cnt, void* stream) {
+                                         int nch, int64_t* cnt, const int32_t* dhist, int64_t* dcnt, uint8_t* mode,
+                                         void* stream) {
   if (R <= 0) return 0;
   if (nch > LONG_MAXCH || R > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  if (dhist != nullptr && (dcnt == nullptr || mode == nullptr)) return (int)hipErrorInvalidValue;
+  // items of more than dmin products take their long products directly
+  // (SPMM_LONG_DIRECT_MIN, default LR_CAP: the smaller ones are long_rank's)
+  static const int64_t dmin = [] {
+    const char* e = getenv("SPMM_LONG_DIRECT_MIN");
+    return e ? (int64_t)atoll(e) : (int64_t)LR_CAP;
+  }();
   hipLaunchKernelGGL(long_wg_scan, dim3((unsigned)R, (unsigned)((nch + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, wg_hist, wg0, nwg, nch, cnt);
+                     (hipStream_t)stream, wg_hist, wg0, nwg, nch, cnt, dhist, dcnt, mode, dmin);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -1735,10 +1990,16 @@ SPMM_EXPORT int spmm_spgemm_long_btab(const int64_t* Brp, const int32_t* Bci, co
 }
 
 SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_cnt, int64_t nrt, int nch,
-                                       void* scratch, int64_t* rt_nnz, int32_t* ws, void* stream) {
+                                       void* scratch, int64_t* rt_nnz, int32_t* ws, const int64_t* dt_cnt,
+                                       const void* dl, const int64_t* dl_rp, const uint32_t* btab, const int32_t* Bci,
+                                       const float* Bv, void* stream) {
   // ws: 2 * nrt + 2 int32 (the two work lists and their lengths)
+  // direct products (optional): dt_cnt per item, dl / dl_rp the batch rows'
+  // long entries (long_route), btab, B
   if (nrt <= 0) return 0;
   if (nrt >= (int64_t(1) << 31)) return (int)hipErrorInvalidValue;
+  if (dt_cnt != nullptr && (dl == nullptr || dl_rp == nullptr || btab == nullptr || Bci == nullptr || Bv == nullptr))
+    return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   static int ncu = 0;
   if (ncu == 0) {
@@ -1759,7 +2020,7 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
   hipError_t e = hipMemsetAsync(nl, 0, 2 * sizeof(int32_t), s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(long_partition, dim3((unsigned)((nrt + 255) / 256)), dim3(256), 0, s, rt_cnt, nrt,
-                     use_rank ? (int64_t)LR_CAP : int64_t(0), rank_list, dense_list, nl, rt_nnz);
+                     use_rank ? (int64_t)LR_CAP : int64_t(0), rank_list, dense_list, nl, rt_nnz, dt_cnt);
   SPMM_LAUNCH_CHECK();
   // persistent grids at the resident capacity (list lengths are device-side)
   if (use_rank) {
@@ -1772,17 +2033,20 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
                          (unsigned long long*)scratch, rt_nnz);
     SPMM_LAUNCH_CHECK();
   }
-  int per = 0;   // resident workgroups per CU (LDS-bound with values: 132 KB at W = 2^15)
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, values ? long_dense<true> : long_dense<false>, LONG_DNT, 0) !=
-          hipSuccess || per <= 0)
-    per = 1;
-  const unsigned grid = (unsigned)std::min<int64_t>(nrt, (int64_t)per * ncu);
-  if (values)
-    hipLaunchKernelGGL(long_dense<true>, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
-                       (unsigned long long*)scratch, rt_nnz);
-  else
-    hipLaunchKernelGGL(long_dense<false>, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
-                       (unsigned long long*)scratch, rt_nnz);
+  auto launch = [&](auto kern) {
+    int per = 0;   // resident workgroups per CU (LDS-bound with values: 132 KB at W = 2^15)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, LONG_DNT, 0) != hipSuccess || per <= 0) per = 1;
+    const unsigned grid = (unsigned)std::min<int64_t>(nrt, (int64_t)per * ncu);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
+                       (unsigned long long*)scratch, rt_nnz, dt_cnt, (const uint4*)dl, dl_rp, btab, Bci, Bv);
+  };
+  if (dt_cnt != nullptr) {
+    if (values) launch(long_dense<true, true>);
+    else launch(long_dense<false, true>);
+  } else {
+    if (values) launch(long_dense<true, false>);
+    else launch(long_dense<false, false>);
+  }
   SPMM_LAUNCH_CHECK();
   return 0;
 }

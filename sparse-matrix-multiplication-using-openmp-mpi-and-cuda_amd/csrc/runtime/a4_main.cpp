@@ -966,7 +966,10 @@ int main(int argc, char** argv) {
   try {
     rc = a4::run(o, rank, world, t_start);
   } catch (const std::exception& e) {
-    std::cerr << "a4 rank " << rank << ": " << e.what() << std::endl;
+    // one write(2): a peer's MPI_Abort may end this process between two writes
+    const std::string msg = "a4 rank " + std::to_string(rank) + ": " + e.what() + "\n";
+    std::fwrite(msg.data(), 1, msg.size(), stderr);
+    std::fflush(stderr);
     MPI_Abort(MPI_COMM_WORLD, 1);   // fail fast: peers blocked in a transfer are torn down
     return 1;
   }

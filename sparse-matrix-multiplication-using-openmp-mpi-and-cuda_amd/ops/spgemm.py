@@ -25,6 +25,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from .. import _native
@@ -46,10 +47,11 @@ _native.register_hip("spmm_spgemm_lds", C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, c_
                      C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_compact", c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, c_vp,
-                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_long_wg_scan", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
+                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_wg_scan", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_btab", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                     c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
@@ -267,6 +269,16 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
     ``Crp[row]`` (and its count to ``out_nnz`` when given).  Rows are
     processed in batches whose products fit the scratch budget.
 
+    Direct mode (``CONFIG.spgemm_long_direct``, B with long rows): items of
+    more than LR_CAP products take the products of the row's long B rows
+    straight from B (long_dense reads their chunk segments through the btab
+    table) instead of through the scratch.
+
+    The batches are planned on the host from ONE read-back of the rows'
+    product and entry counts, and the loop has no device->host sync (buffers
+    are sized from that plan); the product-count consistency checks
+    accumulate on the device and are read once at the end.
+
     ``defer``: instead of placing the rows at ``Crp``, append each batch's
     ``(rows, rt_off, rt_nnz, scratch)`` (chunk results still in the scratch)
     so the caller places them at final offsets once those are known
@@ -278,67 +290,99 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
     nch = (B.n + (1 << lgw) - 1) >> lgw
     if nch > maxch:
         raise ValueError(f"long-row path supports at most {maxch << lgw} columns, got {B.n}")
-    cap = max(GLOBAL_WS_BYTES // 8, int(nprod_rows.max()))
     lidx, btab = _long_btab(B, nch) if CONFIG.spgemm_long_btab else (None, None)
+    direct = bool(CONFIG.spgemm_long_direct) and btab is not None and B.nnz < (1 << 32)
     rows = rows.long()
-    csum = torch.cumsum(nprod_rows.long(), 0)
     nrows = rows.numel()
+    if nrows == 0:
+        return
+    na_all = (A.rowptr[rows + 1] - A.rowptr[rows])
+    host = torch.stack([nprod_rows.long(), na_all]).cpu()   # the one planning read-back
+    np_h, na_h = host[0].numpy(), host[1].numpy()
+    csum_h = np.cumsum(np_h)
+    cap = max(GLOBAL_WS_BYTES // 8, int(np_h.max()))
+    nwg_h = np.maximum((na_h + epw - 1) // epw, 1)
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)   # rows whose counts disagree (device-side)
+    nil = None
     start, done = 0, 0
     while start < nrows:
-        # batch = the longest run of rows from start whose products fit cap (at
-        # least one row): one device search per batch, not a host walk per row
-        end = int(torch.searchsorted(csum, torch.tensor([done + cap], device=csum.device), right=True))
+        # batch = the longest run of rows from start whose products fit cap (at least one row)
+        end = int(np.searchsorted(csum_h, done + cap, side="right"))
         end = min(max(end, start + 1), nrows)
         rb = rows[start:end]
         R = end - start
+        nwg = int(nwg_h[start:end].sum())
         a0 = A.rowptr[rb]
-        na = A.rowptr[rb + 1] - a0
+        na = na_all[start:end]
         nwg_r = torch.clamp((na + epw - 1) // epw, min=1)
-        nwg = int(nwg_r.sum())
-        row_of_wg = torch.repeat_interleave(torch.arange(R, device=dev), nwg_r)
+        row_of_wg = torch.repeat_interleave(torch.arange(R, device=dev), nwg_r, output_size=nwg)
         first_wg = torch.cumsum(nwg_r, 0) - nwg_r
         kk = torch.arange(nwg, device=dev) - first_wg[row_of_wg]
         wg_e0 = (a0[row_of_wg] + kk * epw).contiguous()
         wg_e1 = torch.minimum(wg_e0 + epw, (a0 + na)[row_of_wg]).contiguous()
         wg_hist = torch.empty(nwg * nch, dtype=torch.int32, device=dev)
-        nil = None
+        wg_dhist = torch.empty(nwg * nch, dtype=torch.int32, device=dev) if direct else None
+        wg_nlong = torch.empty(nwg, dtype=torch.int32, device=dev) if direct else None
         _native.check(lib.spmm_spgemm_long_route(0, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
                                                  P(wg_e1), nwg, nch, P(wg_hist), nil, nil, nil,
                                                  P(lidx) if lidx is not None else nil,
-                                                 P(btab) if btab is not None else nil, stream), "long_route")
+                                                 P(btab) if btab is not None else nil,
+                                                 P(wg_dhist) if direct else nil, P(wg_nlong) if direct else nil,
+                                                 nil, nil, nil, stream), "long_route")
         # the [workgroups x chunks] histogram becomes per-workgroup offsets in
         # place (one kernel); only the [rows x chunks] region sizes go through
         # torch
         T = torch.empty((R, nch), dtype=torch.int64, device=dev)
-        _native.check(lib.spmm_spgemm_long_wg_scan(P(wg_hist), P(first_wg), P(nwg_r), R, nch, P(T), stream),
-                      "long_wg_scan")
-        chunk_off = torch.cumsum(T, 1) - T
-        row_tot = T.sum(1)
-        row_base = torch.cumsum(row_tot, 0) - row_tot
+        D = torch.empty((R, nch), dtype=torch.int64, device=dev) if direct else None
+        mode = torch.empty(R * nch, dtype=torch.uint8, device=dev) if direct else None
+        _native.check(lib.spmm_spgemm_long_wg_scan(P(wg_hist), P(first_wg), P(nwg_r), R, nch, P(T),
+                                                   P(wg_dhist) if direct else nil, P(D) if direct else nil,
+                                                   P(mode) if direct else nil, stream), "long_wg_scan")
+        del wg_dhist
+        # scratch regions: the routed products; a direct item also holds its
+        # compacted result (<= min(W, all its products) entries)
+        region = torch.maximum(T, torch.clamp(T + D, max=1 << lgw)) if direct else T
+        chunk_off = torch.cumsum(region, 1) - region
+        row_reg = region.sum(1)
+        row_base = torch.cumsum(row_reg, 0) - row_reg
         # the scatter pass writes exactly the histogram's slots: a histogram
-        # that disagrees with the rows' product counts would overrun them
-        ntot, nbad = torch.stack([row_tot.sum(), (row_tot != nprod_rows[start:end]).sum()]).tolist()
-        if nbad:
-            raise RuntimeError(f"spgemm long rows: routing histogram disagrees with the product counts ({nbad} rows)")
-        scratch = torch.empty(ntot, dtype=torch.int64, device=dev)
+        # that disagrees with the rows' product counts is an invariant failure
+        # (checked once after the loop; the scratch is sized by the histogram)
+        bad += ((T + D).sum(1) if direct else T.sum(1)).ne(nprod_rows[start:end]).sum()
         rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()   # each (row, chunk) region's base
+        # sizes from the host plan (no read-back): the regions never exceed the
+        # batch's products, the long-entry list never its A entries
+        if direct:
+            nl_r = wg_nlong.long()
+            dl_off = (torch.cumsum(nl_r, 0) - nl_r).contiguous()
+            dl_rp = torch.cat([dl_off[first_wg], (dl_off[-1:] + nl_r[-1:])]).contiguous()
+            dl = torch.empty((max(int(na_h[start:end].sum()), 1), 4), dtype=torch.int32, device=dev)
+        ntot = int(csum_h[end - 1]) - done
+        scratch = torch.empty(max(ntot, 1), dtype=torch.int64, device=dev)
         wg_row = row_of_wg.to(torch.int32)
         _native.check(lib.spmm_spgemm_long_route(1, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
-                                                 P(wg_e1), nwg, nch, P(wg_hist), P(wg_row), P(rt_off), P(scratch), nil,
-                                                 nil, stream), "long_route")
+                                                 P(wg_e1), nwg, nch, P(wg_hist), P(wg_row), P(rt_off), P(scratch),
+                                                 P(lidx) if direct else nil, P(btab) if direct else nil, nil, nil,
+                                                 P(mode) if direct else nil, P(dl) if direct else nil,
+                                                 P(dl_off) if direct else nil, stream), "long_route")
         del wg_hist, wg_row
         rt_cnt = T.reshape(-1)
         if LONG_STATS is not None:
-            _long_stats(rt_cnt)
+            _long_stats(rt_cnt + D.reshape(-1) if direct else rt_cnt)
         rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
         lists = torch.empty(2 * R * nch + 2, dtype=torch.int32, device=dev)   # the two kernels' item lists
         _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
-                                                 P(lists), stream), "long_dense")
+                                                 P(lists), P(D) if direct else nil, P(dl) if direct else nil,
+                                                 P(dl_rp) if direct else nil, P(btab) if direct else nil,
+                                                 P(B.col) if direct else nil, P(B.val) if direct else nil, stream),
+                      "long_dense")
         del lists
+        if direct:
+            del dl, dl_rp, dl_off, mode
         nnz_rt = rt_nnz.view(R, nch)
         nnz_r = nnz_rt.sum(1)
-        if expect_nnz is not None and not torch.equal(nnz_r, expect_nnz[rb].long()):
-            raise RuntimeError("spgemm long rows: numeric count differs from the symbolic count")
+        if expect_nnz is not None:
+            bad += nnz_r.ne(expect_nnz[rb].long()).sum()
         if out_nnz is not None:
             out_nnz[rb] = nnz_r.to(out_nnz.dtype)
         if values and defer is not None:
@@ -348,8 +392,12 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
             _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
                                                      P(Cv), stream), "long_place")
         del scratch
-        done = int(csum[end - 1])
+        done = int(csum_h[end - 1])
         start = end
+    nbad = int(bad)
+    if nbad:
+        raise RuntimeError(f"spgemm long rows: routing histogram or numeric count disagrees with the product / "
+                           f"symbolic counts ({nbad} rows)")
 
 
 def place_long(defer: list, rowptr: torch.Tensor, Cci: torch.Tensor, Cv: torch.Tensor, stream) -> None:

@@ -58,6 +58,10 @@ class Config:
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     # long-row routing histogram reads a chunk-offset table for the long rows of B (1) or their columns (0)
     spgemm_long_btab: int = field(default_factory=lambda: _env("SPMM_SPGEMM_LONG_BTAB", 1, int))
+    # long rows: items of > LR_CAP products read their long B rows' products
+    # straight from B (no scratch round trip; needs spgemm_long_btab).  Off by
+    # default: R-MAT 24 17.0 s vs 16.1 s (PERF_LOG "direct long-row products")
+    spgemm_long_direct: int = field(default_factory=lambda: _env("SPMM_SPGEMM_LONG_DIRECT", 0, int))
     # MFMA panel SpMM when the panel column reuse reaches this.  At reuse 1.03
     # (65536^2 @ 0.1 % x 128 cols, BASELINE config 3, which names the MFMA path)
     # the two kernels are within 5 %: MFMA 149 us, row kernel 142 us (PERF_LOG)

@@ -870,14 +870,64 @@ def test_spgemm_gpu_long_rows_btab_histogram(monkeypatch, onepass):
     lidx, btab = OS._long_btab(Bd, (n + (1 << OS._long_params()[0]) - 1) >> OS._long_params()[0])
     assert lidx is not None and int((lidx >= 0).sum()) == int(((B.rowptr[1:] - B.rowptr[:-1]) >= 4 * 33).sum())
     monkeypatch.setattr(CONFIG, "spgemm_onepass", onepass)
-    for tab in (1, 0):
+    for tab, direct in ((1, 1), (1, 0), (0, 0)):
         monkeypatch.setattr(CONFIG, "spgemm_long_btab", tab)
+        monkeypatch.setattr(CONFIG, "spgemm_long_direct", direct)
         info = SG.SpgemmInfo()
         Cg = SG.spgemm(Ad, Bd, info)
         assert SG.NUM_GLOBAL in info.rows_per_bin_num
         assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
         assert torch.equal(Cg.col.cpu(), Cc.col)
         assert torch.equal(Cg.val.cpu(), Cc.val)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("onepass", ["on", "off"])
+def test_spgemm_gpu_long_rows_direct_products(monkeypatch, onepass):
+    """Direct long-row products: items of > 1024 products read their long B
+    rows' chunk segments straight from B (long_dense), items of <= 1024
+    products route them through the scratch with the short rows (long_rank,
+    mode 0), rows without long B rows stay routed; hub rows with 0, 1 and many
+    64-entry blocks of long entries.  C equals the CPU product exactly (small
+    integers) and the run with the direct mode off."""
+    from spmm_amd.utils.config import CONFIG
+
+    k, n = 9000, (1 << 22) + 5                     # 129 column chunks, a partial last one
+    g = torch.Generator().manual_seed(17)
+    r_ = torch.arange(k)
+    lens = torch.where(r_ % 50 == 0, 6000, torch.where(r_ % 7 == 0, 600, 12))   # hub / long (>= 4 * 129) / short
+    rr = torch.repeat_interleave(r_, lens)
+    cc = torch.randint(0, n, (rr.numel(),), generator=g)   # (rare repeats are summed)
+    B = CS.from_coo(rr, cc, torch.randint(-3, 4, (rr.numel(),), generator=g).float(), k, n)
+    ra, ca = [], []
+    short = torch.tensor([r for r in range(k) if r % 7 and r % 50])
+    for r, na in enumerate([4000, 500, 1500, 0, 800]):
+        ra.append(torch.full((na,), r))
+        ca.append(torch.randperm(k, generator=g)[:na])
+    ra.append(torch.full((6000,), 5))                  # a hub row over short B rows only: no long entries
+    ca.append(short[torch.randperm(short.numel(), generator=g)[:6000]])
+    light = gen_csr.uniform_csr(30, k, 0.001, seed=18)
+    ra.append(light.row_ids() + 6)
+    ca.append(light.col.long())
+    ra, ca = torch.cat(ra), torch.cat(ca)
+    A = CS.from_coo(ra, ca, torch.randint(-2, 3, (ra.numel(),), generator=g).float(), 36, k)
+    Cc = SG.spgemm(A, B)
+    dev = torch.device("cuda")
+    Ad, Bd = A.to(dev), B.to(dev)
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", onepass)
+    outs = []
+    for direct in (1, 0):
+        monkeypatch.setattr(CONFIG, "spgemm_long_direct", direct)
+        info = SG.SpgemmInfo()
+        Cg = SG.spgemm(Ad, Bd, info)
+        assert SG.NUM_GLOBAL in info.rows_per_bin_num
+        assert torch.equal(Cg.rowptr.cpu(), Cc.rowptr)
+        assert torch.equal(Cg.col.cpu(), Cc.col)
+        assert torch.equal(Cg.val.cpu(), Cc.val)
+        outs.append(Cg)
+    # both modes' item sizes: long rows with items above and below 1024 products
+    nprod = SG.row_nprod(Ad, Bd).cpu()
+    assert int((nprod[:6] > 1024 * 129).sum()) >= 2 and int(((nprod[:6] > 60000) & (nprod[:6] < 1024 * 129)).sum()) >= 1
 
 
 def test_streamed_spgemm_splits_panels_on_oom(monkeypatch):
