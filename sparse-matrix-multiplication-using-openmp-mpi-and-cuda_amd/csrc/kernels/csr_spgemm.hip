@@ -1916,6 +1916,17 @@ SPMM_EXPORT int spmm_spgemm_esc_ordered(const int64_t* Arp, const int32_t* Aci, 
 }
 
 // ---- long rows (see the kernels' comment) -----------------------------------
+// Diagnostic (SPMM_LONG_ROUTE_LDS_PAD = bytes of dynamic LDS): fewer scatter
+// workgroups per CU, so fewer (workgroup, chunk) write runs are open in an
+// XCD's L2 at once.
+static size_t route_lds_pad() {
+  static const size_t pad = [] {
+    const char* e = getenv("SPMM_LONG_ROUTE_LDS_PAD");
+    return e ? (size_t)atoll(e) : (size_t)0;
+  }();
+  return pad;
+}
+
 SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp,
                                        const int32_t* Bci, const float* Bv, const int64_t* wg_e0,
                                        const int64_t* wg_e1, int64_t nwg, int nch, int32_t* wg_hist,
@@ -1942,7 +1953,7 @@ SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const fl
                        wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, lidx, btab, nullptr, nullptr,
                        rt_mode, (uint4*)dl, dl_off);
   else if (scatter)
-    hipLaunchKernelGGL((long_route<true, false>), dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv,
+    hipLaunchKernelGGL((long_route<true, false>), dim3((unsigned)nwg), dim3(LONG_NT), route_lds_pad(), s, Aci, Av, Brp, Bci, Bv,
                        wg_e0, wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, nullptr, nullptr,
                        nullptr, nullptr, nullptr, nullptr, nullptr);
   else if (wg_dhist != nullptr)

@@ -342,6 +342,81 @@ __global__ __launch_bounds__(NT) void spmm_rowwise(const int64_t* __restrict__ r
   }
 }
 
+// spmm_rowwise_v8 — the row kernel with 16-byte gathers (D % 8 == 0, X
+// 16-byte aligned).  Lane = (group g = lane / 16, part p = lane % 16): part p
+// owns output columns d0 + 8p .. d0 + 8p + 7 of every 128, group g takes the
+// row's entries g, g + 4, g + 8, ...  One load instruction gathers four X rows
+// (4 x 256 B instead of one), RW8_DEPTH loads in flight per lane cover
+// 4 * RW8_DEPTH entries, so a 65-entry row needs ~2 memory latencies instead
+// of ~5; the four groups' partial sums meet in two cross-lane adds.
+constexpr int RW8_DEPTH = 8;
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(NT) void spmm_rowwise_v8(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                      const unsigned short* __restrict__ av,
+                                                      const unsigned short* __restrict__ X, int64_t ldx, int64_t m,
+                                                      int64_t D, void* __restrict__ Yv, int64_t ldy) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, p = lane & 15;
+  const int64_t row = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= m) return;   // wave-uniform
+  const int64_t e0 = rp[row], e1 = rp[row + 1];
+  for (int64_t d0 = 0; d0 < D; d0 += 128) {
+    const int64_t col = d0 + 8 * p;
+    const bool live = col < D;
+    const unsigned short* Xc = X + (live ? col : 0);
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    for (int64_t eb = e0; eb < e1; eb += 64) {   // 64 entries per lane-round
+      const int ne = (int)(e1 - eb < 64 ? e1 - eb : 64);
+      const int myj = lane < ne ? ci[eb + lane] : 0;
+      const float mya = lane < ne ? bf2f(av[eb + lane]) : 0.f;
+      for (int k0 = 0; k0 < ne; k0 += 4 * RW8_DEPTH) {
+        uint4 x[RW8_DEPTH];
+        float a[RW8_DEPTH];
+#pragma unroll
+        for (int u = 0; u < RW8_DEPTH; ++u) {
+          const int k = k0 + 4 * u + g;
+          const int kk = k < ne ? k : 0;   // (past the row: entry 0 reloaded, not accumulated)
+          const int j = __shfl(myj, kk);
+          a[u] = __shfl(mya, kk);
+          x[u] = *reinterpret_cast<const uint4*>(Xc + (int64_t)j * ldx);
+        }
+#pragma unroll
+        for (int u = 0; u < RW8_DEPTH; ++u) {
+          if (k0 + 4 * u < ne && k0 + 4 * u + g < ne) {
+            const unsigned w4[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              s[2 * h] += a[u] * bf2f((unsigned short)(w4[h] & 0xFFFF));
+              s[2 * h + 1] += a[u] * bf2f((unsigned short)(w4[h] >> 16));
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s[i] += __shfl_xor(s[i], 16);
+      s[i] += __shfl_xor(s[i], 32);
+    }
+    if (g == 0 && live) {
+      if (OUT_BF16) {
+        uint4 o;
+        o.x = (unsigned)f2bf(s[0]) | ((unsigned)f2bf(s[1]) << 16);
+        o.y = (unsigned)f2bf(s[2]) | ((unsigned)f2bf(s[3]) << 16);
+        o.z = (unsigned)f2bf(s[4]) | ((unsigned)f2bf(s[5]) << 16);
+        o.w = (unsigned)f2bf(s[6]) | ((unsigned)f2bf(s[7]) << 16);
+        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned short*>(Yv) + row * ldy + col) = o;
+      } else {
+        float4* Y = reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + row * ldy + col);
+        Y[0] = make_float4(s[0], s[1], s[2], s[3]);
+        Y[1] = make_float4(s[4], s[5], s[6], s[7]);
+      }
+    }
+  }
+}
+
 // ---- inspector: the panel plan on the device -------------------------------
 // (ops/spmm.py plan_panels; was a chain of torch sort / unique / bincount
 // launches, ~37 ms for the 65536^2 config.)  Per 64-row panel, one workgroup:
@@ -603,6 +678,24 @@ SPMM_EXPORT int spmm_spmm_rowwise(const int64_t* rp, const int32_t* ci, const vo
   if (m <= 0) return 0;
   if (D % 2 != 0 || ldx % 2 != 0) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((m + 3) / 4));
+  // 16-byte gathers when every X row and Y row piece is 16-byte aligned
+  // (SPMM_SPMM_ROWWISE_V8=0: the 4-byte kernel, for A/B runs)
+  static const int v8 = [] {
+    const char* e = getenv("SPMM_SPMM_ROWWISE_V8");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  const bool al16 = D % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0 &&
+                    ldy % 8 == 0;
+  if (v8 && al16) {
+    if (out_bf16)
+      hipLaunchKernelGGL(spmm_rowwise_v8<true>, grid, dim3(NT), 0, (hipStream_t)stream, rp, ci,
+                         (const unsigned short*)av, (const unsigned short*)X, ldx, m, D, Y, ldy);
+    else
+      hipLaunchKernelGGL(spmm_rowwise_v8<false>, grid, dim3(NT), 0, (hipStream_t)stream, rp, ci,
+                         (const unsigned short*)av, (const unsigned short*)X, ldx, m, D, Y, ldy);
+    SPMM_LAUNCH_CHECK();
+    return 0;
+  }
   if (out_bf16)
     hipLaunchKernelGGL(spmm_rowwise<true>, grid, dim3(NT), 0, (hipStream_t)stream, rp, ci,
                        (const unsigned short*)av, (const unsigned short*)X, ldx, m, D, Y, ldy);

@@ -119,11 +119,12 @@ def test_spmm_mfma_exact_small_integers():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D", [128, 256])
+@pytest.mark.parametrize("D", [128, 256, 72, 130])
 def test_spmm_rowwise_exact_small_integers(D):
-    """Row kernels (XCD-sliced at D = 128, full width otherwise) on exact
-    integer data: rows of 0 .. ~150 entries (several 64-entry rounds), a row
-    count that leaves the last wave partly empty, both output types."""
+    """Row kernels (16-byte gathers when D % 8 == 0, incl. a partial 128-column
+    block at D = 72; 4-byte gathers at D = 130) on exact integer data: rows of
+    0 .. ~150 entries (several 64-entry rounds), a row count that leaves the
+    last wave partly empty, both output types."""
     dev = torch.device("cuda")
     m, n = 301, 2000
     A = gen_csr.uniform_csr(m, n, 0.05, seed=19, values="small_int")
