@@ -57,6 +57,10 @@
 #define SPMM_BM_PREFETCH 0
 #endif
 
+#ifndef SPMM_BM_FUSED_RC   // fused row kernel: column loads in flight per thread in the count phase
+#define SPMM_BM_FUSED_RC 8
+#endif
+
 #ifndef SPMM_BM_NT_STORE   // numeric write-out: non-temporal stores of C (C does not displace B in L2 / MALL;
 #define SPMM_BM_NT_STORE 1   // 1M step 76.55 -> 75.41 ms, 64k 1.755 -> 1.697 ms, same box)
 #endif
@@ -844,6 +848,10 @@ struct BmRowArgs {
   const uint4* ws8;
   int q0, q1;   // windows [q0, q1) of every row (window-major passes: the B column slice of a
                 // pass stays in the MALL while every row's products in it are formed)
+  // fused kernel only (count phase + row look-back, no count kernel):
+  int64_t* uoff_out;           // [m * nwin + 1] unit offsets, written by the kernel (for the reload kernel)
+  unsigned long long* rstat;   // [m] per-row look-back words, zeroed: flag (2 bits) | value (62 bits)
+  uint32_t* ticket;            // zeroed row ticket counter
 };
 
 // First B index of window q0 inside this entry's B row: the row start plus
@@ -857,7 +865,44 @@ __device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb
   return b;
 }
 
-template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET>
+// ---- fused mode: row look-back ----------------------------------------------
+// A fused workgroup counts its row (every window) before forming any product,
+// publishes the row's nnz as an AGGREGATE, and resolves its start in C
+// (sum of all earlier rows) only when its first window is about to be
+// written: by then the earlier rows, which took smaller tickets and hence
+// started earlier, have almost always published at least their aggregate.
+// One wave reads the 64 nearest predecessors' words per memory round trip
+// and sums back to the first INCLUSIVE prefix, then publishes its own.
+constexpr unsigned long long kRsAgg = 1ull << 62, kRsInc = 2ull << 62, kRsVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ int64_t bm_row_lookback(unsigned long long* rstat, int64_t row, int64_t count, int lane) {
+  int64_t pre = 0;
+  for (int64_t end = row; end > 0;) {
+    const int64_t j = end - 1 - lane;   // lane 0 = nearest predecessor
+    const unsigned long long st =
+        j >= 0 ? __hip_atomic_load(&rstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kRsInc;
+    const unsigned f = (unsigned)(st >> 62);
+    const unsigned long long inc = __ballot(f == 2), notready = __ballot(f == 0);
+    const int first = inc ? __ffsll((long long)inc) - 1 : 64;
+    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1);   // lanes 0..first
+    if (notready & need) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    int64_t v = lane <= first ? (int64_t)(st & kRsVal) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    pre += v;
+    if (first < 64) break;
+    end -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&rstat[row], kRsInc | (unsigned long long)(pre + count), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return pre;
+}
+
+template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET, bool FUSED = false>
 __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_bm_rows(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
@@ -875,6 +920,10 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   __shared__ __attribute__((aligned(8))) uint2 dlist[LCAP];
   __shared__ int wsum[2 * NW];
   __shared__ int sdup, sfix, snl;
+  __shared__ int csum[FUSED ? NW : 1];          // fused count phase: per-wave popcounts
+  __shared__ uint32_t s_tk[2];                  // fused: row tickets (double-buffered by row parity)
+  __shared__ int64_t s_rs;                      // fused: resolved start of the row in C
+  __shared__ int s_cnt[8], s_cex[8];            // fused: nnz of each window of the row, exclusive prefix
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -888,6 +937,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   int vz;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   BM_STAMP_DECL
+  if constexpr (FUSED) {
+    if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
+  }
 
   auto clear_bm = [&]() {
     for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
@@ -903,8 +955,15 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
   const int64_t m = p.m;
 
-  // row pipeline registers
-  int64_t row = me;               // current row
+  // row pipeline registers.  Rows: static (me, me + NG, ...) or, fused,
+  // from a ticket counter (the look-back needs every earlier row to be owned
+  // by a running workgroup); row1 / row2 = the next two rows of this workgroup
+  int64_t row = me, row1 = me + NG, row2 = me + 2 * NG;
+  if constexpr (FUSED) {
+    if (tid == 0) s_tk[1] = atomicAdd(ra.ticket, 1u);
+    __syncthreads();
+    row = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)s_tk[1]);   // (uniform: scalar registers)
+  }
   int ca0 = 0, cna = 0;           // its A row (scalars after the copy)
   float cav = 0.f;                // its A value (thread = entry)
   uint4 cwa = make_uint4(0, 0, 0, 0);   // its packed window bounds
@@ -940,7 +999,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
         nwa = ra.ws8[2 * (int64_t)njj];
         nwb = ra.ws8[2 * (int64_t)njj + 1].x;
       }
-      if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
+      if constexpr (!FUSED) {
+        if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
+      }
     }
   };
   auto take_next = [&]() {   // next row -> current row (call only when its loads have landed)
@@ -953,11 +1014,11 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
     n1a = n2a;
     n1b = n2b;
   };
-  // prologue: row me in the current registers, Arp of row me + NG loaded
+  // prologue: row in the current registers, Arp of row1 loaded
   ld_arp(row, n1a, n1b);
   ld_entries(row, n1a, n1b);
   ld_bounds(row, n1a, n1b);
-  ld_arp(row + NG, n2a, n2b);
+  if constexpr (!FUSED) ld_arp(row1, n2a, n2b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   take_next();
   __syncthreads();
@@ -965,9 +1026,122 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   int c[RR];
   float v[RR];
   uint32_t pf0 = 0, pf1 = 0;   // prefetch sinks (SPMM_BM_PREFETCH)
-  for (; row < m; row += NG) {
+  int par = 0;                 // fused: ticket buffer of this row
+  while (row < m) {
     const int na = cna;
     const int q0 = ra.q0, q1 = ra.q1;
+    if constexpr (!FUSED) {
+      row1 = row + NG;
+      row2 = row + 2 * NG;
+    }
+    // ---- fused: count phase (every window's exact nnz, B columns only) ----
+    // (ccnt: lane q = nnz of window q, cex its exclusive prefix: into s_cnt / s_cex; rtot the row's nnz)
+    int64_t rtot = 0, rowstart = 0;
+    bool resolved = false;
+    if constexpr (FUSED) {
+      constexpr int RC = SPMM_BM_FUSED_RC;   // count-phase B loads in flight per thread
+      if (na > NT && tid == 0) atomicOr(p.err, 1);         // (host gate: A rows <= NT) -> host fallback
+      int ccnt = 0;
+      uint32_t cbq = bm_window_start(cwa, cwb, 0);
+      for (int q = 0; q < nwin; ++q) {
+        const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
+        int len = 0, nch = 0;
+        if (tid < na && tid < NT) {
+          len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
+          nch = (len + Gl - 1) >> lg;
+        }
+        const uint32_t b0 = cbq;
+        cbq += (uint32_t)len;
+        int pre, plen, TC, P;
+        bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+        if (P == 0) {   // uniform: nothing to OR
+          __syncthreads();   // wsum reads done before the next scan
+          continue;
+        }
+        const int clo = q << LGW;
+        for (int cb = 0; cb < TC; cb += CCAP) {
+          const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
+          const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
+          for (int kk = k0; kk < k1; ++kk) {
+            const int rem = len - (kk << lg);
+            desc[pre + kk - cb] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
+          }
+          __syncthreads();
+          const int nr = (TCb + ngrp - 1) / ngrp;
+          for (int i0 = 0; i0 < nr; i0 += RC) {
+            uint2 ds[RC];
+#pragma unroll
+            for (int d = 0; d < RC; ++d) {
+              const int t = gid + (i0 + d) * ngrp;
+              ds[d] = desc[t < TCb ? t : TCb - 1];
+            }
+            int x[RC];
+            uint32_t okm = 0;
+#pragma unroll
+            for (int d = 0; d < RC; ++d) {
+              const int t = gid + (i0 + d) * ngrp;
+              const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
+              okm |= (ok ? 1u : 0u) << d;
+              const uint32_t f = ds[d].x + (ok ? (uint32_t)gl : 0u);
+              x[d] = 0;
+              if (i0 + d < nr) {   // wave-uniform
+                // (from the interleaved pairs when the numeric phase reads them:
+                // the same lines, which are then warm for pass 1)
+                if constexpr (CV) x[d] = (int)p.Bcv[f].x;
+                else x[d] = p.Bci[f];
+              }
+            }
+#pragma unroll
+            for (int d = 0; d < RC; ++d) {
+              if ((okm >> d) & 1u) {
+                const int cc = x[d] - clo;
+                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+              }
+            }
+          }
+          __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
+        }
+        // popcount of this wave's bitmap words, cleared as they are read
+        int cnt = 0;
+#pragma unroll
+        for (int kk = 0; kk < WPT; ++kk) {
+          const int wd = w * WPW + kk * 64 + lane;
+          cnt += __popcll(bm[wd]);
+          bm[wd] = 0ull;
+        }
+        cnt = bm_wave_sum(cnt);
+        if (lane == 0) csum[w] = cnt;
+        __syncthreads();
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) t += csum[i];
+        if (lane == q) ccnt = t;
+      }
+      const int incl = bm_wave_incl(ccnt);
+      if (w == 0 && lane < 8) {   // (read below at least one barrier)
+        s_cnt[lane] = ccnt;
+        s_cex[lane] = incl - ccnt;
+      }
+      rtot = (int64_t)(uint32_t)__builtin_amdgcn_readlane(incl, 63);
+      if (tid == 0)
+        __hip_atomic_store(&ra.rstat[row], kRsAgg | (unsigned long long)rtot, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      BM_STAMP(5);   // (fused: the count phase, stamp slot of the count kernel's ORs)
+    }
+    // fused: the row's start in C, by wave 0 before a barrier (issue) and read
+    // by every thread after it (finish); also the unit offsets for the reload kernel
+    auto resolve_issue = [&]() {
+      if (w == 0) {
+        const int64_t s0 = bm_row_lookback(ra.rstat, row, rtot, lane);
+        if (lane == 0) s_rs = s0;
+      }
+    };
+    auto resolve_finish = [&]() {
+      rowstart = bm_rfl64(s_rs);
+      resolved = true;
+      if (w == 0 && lane < nwin) ra.uoff_out[row * nwin + lane] = rowstart + (int64_t)(uint32_t)s_cex[lane];
+      if (w == 0 && lane == 0 && row == m - 1) ra.uoff_out[m * nwin] = rowstart + rtot;
+    };
     uint32_t bq = bm_window_start(cwa, cwb, q0);   // first B index of window q of this thread's entry
     for (int q = q0; q < q1; ++q) {
       const bool last = q == q1 - 1;
@@ -975,11 +1149,19 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       asm volatile("" ::"v"(pf0), "v"(pf1));   // the previous unit's prefetches: a use, so their registers stay reserved
 #endif
       // ---- pipeline hooks (every path) ---------------------------------
-      if (q == q0) {
-        ld_entries(row + NG, n1a, n1b);
-        ld_arp(row + 2 * NG, n2a, n2b);
+      if constexpr (FUSED) {
+        // the next row's ticket only now (a ticket taken early but started
+        // late would hold up the look-back of every later row); its A row is
+        // staged during this window: Arp after the scan, entries after pass 1,
+        // bounds before the write-out, into the current registers at the row end
+        if (last && tid == 0) s_tk[par] = atomicAdd(ra.ticket, 1u);
+      } else {
+        if (q == q0) {
+          ld_entries(row1, n1a, n1b);
+          ld_arp(row2, n2a, n2b);
+        }
+        if (last) ld_bounds(row1, n1a, n1b);
       }
-      if (last) ld_bounds(row + NG, n1a, n1b);
       // ---- staging from registers ---------------------------------------
       const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
       int len = 0, nch = 0;
@@ -1009,13 +1191,23 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
 #endif
       const int clo = q << LGW;
       const int u = (int)(row * nwin + q);
-      // (both halves zero-extended: offsets pass 2^31 on the 1M product)
-      const int64_t off =
-          (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)cuo >> 32), q) << 32) |
-                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cuo, q));
-      const int want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
+      int64_t off = 0;
+      int want = 0;
+      if constexpr (!FUSED) {   // (fused: both at the write-out, once the row's start is resolved)
+        // (both halves zero-extended: offsets pass 2^31 on the 1M product)
+        off = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)cuo >> 32), q)
+                         << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cuo, q));
+        want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
+      }
       int pre, plen, TC, P;
       bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+      if constexpr (FUSED) {
+        if (last) {
+          row1 = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)s_tk[par]);
+          ld_arp(row1, n1a, n1b);
+        }
+      }
       const bool too_big = na > NT || P > PCAP || TC > CCAP || TC > R * ngrp;
       if (P == 0 || too_big) {   // uniform
         if (too_big && P != 0 && tid == 0) {
@@ -1023,7 +1215,14 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
           if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
           else atomicOr(p.err, 4);
         }
-        if (last) take_next();   // (rare: waits for the next row's loads here)
+        if constexpr (FUSED) {
+          if (last) {   // (rare: the next row's chain back to back)
+            ld_entries(row1, n1a, n1b);
+            ld_bounds(row1, n1a, n1b);
+          }
+        } else if (last) {
+          take_next();   // (rare: waits for the next row's loads here)
+        }
         __syncthreads();         // wsum reads done before the next scan
         continue;
       }
@@ -1164,9 +1363,25 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
 #endif
       // this unit's B loads have landed, and with them every older load:
       // the next row's registers are ready to be taken
-      if (last) take_next();
+      if constexpr (FUSED) {
+        if (last) ld_entries(row1, n1a, n1b);
+      } else if (last) {
+        take_next();
+      }
       if (dupm) sdup = 1;
+      if constexpr (FUSED) {
+        if (!resolved) {   // uniform
+          BM_STAMP(1);
+          resolve_issue();
+        }
+      }
       __syncthreads();
+      if constexpr (FUSED) {
+        if (!resolved) {
+          resolve_finish();
+          BM_STAMP(6);   // (fused: the look-back, stamp slot of the count kernel's popcount)
+        }
+      }
       BM_STAMP(1);
       // ---- rank prefix per 64-bit word ---------------------------------
       // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
@@ -1314,6 +1529,11 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       }
       BM_STAMP(3);
       // ---- write-out -----------------------------------------------------
+      if constexpr (FUSED) {
+        if (last) ld_bounds(row1, n1a, n1b);
+        want = __builtin_amdgcn_readfirstlane(s_cnt[q]);
+        off = rowstart + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_cex[q]);
+      }
       int lim = skip ? 0 : total;
       if (!skip && (want != total || off < 0 || off + total > p.cap)) {   // never write outside the unit or C
         if (tid == 0) atomicOr(p.err, 2);
@@ -1328,6 +1548,18 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       __syncthreads();
       BM_STAMP(4);
       BM_STAMP_UNIT();
+    }
+    if constexpr (FUSED) {
+      if (!resolved) {   // uniform: no window of the row reached pass 1 (empty or deferred windows)
+        resolve_issue();
+        __syncthreads();
+        resolve_finish();
+      }
+      take_next();   // (the next row's bounds: loaded during the last write-out)
+      row = row1;
+      par ^= 1;
+    } else {
+      row += NG;
     }
   }
   BM_STAMP_FLUSH();
@@ -2031,7 +2263,10 @@ struct BmRowKernel {
   static constexpr auto kcv = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false>;
   static constexpr auto k_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, true>;
   static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, true>;
+  static constexpr auto k_fused = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, false, true>;
+  static constexpr auto kcv_fused = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false, true>;
 };
+
 
 template <typename Kern>
 int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastNT) {
@@ -2044,6 +2279,16 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastN
   hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(nt), 0, s, ra);
   SPMM_LAUNCH_CHECK();
   return 0;
+}
+
+// fused row kernel (count phase + row look-back) over every row, then the
+// reload kernel over the deferred units (which reads the offsets it wrote)
+template <int C>
+int bm_fused_rows(BmRowArgs ra, hipStream_t s) {
+  using K = BmRowKernel<C>;
+  const int rc = ra.a.Bcv ? launch_rows(K::kcv_fused, ra, s, K::NT) : launch_rows(K::k_fused, ra, s, K::NT);
+  if (rc) return rc;
+  return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
 }
 
 // count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
@@ -2235,6 +2480,38 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
     case 0: return bm_numeric_rows<0>(ra, pipe, passes, det, s);
     case 1: return bm_numeric_rows<1>(ra, pipe, passes, det, s);
     default: return bm_numeric_rows<2>(ra, pipe, passes, det, s);
+  }
+}
+
+// Fused row-major SpGEMM (nwin <= 8, every A row <= 256 entries, ws8 packed):
+// no count kernel and no host read-back between count and numeric.  Each
+// workgroup counts its row (all windows), publishes the count, resolves the
+// row's start in C by a decoupled look-back over the rows (tickets give the
+// order) and writes its windows there.  C must hold cap >= nnz(C) entries
+// (the product count is a bound).  uoff[m * nwin + 1] is OUTPUT (unit
+// offsets; uoff[m * nwin] = nnz(C)); ws_rows: device scratch of m + 1 u64
+// (zeroed here: row look-back words + the ticket counter).  err as in
+// spmm_spgemm_bm_numeric; bit 3 set on entry (ws8 truncated) makes the kernel
+// return at once and the host takes the per-unit kernels.
+SPMM_EXPORT int spmm_spgemm_bm_fused_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                                          const void* ws8, const uint32_t* ws, const int32_t* Bci, const float* Bv,
+                                          const void* Bcv, int64_t m, int nwin, int lg, int64_t* uoff, int64_t cap,
+                                          int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
+                                          int32_t* err, void* ws_rows, void* stream) {
+  if (m <= 0) return 0;
+  if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
+  if (m >= (int64_t)UINT32_MAX / 2 || m * nwin >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* rstat = (unsigned long long*)ws_rows;
+  hipError_t e = hipMemsetAsync(rstat, 0, (size_t)(m + 1) * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return (int)e;
+  BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
+                      (const uint2*)Bcv, err},
+               (const uint4*)ws8, 0, nwin, uoff, rstat, (uint32_t*)(rstat + m)};
+  switch (cfg) {
+    case 0: return bm_fused_rows<0>(ra, s);
+    case 1: return bm_fused_rows<1>(ra, s);
+    default: return bm_fused_rows<2>(ra, s);
   }
 }
 

@@ -22,6 +22,8 @@ product), the convention of BASELINE.md.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -64,6 +66,8 @@ _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp,
                      c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, c_vp)
+_native.register_hip("spmm_spgemm_bm_fused_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
+                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp,
@@ -756,6 +760,11 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         ws8 = torch.empty(B.m * 8, dtype=torch.int32, device=dev)
         _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err), st), "spgemm_bm_pack_ws8")
     count_rows = ws8 is not None and pre is not None and pre.get("amax", 1 << 30) <= 256
+    if count_rows and not det and _fused_ok(cfg, rows_mode, tot, m, dev):
+        C_ = _bitmap_fused(A, B, info, B_ready, cfg, nwin, lg_num, ws8, ws, err, novf, z)
+        if C_ is not None:
+            return C_ if C_ is not _FALLBACK else None
+        ws8, count_rows = None, False   # err bit 3 (ws8 lengths truncated): the per-unit kernels below
 
     def count(use_rows: bool):
         if use_rows:
@@ -819,6 +828,64 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     info.deterministic = bool(det)
     rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
     return CSR(m, B.n, rowptr, Cci, Cv)
+
+
+_FALLBACK = object()   # _bitmap_fused: the product needs the binned path
+
+
+def _fused_ok(cfg: int, rows_mode: str, total_products: int, m: int, dev: torch.device) -> bool:
+    """Fused row kernel (count phase + row look-back in the numeric kernel):
+    C is allocated at the product count (a bound on nnz), so it must fit."""
+    mode = CONFIG.spgemm_bitmap_fused
+    if mode == "off" or rows_mode in ("pipe", "off"):
+        return False
+    if int(os.environ.get("SPMM_BM_NUM_PASS_WINDOWS", "0") or 0) > 0:   # window-major passes: the two-kernel path
+        return False
+    if mode == "auto" and not (cfg == 0 or rows_mode in ("on", "nopipe")):
+        return False
+    return _FreeMem(dev).fits(total_products * 8 + m * 16)
+
+
+def _bitmap_fused(A: CSR, B: CSR, info: SpgemmInfo, B_ready, cfg: int, nwin: int, lg: int, ws8, ws, err, novf, z):
+    """One kernel instead of count + scan + numeric (csr_spgemm_bitmap.hip
+    ``spmm_spgemm_bm_fused_rows``): every row is counted by the workgroup that
+    then forms it, rows find their start in C by a decoupled look-back, and the
+    one read-back (nnz, error bits) comes after the product.  Returns the CSR,
+    ``_FALLBACK`` (binned path), or None when the ws8 window lengths were
+    truncated (the caller's per-unit kernels then run)."""
+    dev = A.device
+    m = A.m
+    if B_ready is not None:   # the fused kernel reads the values from the start
+        B = B_ready()
+    lib = _native.hip()
+    P = _native.ptr
+    cap = max(info.flops // 2, 1)
+    nunits = m * nwin
+    Cci = torch.empty(cap, dtype=torch.int32, device=dev)
+    Cv = torch.empty(cap, dtype=torch.float32, device=dev)
+    uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
+    wsr = torch.empty(m + 1, dtype=torch.int64, device=dev)
+    ovf_cap = min(nunits, 1 << 20)
+    ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
+    Bcv = interleaved(B) if CONFIG.spgemm_bitmap_cv else None
+    _native.check(lib.spmm_spgemm_bm_fused_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
+                                                P(B.val), P(Bcv) if Bcv is not None else None, m, nwin, lg,
+                                                P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap, P(err), P(wsr),
+                                                _native.stream_ptr(dev)), "spgemm_bm_fused_rows")
+    nnz, e, deferred = torch.stack([uoff[-1], z[0].long(), z[1].long()]).tolist()   # one read-back
+    if e & 8:
+        return None
+    info.rows_per_bin_num.update(bitmap_units=nunits, bitmap_cfg=cfg, bitmap_deferred=deferred, bitmap_rows=1,
+                                 bitmap_fused=1)
+    if e & 2:
+        raise RuntimeError("spgemm bitmap (fused): numeric and count phases disagree (kernel invariant violated)")
+    if e & 5:
+        info.rows_per_bin_num["bitmap_fallback"] = 1
+        return _FALLBACK
+    info.nnz = nnz
+    info.deterministic = False
+    rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
+    return CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz])
 
 
 def _det_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:

@@ -49,6 +49,10 @@ class Config:
     spgemm_bitmap_rows: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_ROWS", "auto", str))
     # row-major numeric kernel reads an interleaved (column, value) copy of B (1) or the two arrays (0)
     spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
+    # fused row kernel on the bitmap path (count phase + row look-back inside the numeric kernel, no
+    # count kernel, C allocated at the product-count bound): "auto" = where the row kernel is the
+    # default (widest windows), "on" = whenever the row kernels run, "off"
+    spgemm_bitmap_fused: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_FUSED", "off", str))
     # windows per row-major count unit (1: 16 KB bitmaps, 8 per CU; 2: 32 KB, 4 per CU)
     spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
     # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU

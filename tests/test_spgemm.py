@@ -618,6 +618,45 @@ def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["uniform", "empty_rows", "deferred", "tiny", "off"])
+def test_spgemm_gpu_bitmap_fused(monkeypatch, case):
+    """Fused row kernel (each workgroup counts its row, then a decoupled
+    look-back over rows gives its start in C; C allocated at the product
+    bound, no count kernel) equals the binned path: 20000 rows (look-back
+    over many 64-row rounds), runs of empty rows (rows that never reach pass
+    1), units deferred to the reload kernel (which reads the offsets the fused
+    kernel wrote), a 5-row product, and the knob off (two-kernel path)."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    k, n = 20000, 600000
+    if case == "deferred":
+        k, n = 6000, 300000
+        base = gen_csr.uniform_csr(1500, k, 0.01, seed=93)
+        big = torch.arange(0, 1500, 97)   # rows of 250 entries: ~6.5k products per window > 2048 (fast capacity)
+        r0, c0 = base.row_ids(), base.col.long()
+        keep = torch.isin(r0, big, invert=True)
+        rows = torch.cat([r0[keep], big.repeat_interleave(250)])
+        cols = torch.cat([c0[keep], torch.cat([torch.randperm(k)[:250] for _ in range(big.numel())])])
+        A = CS.from_coo(rows, cols, torch.rand(rows.numel()) - 0.5, 1500, k).to(dev)
+        B = gen_csr.uniform_csr(k, n, 2e-4, seed=94, device=dev)
+    elif case == "empty_rows":
+        base = gen_csr.uniform_csr(6000, k, 0.002, seed=97)
+        r0 = base.row_ids()
+        keep = ((r0 // 300) % 3 != 1) & (r0 != 0) & (r0 != 5999)   # blocks of 300 empty rows, first/last empty
+        A = CS.from_coo(r0[keep], base.col.long()[keep], base.val[keep], 6000, k).to(dev)
+        B = gen_csr.uniform_csr(k, n, 1.4e-4, seed=98, device=dev)
+    else:
+        A = gen_csr.uniform_csr(5 if case == "tiny" else 20000, k, 0.002, seed=97, device=dev)
+        B = gen_csr.uniform_csr(k, n, 1.4e-4, seed=98, device=dev)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_fused", "off" if case == "off" else "on")
+    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    assert info.rows_per_bin_num.get("bitmap_fused", 0) == (0 if case == "off" else 1)
+    if case == "deferred":
+        assert info.rows_per_bin_num["bitmap_deferred"] >= 16
+
+
+@pytest.mark.gpu
 def test_spgemm_gpu_bitmap_deferred_units_and_fallback(monkeypatch):
     """Rows too long for the fast kernel (A rows > 256 entries, windows above
     its product capacity) are deferred to the reload kernel; a unit beyond the

@@ -43,6 +43,8 @@ lib.spmm_spgemm_bm_stamps(0, None)
 st = list(out)
 units = max(st[7], 1)
 names = ["num staging", "num pass1", "num scan", "num pass2", "num writeout", "count stage+OR", "count pop+clear"]
+if info.rows_per_bin_num.get("bitmap_fused"):
+    names[5:7] = ["fused count phase", "fused look-back"]
 tot = sum(st[:5])
 print(f"n={n} d={d} plain step {plain * 1e3:.2f} ms  info={info.rows_per_bin_num}")
 for i, nm in enumerate(names):
