@@ -61,6 +61,10 @@
 #define SPMM_BM_FUSED_RC 8
 #endif
 
+#ifndef SPMM_BM_DESC4   // row-major numeric: 16-byte chunk descriptors {B index, lanes, a(i, j), -}, padded to
+#define SPMM_BM_DESC4 0   // whole rounds (one LDS read per round, no TC clamps) instead of uint2 + float arrays
+#endif
+
 #ifndef SPMM_BM_NT_STORE   // numeric write-out: non-temporal stores of C (C does not displace B in L2 / MALL;
 #define SPMM_BM_NT_STORE 1   // 1M step 76.55 -> 75.41 ms, 64k 1.755 -> 1.697 ms, same box)
 #endif
@@ -908,15 +912,21 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   constexpr int NW = NT / 64;
   constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int RR = R;
-  constexpr int LCAP = DET ? 256 : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
+  constexpr int LCAP = DET ? (SPMM_BM_DESC4 ? 184 : 256) : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
   static_assert(WPW % 64 == 0 && PCAP < 65536, "geometry");
   static_assert(!DET || (CCAP << 6) <= (1 << kKeyBits), "DET keys fit 17 bits");
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
   __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
+#if SPMM_BM_DESC4
+  static_assert(!SPMM_BM_P1_SPLIT, "DESC4 with the split pass 1 is not implemented");
+  __shared__ __attribute__((aligned(16))) uint4 desc4[CCAP];   // chunk: {first B index, valid lanes, a(i, j) bits, 0}
+  uint4* const desc = desc4;                                   // (fused count phase: .x, .y only)
+#else
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];   // chunk: {first B index, valid lanes}
   __shared__ float dval[CCAP];                                 //        a(i, j)
+#endif
   __shared__ __attribute__((aligned(8))) uint2 dlist[LCAP];
   __shared__ int wsum[2 * NW];
   __shared__ int sdup, sfix, snl;
@@ -1064,7 +1074,8 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
           const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
           for (int kk = k0; kk < k1; ++kk) {
             const int rem = len - (kk << lg);
-            desc[pre + kk - cb] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
+            desc[pre + kk - cb].x = b0 + ((uint32_t)kk << lg);
+            desc[pre + kk - cb].y = (uint32_t)(rem < Gl ? rem : Gl);
           }
           __syncthreads();
           const int nr = (TCb + ngrp - 1) / ngrp;
@@ -1073,7 +1084,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
 #pragma unroll
             for (int d = 0; d < RC; ++d) {
               const int t = gid + (i0 + d) * ngrp;
-              ds[d] = desc[t < TCb ? t : TCb - 1];
+              ds[d] = make_uint2(desc[t < TCb ? t : TCb - 1].x, desc[t < TCb ? t : TCb - 1].y);
             }
             int x[RC];
             uint32_t okm = 0;
@@ -1226,11 +1237,22 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
         __syncthreads();         // wsum reads done before the next scan
         continue;
       }
+#if SPMM_BM_DESC4
+      for (int kk = 0; kk < nch; ++kk) {
+        const int rem = len - (kk << lg);
+        desc4[pre + kk] = make_uint4(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl), __float_as_uint(cav), 0u);
+      }
+      {   // the last round's chunks past TC: no valid lane
+        const int pad_end = ((TC + ngrp - 1) / ngrp) * ngrp;
+        if (TC + tid < pad_end) desc4[TC + tid] = make_uint4(0u, 0u, 0u, 0u);
+      }
+#else
       for (int kk = 0; kk < nch; ++kk) {
         const int rem = len - (kk << lg);
         desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
         dval[pre + kk] = cav;
       }
+#endif
       __syncthreads();
       BM_STAMP(0);
       // ---- pass 1 ----------------------------------------------------------
@@ -1303,6 +1325,42 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       const uint32_t dupm = nr <= RR / 2 ? pass1(std::integral_constant<int, RR / 2>{})
                             : nr <= RR - 2 ? pass1(std::integral_constant<int, RR - 2>{})
                                            : pass1(std::integral_constant<int, RR>{});
+#elif SPMM_BM_DESC4
+      {
+        uint4 ds[RR];
+#pragma unroll
+        for (int d = 0; d < RR; ++d) ds[d] = desc4[gid + d * ngrp];   // (rounds >= nr: stale, masked below)
+        uint32_t f[RR];
+        uint32_t okm = 0;
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          const bool ok = (d < nr) & ((uint32_t)gl < ds[d].y);
+          okm |= (ok ? 1u : 0u) << d;
+          f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
+        }
+        int x[RR];
+        float b[RR];
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          x[d] = 0;
+          b[d] = 0.f;
+          if (d < nr) {   // wave-uniform
+            if constexpr (CV) {
+              const uint2 e = p.Bcv[f[d]];
+              x[d] = (int)e.x;
+              b[d] = __uint_as_float(e.y);
+            } else {
+              x[d] = p.Bci[f[d]];
+              b[d] = p.Bv[f[d]];
+            }
+          }
+        }
+#pragma unroll
+        for (int d = 0; d < RR; ++d) {
+          c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
+          v[d] = __uint_as_float(ds[d].z) * b[d];
+        }
+      }
 #else
       {
         uint2 ds[RR];
@@ -1349,6 +1407,8 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
           v[d] *= b[d];
         }
       }
+#endif
+#if !SPMM_BM_P1_SPLIT
       uint32_t dupm = 0;
       {
         uint32_t old[RR];
