@@ -65,6 +65,10 @@
 #define SPMM_BM_DESC4 0   // whole rounds (one LDS read per round, no TC clamps) instead of uint2 + float arrays
 #endif
 
+#ifndef SPMM_BM_COUNT_LGV   // row-major count: log2 columns per lane and load (1: one 8-byte load covers two
+#define SPMM_BM_COUNT_LGV 0   // consecutive products of a chunk: half the load instructions / memory requests)
+#endif
+
 #ifndef SPMM_BM_NT_STORE   // numeric write-out: non-temporal stores of C (C does not displace B in L2 / MALL;
 #define SPMM_BM_NT_STORE 1   // 1M step 76.55 -> 75.41 ms, 64k 1.755 -> 1.697 ms, same box)
 #endif
@@ -1983,6 +1987,8 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
   constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int WORDS_PER_WIN = NWORD / NSUB;
   static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
+  constexpr int LGV = SPMM_BM_COUNT_LGV;
+  static_assert(LGV == 0 || LGV == 1, "one or two columns per lane and load");
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
@@ -2074,7 +2080,7 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
           static_assert(NSUB == 2, "count units of one or two windows");
           len = (int)(wl & 0xffffu) + (q + 1 < nwin ? (int)(wl >> 16) : 0);
         }
-        nch = (len + Gl - 1) >> lg;
+        nch = (len + (Gl << LGV) - 1) >> (lg + LGV);
       }
       const uint32_t b0 = bq;
       bq += (uint32_t)len;
@@ -2098,8 +2104,9 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
         const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
         const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
         for (int kk = k0; kk < k1; ++kk) {
-          const int rem = len - (kk << lg);
-          desc[pre + kk - cb] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
+          const int rem = len - (kk << (lg + LGV));
+          desc[pre + kk - cb] =
+              make_uint2(b0 + ((uint32_t)kk << (lg + LGV)), (uint32_t)(rem < (Gl << LGV) ? rem : (Gl << LGV)));
         }
         __syncthreads();
         const int nr = (TCb + ngrp - 1) / ngrp;
@@ -2110,6 +2117,38 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
             const int t = gid + (i0 + d) * ngrp;
             ds[d] = desc[t < TCb ? t : TCb - 1];
           }
+#if SPMM_BM_COUNT_LGV == 1
+          // two consecutive products per lane, one 8-byte load (4-byte aligned);
+          // the last element of B is never the first of a pair load
+          typedef int i2a4 __attribute__((ext_vector_type(2), aligned(4)));
+          i2a4 x2[RR];
+          uint32_t okm = 0, ok2m = 0, hi1m = 0;
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            const int t = gid + (i0 + d) * ngrp;
+            const int nv = (int)ds[d].y - 2 * gl;
+            const bool ok = (t < TCb) & (nv > 0);
+            okm |= (ok ? 1u : 0u) << d;
+            ok2m |= (ok & (nv > 1) ? 1u : 0u) << d;
+            uint32_t f = ds[d].x + (ok ? 2u * (uint32_t)gl : 0u);
+            const bool atend = (int64_t)f + 1 >= p.cap;   // (a single product at B's last element)
+            hi1m |= (atend ? 1u : 0u) << d;
+            f -= atend ? 1u : 0u;
+            x2[d] = i2a4{0, 0};
+            if (i0 + d < nr) x2[d] = *reinterpret_cast<const i2a4*>(p.Bci + f);   // wave-uniform guard
+          }
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            if ((okm >> d) & 1u) {
+              const int cc = (((hi1m >> d) & 1u) ? x2[d].y : x2[d].x) - clo;
+              atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+            }
+            if ((ok2m >> d) & 1u) {
+              const int cc = x2[d].y - clo;
+              atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+            }
+          }
+#else
           int x[RR];
           uint32_t okm = 0;
 #pragma unroll
@@ -2127,6 +2166,7 @@ __global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   
               atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
             }
           }
+#endif
         }
         __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
       }
@@ -2580,11 +2620,11 @@ SPMM_EXPORT int spmm_spgemm_bm_fused_rows(int cfg, const int64_t* Arp, const int
 // is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
 SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
                                           const int32_t* Bci, int64_t m, int nwin, int lg, int nsub, int32_t* ucnt,
-                                          int32_t* err, void* stream) {
+                                          int32_t* err, int64_t nnzb, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   BmRowArgs ra{BmArgs{Arp, Aci, nullptr, nullptr, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr,
-                      nullptr, 0, 0, nullptr, err},
+                      nullptr, 0, nnzb, nullptr, err},   // (cap = nnz(B): the pair loads stay inside B)
                (const uint4*)ws8, 0, nwin};
   hipStream_t s = (hipStream_t)stream;
   const int passes = bm_env_int("SPMM_BM_COUNT_PASS_WINDOWS", 0);

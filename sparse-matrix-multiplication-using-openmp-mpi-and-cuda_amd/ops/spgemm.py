@@ -63,7 +63,7 @@ _native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_v
 _native.register_hip("spmm_spgemm_bm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, C_INT, c_vp, c_vp,
-                     c_vp)
+                     C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_fused_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
@@ -772,7 +772,8 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
             sl = seg * nsub_c / nwin   # B-segment length per count unit
             lg_c = 4 if sl < 48 else (5 if sl < 96 else 6)
             _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8), P(B.col), m, nwin,
-                                                        lg_c, nsub_c, P(ucnt), P(err), st), "spgemm_bm_count_rows")
+                                                        lg_c, nsub_c, P(ucnt), P(err), B.col.numel(), st),
+                          "spgemm_bm_count_rows")
         else:
             _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, lg_count,
                                                    P(ucnt), P(err), st), "spgemm_bm_count")
