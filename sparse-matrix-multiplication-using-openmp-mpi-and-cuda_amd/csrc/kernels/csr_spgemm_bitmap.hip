@@ -2301,13 +2301,16 @@ __global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __rest
 //          count 8 windows per unit (128 KB bitmap, 1024 threads)
 //          fast  <= 2048 products, 12 register rounds
 //   cfg 1: W = 2^15 (65536 columns at ~65 nnz per row: ~2.1k per window)
-//          count 2 windows (8 KB, 512 threads); fast <= 3840 products, 16 rounds
+//          count 2 windows (8 KB, 512 threads); fast <= 3840 products, SPMM_BM_CFG1_R (14) rounds
 //   cfg 2: W = 2^16: count 4 windows (32 KB, 1024 threads); fast <= 3072, 16 rounds
 // Reload (deferred units): min(1024, W / 64) threads, <= 12288 products, 2048 chunks.
 struct BmCfg {
   int lgw, nsub_count, pcap_fast, rounds_fast;
 };
-constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12}, {15, 2, 3840, 16}, {16, 4, 3072, 16}};
+#ifndef SPMM_BM_CFG1_R   // register rounds of cfg 1's per-unit fast kernel (the 65536^2 config)
+#define SPMM_BM_CFG1_R 14   // 65536^2: 16 rounds spill 5 VGPRs; 14 = 1.64 -> 1.56 ms (384 of 131072 units deferred), 13: 1.61-1.67, 12: 1.82
+#endif
+constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12}, {15, 2, 3840, SPMM_BM_CFG1_R}, {16, 4, 3072, 16}};
 constexpr int kNumCfgs = 3;
 constexpr int kFastNT = 256, kReloadPcap = 12288, kReloadCcap = 2048;
 #ifndef SPMM_BM_ROWS_NT   // threads of the row-major numeric kernel's workgroups (256 or 512; 4 workgroups per CU)
