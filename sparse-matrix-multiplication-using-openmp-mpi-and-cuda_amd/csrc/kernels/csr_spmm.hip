@@ -349,7 +349,10 @@ __global__ __launch_bounds__(NT) void spmm_rowwise(const int64_t* __restrict__ r
 // (4 x 256 B instead of one), RW8_DEPTH loads in flight per lane cover
 // 4 * RW8_DEPTH entries, so a 65-entry row needs ~2 memory latencies instead
 // of ~5; the four groups' partial sums meet in two cross-lane adds.
-constexpr int RW8_DEPTH = 8;
+#ifndef SPMM_RW8_DEPTH   // 16-byte gathers in flight per lane (4 X rows each per load instruction)
+#define SPMM_RW8_DEPTH 8
+#endif
+constexpr int RW8_DEPTH = SPMM_RW8_DEPTH;
 
 template <bool OUT_BF16>
 __global__ __launch_bounds__(NT) void spmm_rowwise_v8(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
@@ -412,6 +415,170 @@ __global__ __launch_bounds__(NT) void spmm_rowwise_v8(const int64_t* __restrict_
         float4* Y = reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + row * ldy + col);
         Y[0] = make_float4(s[0], s[1], s[2], s[3]);
         Y[1] = make_float4(s[4], s[5], s[6], s[7]);
+      }
+    }
+  }
+}
+
+// ---- row-owning sweep: resident waves, grouped 16-byte gathers -------------
+// The row kernels launch one wave per row: a wave gathers its row's ~65 X
+// rows in two or three dependent rounds and exits, with every wave at its own
+// column position, so the X rows an XCD touches span all of X (16.8 MB at
+// 65536 x 128 bf16) against a 4 MB L2 (~55 % of gathers miss:
+// profiles/r3/spmm_pmc.md, 434 MB fetched per call).  Here the grid is
+// resident and every wave owns up to SW_RPW rows (gw, gw + G, ...): it stages
+// their entries in LDS once (column-sorted, with each row's offsets at SW_S
+// column-slice boundaries), then walks the slices in order, slice s of every
+// owned row before slice s + 1, so all waves sweep A's columns together.  A
+// 16-lane group owns 4 of the wave's rows (a lane: 8 output columns of each,
+// 32 accumulator VGPRs for the whole sweep); every load instruction gathers
+// four X rows (one per group, 16 B per lane) and SW_U entries of each of a
+// group's rows are in flight per round (16 loads).  Measured (65536^2 @ 0.1 %
+// x 128): 0.106 ms per call vs 0.123 ms for the one-row-per-wave kernel; the
+// fabric traffic drops ~3.6x with 16 slices but more slices mean more rounds,
+// and 1 slice is within 2 % of the best (2): the win is the many independent
+// gathers per wave more than the L2 reuse.  The host plans the rows so that
+// no wave holds more than SW_CAP entries; a wave that would sets err (its Y
+// rows are then zeros and the host reruns the product on the row kernel).
+// D = 128 (one column block).
+#ifndef SPMM_SW_U   // spmm_sweep: entries of each owned row in flight per round
+#define SPMM_SW_U 4
+#endif
+#ifndef SPMM_SW_S   // spmm_sweep: column slices
+#define SPMM_SW_S 2   // 65536^2 x 128: 1 / 2 / 4 / 8 slices = 0.108 / 0.106 / 0.110 / 0.118 ms per call
+#endif
+constexpr int SW_RPW = 16, SW_S = SPMM_SW_S, SW_CAP = 1280, SW_U = SPMM_SW_U;
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(NT, 4) void spmm_sweep(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                    const unsigned short* __restrict__ av,
+                                                    const unsigned short* __restrict__ X, int64_t ldx, int64_t m,
+                                                    int lgs, void* __restrict__ Yv, int64_t ldy,
+                                                    int32_t* __restrict__ err) {
+  constexpr int NWV = NT / 64;
+  __shared__ uint32_t ent_all[NWV][SW_CAP];                  // (column - slice base) | bf16 value << 16
+  __shared__ uint16_t bnd_all[NWV][SW_RPW][SW_S + 1];        // entry offsets at the slice boundaries
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t G = (int64_t)gridDim.x * NWV;
+  const int64_t gw = (int64_t)blockIdx.x * NWV + w;
+  uint32_t* const E = ent_all[w];
+  uint16_t(*const bnd)[SW_S + 1] = bnd_all[w];
+  const uint32_t rel_mask = (1u << lgs) - 1u;
+
+  // ---- stage the owned rows (row k = gw + k G), slice offsets by ballots ----
+  int off = 0;
+  bool fits = true;
+#pragma unroll 1
+  for (int k = 0; k < SW_RPW; ++k) {
+    const int64_t r = gw + k * G;
+    int64_t e0 = 0, e1 = 0;
+    if (r < m) {
+      e0 = rp[r];
+      e1 = rp[r + 1];
+    }
+    const int nk = (int)(e1 - e0);
+    fits = fits && off + nk <= SW_CAP;   // uniform
+    int lt = 0;                          // lane s: entries of the row in slices < s
+#pragma unroll 1
+    for (int i0 = 0; i0 < nk; i0 += 64) {
+      const int i = i0 + lane;
+      const bool ok = i < nk;
+      int c = 0;
+      unsigned short v = 0;
+      if (ok) {
+        c = ci[e0 + i];
+        v = av[e0 + i];
+      }
+      const int sl = c >> lgs;
+#pragma unroll
+      for (int s = 1; s <= SW_S; ++s) {
+        const unsigned long long b = __ballot(ok && sl < s);
+        if (lane == s) lt += __popcll(b);
+      }
+      if (fits && ok) E[off + i] = ((uint32_t)c & rel_mask) | ((uint32_t)v << 16);
+    }
+    if (lane <= SW_S) bnd[k][lane] = (uint16_t)(fits ? off + lt : 0);
+    off += nk;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  if (!fits && lane == 0) atomicOr(err, 1);   // (the host's plan rules it out; Y rows of this wave: 0)
+  // lane = (group g = lane / 16, part p = lane % 16): group g owns rows
+  // g, g + 4, g + 8, g + 12 of the wave (slot t = row / 4), part p output
+  // columns 8p .. 8p + 7; one load instruction gathers four X rows (one per
+  // group, 16 B per lane), SW_U entries of each of a group's rows per round
+  const int g = lane >> 4, p = lane & 15;
+  float acc[SW_RPW / 4][8];
+#pragma unroll
+  for (int t = 0; t < SW_RPW / 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[t][i] = 0.f;
+
+  if (fits) {
+    // ---- the sweep: slice s of every owned row, then slice s + 1 ----------
+#pragma unroll 1
+    for (int s = 0; s < SW_S; ++s) {
+      const int64_t cbase = (int64_t)s << lgs;
+      int bb[SW_RPW / 4], ee[SW_RPW / 4], lm = 0;
+#pragma unroll
+      for (int t = 0; t < SW_RPW / 4; ++t) {
+        bb[t] = bnd[g + 4 * t][s];
+        ee[t] = bnd[g + 4 * t][s + 1];
+        lm = max(lm, ee[t] - bb[t]);
+      }
+#pragma unroll
+      for (int o = 32; o >= 16; o >>= 1) lm = max(lm, __shfl_xor(lm, o));   // (groups differ; parts agree)
+      const int longest = __builtin_amdgcn_readfirstlane(lm);
+#pragma unroll 1
+      for (int j = 0; j < longest; j += SW_U) {
+        uint4 x[SW_RPW / 4][SW_U];
+#pragma unroll
+        for (int t = 0; t < SW_RPW / 4; ++t)
+#pragma unroll
+          for (int u = 0; u < SW_U; ++u) {
+            const int idx = bb[t] + j + u;
+            x[t][u] = make_uint4(0u, 0u, 0u, 0u);
+            if (idx < ee[t]) {
+              const uint32_t e = E[idx];
+              x[t][u] = *reinterpret_cast<const uint4*>(X + (cbase + (int64_t)(e & 0xFFFFu)) * ldx + 8 * p);
+            }
+          }
+#pragma unroll
+        for (int t = 0; t < SW_RPW / 4; ++t)
+#pragma unroll
+          for (int u = 0; u < SW_U; ++u) {
+            const int idx = bb[t] + j + u;
+            if (idx < ee[t]) {
+              const float a = bf2f((unsigned short)(E[idx] >> 16));
+              const unsigned w4[4] = {x[t][u].x, x[t][u].y, x[t][u].z, x[t][u].w};
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                acc[t][2 * h] += a * bf2f((unsigned short)(w4[h] & 0xFFFFu));
+                acc[t][2 * h + 1] += a * bf2f((unsigned short)(w4[h] >> 16));
+              }
+            }
+          }
+      }
+    }
+  }
+  // ---- Y rows: group g writes its rows' columns 8p .. 8p + 7 ---------------
+#pragma unroll
+  for (int t = 0; t < SW_RPW / 4; ++t) {
+    const int64_t r = gw + (int64_t)(g + 4 * t) * G;
+    if (r < m) {
+      if constexpr (OUT_BF16) {
+        uint4 o;
+        o.x = (unsigned)f2bf(acc[t][0]) | ((unsigned)f2bf(acc[t][1]) << 16);
+        o.y = (unsigned)f2bf(acc[t][2]) | ((unsigned)f2bf(acc[t][3]) << 16);
+        o.z = (unsigned)f2bf(acc[t][4]) | ((unsigned)f2bf(acc[t][5]) << 16);
+        o.w = (unsigned)f2bf(acc[t][6]) | ((unsigned)f2bf(acc[t][7]) << 16);
+        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned short*>(Yv) + r * ldy + 8 * p) = o;
+      } else {
+        float4* const y = reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + r * ldy + 8 * p);
+        y[0] = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+        y[1] = make_float4(acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
       }
     }
   }
@@ -669,6 +836,59 @@ SPMM_EXPORT int spmm_spmm_panel_mfma(const int64_t* panel_chunk_ptr, const int32
               : (out_bf16 ? spmm_panel_mfma<true> : spmm_panel_mfma<false>);
   hipLaunchKernelGGL(k, grid, dim3(NT), 0, (hipStream_t)stream, panel_chunk_ptr, chunk_cols, chunk_ent_ptr, ent_rc,
                      (const unsigned short*)ent_val, (const unsigned short*)X, ldx, m, Y, ldy);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// spmm_spmm_sweep's launch for an m x n operand: *waves = G (row k of wave
+// w is w + k G), *rpw = rows per wave (<= SW_RPW), *cap = LDS entries per
+// wave; *waves = 0 when it cannot run (too many rows for the resident grid,
+// or slices wider than 2^16 columns).  The host checks every wave's entry
+// count against *cap once per operand (ops/spmm.py sweep_plan).
+SPMM_EXPORT int spmm_spmm_sweep_geometry(int64_t m, int64_t n, int64_t* waves, int* rpw, int* cap) {
+  *waves = 0;
+  *rpw = SW_RPW;
+  *cap = SW_CAP;
+  int lgs = 0;
+  while (((int64_t)SW_S << lgs) < n) ++lgs;
+  if (lgs > 16 || m <= 0) return 0;
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  int per_bf = 0;   // (both output types share one geometry: the smaller residency)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, spmm_sweep<false>, NT, 0) != hipSuccess || per <= 0) per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_bf, spmm_sweep<true>, NT, 0) == hipSuccess && per_bf > 0 &&
+      per_bf < per)
+    per = per_bf;
+  int64_t g = (int64_t)per * ncu;
+  const int64_t need = (m + (int64_t)(NT / 64) * SW_RPW - 1) / ((int64_t)(NT / 64) * SW_RPW);
+  if (need > g) return 0;
+  const int64_t one_row = (m + NT / 64 - 1) / (NT / 64);
+  if (one_row < g) g = one_row;
+  *waves = g * (NT / 64);
+  return 0;
+}
+
+// Row-owning sweep (spmm_sweep): D == 128, ldx / ldy multiples of 8, 16-byte aligned X
+// and Y; the grid is the resident capacity and must hold every row in
+// SW_RPW rows per wave (else hipErrorInvalidValue: use spmm_spmm_rowwise).
+// n = columns of A: the slices are 2^lgs columns, lgs = ceil(log2(n / SW_S)).
+SPMM_EXPORT int spmm_spmm_sweep(const int64_t* rp, const int32_t* ci, const void* av, const void* X, int64_t ldx,
+                                int64_t m, int64_t n, int64_t D, void* Y, int64_t ldy, int out_bf16, int32_t* err,
+                                void* stream) {
+  if (m <= 0) return 0;
+  if (D != 128 || ldx % 8 != 0 || ldy % 8 != 0 || ((uintptr_t)X & 15) || ((uintptr_t)Y & 15)) return (int)hipErrorInvalidValue;
+  int lgs = 0;
+  while (((int64_t)SW_S << lgs) < n) ++lgs;   // (<= 16: slice-relative columns are 16-bit; geometry checks)
+  auto k = out_bf16 ? spmm_sweep<true> : spmm_sweep<false>;
+  int64_t waves = 0;
+  int rpw = 0, cap = 0;
+  const int rc = spmm_spmm_sweep_geometry(m, n, &waves, &rpw, &cap);
+  if (rc) return rc;
+  if (waves == 0) return (int)hipErrorInvalidValue;
+  const int64_t g = waves / (NT / 64);
+  hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(NT), 0, (hipStream_t)stream, rp, ci, (const unsigned short*)av,
+                     (const unsigned short*)X, ldx, m, lgs, Y, ldy, err);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

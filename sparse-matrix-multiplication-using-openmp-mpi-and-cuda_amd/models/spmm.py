@@ -20,7 +20,7 @@ from typing import Optional
 import torch
 
 from ..ops.csr import CSR
-from ..ops.spmm import PanelPlan, SpmmGraph, plan_panels, spmm
+from ..ops.spmm import PanelPlan, SpmmGraph, plan_panels, spmm, sweep_ok
 from ..parallel.comm import Comm
 from ..parallel.partition import row_panels
 from ..utils.config import CONFIG
@@ -104,7 +104,8 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
             # gather the same X bytes, so time both on this operand (one local
             # SpMM each, warm) and keep the faster one; both times are reported
             Xfull = torch.zeros((n, cols), dtype=torch.bfloat16, device=comm.device)
-            for meth in ("mfma", "rowwise"):
+            cands = ("mfma", "rowwise") + (("sweep",) if cols == 128 and sweep_ok(A) else ())
+            for meth in cands:
                 spmm(A, Xfull, method=meth, plan=plan)
                 torch.cuda.synchronize(comm.device)
                 t0 = time.perf_counter()
@@ -114,8 +115,9 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
                 kernel_ms[meth] = (time.perf_counter() - t0) * 1e3 / 10
             del Xfull
             # the slowest rank's view decides, so every rank runs the same kernel
-            faster = comm.allreduce_max(kernel_ms["mfma"] - kernel_ms["rowwise"])
-            method = "mfma" if faster <= 0 else "rowwise"
+            # (a kernel not available on some rank counts as infinitely slow there)
+            worst = {k: comm.allreduce_max(kernel_ms.get(k, float("inf"))) for k in ("mfma", "rowwise", "sweep")}
+            method = min(worst, key=worst.get)
     step = lambda: rowblock_spmm(A, Xp, comm, counts, plan=plan, method=method)  # noqa: E731
     if not comm.is_dist and comm.device.type == "cuda":
         # one GPU: the step is a single launch-bound SpMM -> replay it from a HIP graph

@@ -8,6 +8,10 @@ Two gfx950 kernels (``csrc/kernels/csr_spmm.hip``):
   entries into a dense 64x64 A tile and runs v_mfma_f32_16x16x32_bf16.
   X rows shared by several rows of a panel are fetched once.
 * ``rowwise`` — VALU row-gather kernel, no inspector; one wave per row.
+* ``sweep``   — VALU row-owning sweep (D = 128): a resident grid of waves,
+  each owning up to 16 rows staged in LDS, walks A's columns slice by slice
+  with 16 independent 16-byte gathers in flight per wave (:func:`sweep_ok`
+  checks once per operand that the rows fit).
 
 ``auto`` picks ``mfma`` when the panel column reuse (nnz / union columns) is
 at least ``MFMA_MIN_REUSE`` — i.e. when the MFMA path moves fewer bytes —
@@ -30,6 +34,9 @@ _native.register_hip("spmm_spmm_panel_mfma", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                      c_vp, C.c_int64, C.c_int, c_vp)
 _native.register_hip("spmm_spmm_rowwise", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp,
                      C.c_int64, C.c_int, c_vp)
+_native.register_hip("spmm_spmm_sweep", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, c_vp,
+                     C.c_int64, C.c_int, c_vp, c_vp)
+_native.register_hip("spmm_spmm_sweep_geometry", C.c_int64, C.c_int64, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spmm_plan_count", c_vp, c_vp, C.c_int64, C.c_int64, c_vp, c_vp)
 _native.register_hip("spmm_spmm_plan_fill", c_vp, c_vp, c_vp, C.c_int, C.c_int64, C.c_int64, c_vp, c_vp, c_vp, c_vp,
                      c_vp, c_vp, c_vp)
@@ -131,6 +138,26 @@ def _plan_panels_torch(A: CSR) -> PanelPlan:
                      int(uniq.numel()), A.nnz)
 
 
+def sweep_ok(A: CSR) -> bool:
+    """Whether the row-owning sweep kernel (``method="sweep"``,
+    csr_spmm.hip spmm_sweep) can take A on this GPU: its resident grid holds
+    every row (<= 16 rows per wave) and no wave's rows hold more entries than
+    its LDS stage.  One read-back; done once per operand (an inspector step,
+    like :func:`plan_panels`)."""
+    if A.device.type != "cuda" or A.m == 0:
+        return False
+    waves, rpw, cap = C.c_int64(), C.c_int(), C.c_int()
+    _native.check(_native.hip().spmm_spmm_sweep_geometry(A.m, A.n, C.byref(waves), C.byref(rpw), C.byref(cap)),
+                  "spmm_sweep_geometry")
+    G = waves.value
+    if G == 0:
+        return False
+    lens = (A.rowptr[1:] - A.rowptr[:-1]).to(torch.int64)
+    padded = torch.zeros(rpw.value * G, dtype=torch.int64, device=A.device)
+    padded[:A.m] = lens
+    return int(padded.view(rpw.value, G).sum(0).max()) <= cap.value   # row k of wave w = w + k G
+
+
 def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
          plan: Optional[PanelPlan] = None) -> torch.Tensor:
     if X.dim() != 2 or X.shape[0] != A.n:
@@ -164,6 +191,13 @@ def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
         _native.check(lib.spmm_spmm_panel_mfma(P(plan.panel_chunk_ptr), P(plan.chunk_cols), P(plan.chunk_ent_ptr),
                                                P(plan.ent_rc), P(plan.ent_val), P(X), D, A.m, D, P(Y), D, out_bf16,
                                                stream), "spmm_panel_mfma")
+    elif method == "sweep":   # the caller checked sweep_ok(A) (err: a wave over its LDS stage, Y rows zero)
+        if D != 128:
+            raise ValueError("the sweep SpMM kernel needs D == 128")
+        av = A.val.to(torch.bfloat16).contiguous()
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        _native.check(lib.spmm_spmm_sweep(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, A.n, D, P(Y), D, out_bf16,
+                                          P(err), stream), "spmm_sweep")
     elif method == "rowwise":
         av = A.val.to(torch.bfloat16).contiguous()
         _native.check(lib.spmm_spmm_rowwise(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, D, P(Y), D, out_bf16,

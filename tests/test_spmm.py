@@ -138,6 +138,37 @@ def test_spmm_rowwise_exact_small_integers(D):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m,n,d", [(301, 2000, 0.05), (65536, 65536, 1e-3), (7, 100000, 0.01), (20000, 1000, 0.02)])
+def test_spmm_sweep_exact_small_integers(m, n, d):
+    """Row-owning sweep kernel on exact integer data: empty rows, a row
+    count that leaves waves with fewer rows than their 16, the bench operand
+    (16 rows per wave), a ragged last column slice (n = 100000), few columns;
+    both output types equal the fp32 reference bit for bit."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(m, n, d, seed=23, values="small_int")
+    keep = (A.row_ids() % 7) != 3                       # every 7th row empty
+    A = CS.from_coo(A.row_ids()[keep], A.col[keep].long(), A.val[keep].float(), m, n)
+    A = A.with_values(A.val.to(torch.bfloat16)).to(dev)
+    assert SM.sweep_ok(A)
+    X = (torch.arange(n * 128, device=dev).view(n, 128) % 13 - 6).to(torch.bfloat16)
+    R = ref(A, X)
+    assert torch.equal(SM.spmm(A, X, method="sweep"), R)
+    assert torch.equal(SM.spmm(A, X, method="sweep", out_dtype=torch.bfloat16).float(), R.to(torch.bfloat16).float())
+
+
+@pytest.mark.gpu
+def test_spmm_sweep_refuses_what_it_cannot_stage():
+    """sweep_ok: rows whose entries overflow a wave's LDS stage (here every
+    row has 2000 entries) or more rows than the resident grid holds at 16 per
+    wave are refused, so the autotuner never offers the kernel for them."""
+    dev = torch.device("cuda")
+    dense_rows = gen_csr.uniform_csr(64, 4000, 0.5, seed=1, device=dev, dtype=torch.bfloat16)
+    assert not SM.sweep_ok(dense_rows)
+    tall = gen_csr.uniform_csr(1 << 21, 64, 0.01, seed=2, device=dev, dtype=torch.bfloat16)
+    assert not SM.sweep_ok(tall)
+
+
+@pytest.mark.gpu
 def test_spmm_graph_replay_matches_eager():
     """The HIP-graph replay of the SpMM step gives the eager result, also after
     new operands are copied into the static input."""
