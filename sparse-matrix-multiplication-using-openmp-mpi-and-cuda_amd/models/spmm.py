@@ -99,12 +99,15 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     kernel_ms = {}
     if method == "auto":
         method = "mfma" if plan is not None and cols % 128 == 0 and plan.reuse >= CONFIG.spmm_mfma_min_reuse else "rowwise"
-        if method == "mfma" and comm.device.type == "cuda":
-            # executor choice at inspection time: near reuse 1 the two kernels
-            # gather the same X bytes, so time both on this operand (one local
-            # SpMM each, warm) and keep the faster one; both times are reported
+        if comm.device.type == "cuda":
+            # executor choice at inspection time: time every kernel that can
+            # take this operand (one local SpMM each, warm, 10 calls) and keep
+            # the fastest; all times are reported.  Panel reuse decides the
+            # order (tools/probes/spmm_reuse.py: MFMA from reuse ~1.6 up, the
+            # sweep / row kernels near 1), but the measured time decides.
             Xfull = torch.zeros((n, cols), dtype=torch.bfloat16, device=comm.device)
-            cands = ("mfma", "rowwise") + (("sweep",) if cols == 128 and sweep_ok(A) else ())
+            cands = (("mfma",) if plan is not None and cols % 128 == 0 else ()) + ("rowwise",) + (
+                ("sweep",) if cols == 128 and sweep_ok(A) else ())
             for meth in cands:
                 spmm(A, Xfull, method=meth, plan=plan)
                 torch.cuda.synchronize(comm.device)
