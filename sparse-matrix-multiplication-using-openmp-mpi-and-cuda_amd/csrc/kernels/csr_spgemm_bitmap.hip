@@ -1981,7 +1981,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
 // runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
 // wave's own bitmap rows, clear of the same rows, one barrier.
 template <int LGW, int NSUB, int NT, int RR, int CCAP>
-__global__ __launch_bounds__(NT, 8) void spgemm_bm_rows_count(BmRowArgs ra) {   // (8 waves per SIMD: <= 64 VGPRs)
+#ifndef SPMM_BM_COUNT_WPS   // row count kernel: waves per SIMD its registers are sized for (8: <= 64 VGPRs)
+#define SPMM_BM_COUNT_WPS 8   // (64k: 8 = 1.547-1.551 ms with 2 spills, 7 = 1.547-1.565, 6 = 1.641)
+#endif
+__global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
