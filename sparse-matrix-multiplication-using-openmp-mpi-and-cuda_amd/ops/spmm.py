@@ -146,6 +146,14 @@ def sweep_ok(A: CSR) -> bool:
     like :func:`plan_panels`)."""
     if A.device.type != "cuda" or A.m == 0:
         return False
+    cached = getattr(A, "_sweep_ok", None)
+    if cached is not None:
+        return cached
+    A._sweep_ok = _sweep_fits(A)
+    return A._sweep_ok
+
+
+def _sweep_fits(A: CSR) -> bool:
     waves, rpw, cap = C.c_int64(), C.c_int(), C.c_int()
     _native.check(_native.hip().spmm_spmm_sweep_geometry(A.m, A.n, C.byref(waves), C.byref(rpw), C.byref(cap)),
                   "spmm_sweep_geometry")
@@ -191,9 +199,15 @@ def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
         _native.check(lib.spmm_spmm_panel_mfma(P(plan.panel_chunk_ptr), P(plan.chunk_cols), P(plan.chunk_ent_ptr),
                                                P(plan.ent_rc), P(plan.ent_val), P(X), D, A.m, D, P(Y), D, out_bf16,
                                                stream), "spmm_panel_mfma")
-    elif method == "sweep":   # the caller checked sweep_ok(A) (err: a wave over its LDS stage, Y rows zero)
+    elif method == "sweep":
         if D != 128:
             raise ValueError("the sweep SpMM kernel needs D == 128")
+        if getattr(A, "_sweep_ok", None) is None and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("spmm(method='sweep') inside a graph capture: call sweep_ok(A) before capturing")
+        if not sweep_ok(A):   # (cached per operand after the first call)
+            raise ValueError("the sweep SpMM kernel cannot stage this operand (sweep_ok(A) is False)")
+        # err: device-side guard of the same condition (a wave over its LDS stage writes zero rows);
+        # the plan check above rules it out, so it is not read back
         av = A.val.to(torch.bfloat16).contiguous()
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         _native.check(lib.spmm_spmm_sweep(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, A.n, D, P(Y), D, out_bf16,

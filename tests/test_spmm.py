@@ -166,6 +166,8 @@ def test_spmm_sweep_refuses_what_it_cannot_stage():
     assert not SM.sweep_ok(dense_rows)
     tall = gen_csr.uniform_csr(1 << 21, 64, 0.01, seed=2, device=dev, dtype=torch.bfloat16)
     assert not SM.sweep_ok(tall)
+    with pytest.raises(ValueError):
+        SM.spmm(dense_rows, torch.zeros(4000, 128, device=dev, dtype=torch.bfloat16), method="sweep")
 
 
 @pytest.mark.gpu
