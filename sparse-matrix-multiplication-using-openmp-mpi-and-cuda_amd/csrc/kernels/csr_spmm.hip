@@ -504,7 +504,7 @@ __global__ __launch_bounds__(NT, 4) void spmm_sweep(const int64_t* __restrict__ 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  if (!fits && lane == 0) atomicOr(err, 1);   // (the host's plan rules it out; Y rows of this wave: 0)
+  if (!fits && lane == 0 && err != nullptr) atomicOr(err, 1);   // (the host's plan rules it out; Y rows: 0)
   // lane = (group g = lane / 16, part p = lane % 16): group g owns rows
   // g, g + 4, g + 8, g + 12 of the wave (slot t = row / 4), part p output
   // columns 8p .. 8p + 7; one load instruction gathers four X rows (one per
@@ -872,7 +872,8 @@ SPMM_EXPORT int spmm_spmm_sweep_geometry(int64_t m, int64_t n, int64_t* waves, i
 // Row-owning sweep (spmm_sweep): D == 128, ldx / ldy multiples of 8, 16-byte aligned X
 // and Y; the grid is the resident capacity and must hold every row in
 // SW_RPW rows per wave (else hipErrorInvalidValue: use spmm_spmm_rowwise).
-// n = columns of A: the slices are 2^lgs columns, lgs = ceil(log2(n / SW_S)).
+// n = columns of A: the slices are 2^lgs columns, lgs = ceil(log2(n / SW_S)).  err (may be null):
+// set when a wave would overflow its LDS stage (the host plan check rules it out).
 SPMM_EXPORT int spmm_spmm_sweep(const int64_t* rp, const int32_t* ci, const void* av, const void* X, int64_t ldx,
                                 int64_t m, int64_t n, int64_t D, void* Y, int64_t ldy, int out_bf16, int32_t* err,
                                 void* stream) {

@@ -206,12 +206,11 @@ def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
             raise RuntimeError("spmm(method='sweep') inside a graph capture: call sweep_ok(A) before capturing")
         if not sweep_ok(A):   # (cached per operand after the first call)
             raise ValueError("the sweep SpMM kernel cannot stage this operand (sweep_ok(A) is False)")
-        # err: device-side guard of the same condition (a wave over its LDS stage writes zero rows);
-        # the plan check above rules it out, so it is not read back
+        # (the kernel's err word flags the same condition device-side: a wave over its LDS stage
+        # writes zero rows; the plan check above rules it out, so no word is passed or read back)
         av = A.val.to(torch.bfloat16).contiguous()
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
         _native.check(lib.spmm_spmm_sweep(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, A.n, D, P(Y), D, out_bf16,
-                                          P(err), stream), "spmm_sweep")
+                                          None, stream), "spmm_sweep")
     elif method == "rowwise":
         av = A.val.to(torch.bfloat16).contiguous()
         _native.check(lib.spmm_spmm_rowwise(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, D, P(Y), D, out_bf16,
