@@ -318,6 +318,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   int vz;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   BM_STAMP_DECL
+  if constexpr (MODE != 0) {
+    // numeric / reload after a row count that stood down (ws8 lengths
+    // truncated, err bit 3; the host reruns the product on the per-unit count):
+    // the unit offsets are not valid, so nothing is formed (uniform exit)
+    if (*p.err & 8) return;
+  }
 
   // bitmap clear: 16-byte stores, consecutive lanes on consecutive slots (conflict-free)
   auto clear_bm = [&]() {
@@ -951,9 +957,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   int vz;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   BM_STAMP_DECL
-  if constexpr (FUSED) {
-    if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
-  }
+  if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
 
   auto clear_bm = [&]() {
     for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
@@ -1644,6 +1648,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
 // stores too.  The row pipeline is the row-major kernel's, one window earlier.
 template <int LGW, int NT, int PCAP, int R, int CCAP>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
+  if (*ra.a.err & 8) return;   // ws8 lengths truncated (see spgemm_bm_rows)
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;

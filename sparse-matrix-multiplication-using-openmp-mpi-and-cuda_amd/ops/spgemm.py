@@ -719,7 +719,8 @@ def _bitmap_ok(A: CSR, B: CSR, total_products: int, pre: dict) -> bool:
     return _FreeMem(A.device).fits(total_products * 8 + A.m * 64)
 
 
-def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional[dict] = None) -> Optional[CSR]:
+def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional[dict] = None,
+                   _eager: bool = False) -> Optional[CSR]:
     """Bitmap-rank SpGEMM (csr_spgemm_bitmap.hip): a count kernel gives the
     exact nnz of every (row, column window) unit, one scan gives every unit's
     final offset, and the numeric kernel writes each unit there once (no
@@ -780,8 +781,15 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
         uoff[0] = 0
         torch.cumsum(ucnt, 0, out=uoff[1:])
+        if lazy:
+            return uoff, (None, 0)
         return uoff, torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
 
+    # lazy (SPMM_SPGEMM_BITMAP_LAZY=1): C at the product-count bound (what _bitmap_ok admitted), so the
+    # numeric kernels follow the count in stream order and the nnz / error bits are
+    # read once, after the product; the kernels using ws8 exit on err bit 3 (its
+    # lengths truncated), which sends the product through the eager path below
+    lazy = CONFIG.spgemm_bitmap_lazy > 0 and not det and not _eager
     uoff, (nnz, e0) = count(count_rows)
     if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
         ws8 = None
@@ -790,10 +798,12 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     del ucnt
     if B_ready is not None:   # the numeric kernels read the values
         B = B_ready()
-    err.zero_()
-    info.nnz = nnz
-    Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
-    Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
+    if not lazy:
+        err.zero_()
+        info.nnz = nnz
+    cap = max(tot, 1) if lazy else nnz
+    Cci = torch.empty(cap, dtype=torch.int32, device=dev)
+    Cv = torch.empty(cap, dtype=torch.float32, device=dev)
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
     if ws8 is not None and (rows_mode in ("on", "pipe", "nopipe") or cfg == 0):
@@ -803,15 +813,22 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         Bcv = None if pipe or not CONFIG.spgemm_bitmap_cv else interleaved(B)
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
-                                                      lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf),
+                                                      lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf),
                                                       P(novf), ovf_cap, P(err), int(pipe and not det), int(det), st),
                       "spgemm_bm_numeric_rows")
         info.rows_per_bin_num["bitmap_rows"] = 2 if pipe and not det else 1
     else:
         _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
-                                                 nwin, lg_num, P(uoff), nnz, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap,
+                                                 nwin, lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap,
                                                  P(err), int(det), st), "spgemm_bm_numeric")
-    e, deferred = z.tolist()
+    if lazy:
+        nnz, e, deferred = torch.stack([uoff[-1], z[0].long(), z[1].long()]).tolist()   # the one read-back
+        if e & 8:   # ws8 lengths truncated: the count and numeric kernels stood down
+            del Cci, Cv
+            return onepass_bitmap(A, B, info, None, pre, _eager=True)
+        info.nnz = nnz
+    else:
+        e, deferred = z.tolist()
     info.rows_per_bin_num["bitmap_units"] = nunits
     info.rows_per_bin_num["bitmap_cfg"] = cfg
     info.rows_per_bin_num["bitmap_deferred"] = deferred
@@ -828,7 +845,7 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
         return None
     info.deterministic = bool(det)
     rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
-    return CSR(m, B.n, rowptr, Cci, Cv)
+    return CSR(m, B.n, rowptr, Cci[:nnz] if lazy else Cci, Cv[:nnz] if lazy else Cv)
 
 
 _FALLBACK = object()   # _bitmap_fused: the product needs the binned path

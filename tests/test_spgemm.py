@@ -657,6 +657,34 @@ def test_spgemm_gpu_bitmap_fused(monkeypatch, case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lazy", [1, 0])
+def test_spgemm_gpu_bitmap_truncated_window_lengths(monkeypatch, lazy):
+    """A B row with >= 65536 entries inside one window does not fit the row
+    kernels' 16-bit window lengths (ws8, err bit 3).  Eager flow: the row
+    count stands down and the per-unit kernels count; lazy flow (C at the
+    product bound, one read-back): the numeric kernels stand down too and the
+    product reruns eagerly.  Either way C equals the binned path (the long B
+    row is never referenced by A, so no unit exceeds the reload budget)."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    k, n = 4000, 300000
+    base = gen_csr.uniform_csr(k, n, 2e-4, seed=31)
+    r0, c0 = base.row_ids(), base.col.long()
+    keep = r0 != 17
+    long_cols = torch.randperm(1 << 17)[:70000]
+    rows = torch.cat([r0[keep], torch.full((70000,), 17)])
+    cols = torch.cat([c0[keep], long_cols])
+    B = CS.from_coo(rows, cols, torch.rand(rows.numel()) - 0.5, k, n).to(dev)
+    A = gen_csr.uniform_csr(600, k, 0.01, seed=32)
+    ka = A.col.long() != 17
+    A = CS.from_coo(A.row_ids()[ka], A.col.long()[ka], A.val[ka], 600, k).to(dev)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_lazy", lazy)
+    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    assert "bitmap_units" in info.rows_per_bin_num
+
+
+@pytest.mark.gpu
 def test_spgemm_gpu_bitmap_deferred_units_and_fallback(monkeypatch):
     """Rows too long for the fast kernel (A rows > 256 entries, windows above
     its product capacity) are deferred to the reload kernel; a unit beyond the
