@@ -1043,7 +1043,10 @@ __device__ __forceinline__ int wave_incl_max_dpp(int x) {
   return x;
 }
 
-constexpr int LR_R = 16, LR_CAP = LR_R * 64, LR_WAVES = 4;
+#ifndef SPMM_LR_R   // long_rank: register rounds per lane (items of <= 64 * LR_R products; larger ones go to long_dense)
+#define SPMM_LR_R 16   // (8: 4 workgroups/CU instead of 3, but R-MAT 22 2.11-2.15 vs 1.99-2.01 s/step)
+#endif
+constexpr int LR_R = SPMM_LR_R, LR_CAP = LR_R * 64, LR_WAVES = 4;
 constexpr int LR_WORDS = LONG_W / 64;   // 64-bit bitmap words per chunk
 static_assert(LR_WORDS % 64 == 0, "whole bitmap rows per lane");
 
