@@ -279,6 +279,11 @@ def main() -> None:
         print(f"[bench] launcher world size {env_world} != --gpus {args.gpus}", file=sys.stderr, flush=True)
         sys.exit(2)
 
+    if os.environ.get("SPMM_BENCH_DUMP_S"):   # diagnostics: every thread's stack every N seconds (stderr)
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["SPMM_BENCH_DUMP_S"]), repeat=True)
+
     import torch
 
     import spmm_amd  # noqa: F401
