@@ -41,6 +41,9 @@
 #define SPMM_BM_SWEEP_G 2
 #endif
 
+#ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
+#define SPMM_BM_P2_G 4
+#endif
 #ifndef SPMM_BM_SKIP_ROUNDS   // numeric pass 2: skip register rounds past the unit's chunk count (uniform)
 #define SPMM_BM_SKIP_ROUNDS 1
 #endif
@@ -275,7 +278,9 @@ struct BmArgs {
                            // bit 2: deferred list full (host falls back)
 };
 
-template <int LGW, int NSUB, int NT, int PCAP, int R, int CCAP, int MODE, bool DET = false>
+// CV: B read as interleaved (column, value bits) pairs (p.Bcv): one 8-byte load
+// per product instead of two 4-byte ones (numeric modes only)
+template <int LGW, int NSUB, int NT, int PCAP, int R, int CCAP, int MODE, bool DET = false, bool CV = false>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   using Gm = BmGeom<LGW, NSUB, NT, PCAP, R, CCAP, MODE>;
   constexpr int NW = NT / 64;
@@ -470,8 +475,14 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       x[d] = 0;
       b[d] = 0.f;
       if (i0 + d < nr) {   // wave-uniform
-        x[d] = p.Bci[f[d]];
-        if constexpr (VALUES) b[d] = p.Bv[f[d]];
+        if constexpr (CV && VALUES) {
+          const uint2 e = p.Bcv[f[d]];
+          x[d] = (int)e.x;
+          b[d] = __uint_as_float(e.y);
+        } else {
+          x[d] = p.Bci[f[d]];
+          if constexpr (VALUES) b[d] = p.Bv[f[d]];
+        }
       }
     }
 #pragma unroll
@@ -722,17 +733,18 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
       };
       if constexpr (MODE == 1) {
-        // ranks of 4 rounds at a time (their LDS reads in flight together)
+        // ranks of P2G rounds at a time (their LDS reads in flight together)
+        constexpr int P2G = SPMM_BM_P2_G;
 #pragma unroll
-        for (int d0 = 0; d0 < RR; d0 += 4) {
+        for (int d0 = 0; d0 < RR; d0 += P2G) {
 #if SPMM_BM_SKIP_ROUNDS
           if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
 #endif
-          int r[4];
+          int r[P2G];
 #pragma unroll
-          for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
+          for (int dd = 0; dd < P2G && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
 #pragma unroll
-          for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) {
+          for (int dd = 0; dd < P2G && d0 + dd < RR; ++dd) {
             const int d = d0 + dd;
             if (c[d] >= 0 && !((dupm >> d) & 1u))
               items[r[dd]] = ((unsigned long long)__float_as_uint(v[d]) << 32) | (uint32_t)(c[d] + clo);
@@ -2340,6 +2352,8 @@ struct BmKernels {
   static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, kReloadPcap, 8, kReloadCcap, 2>;
   static constexpr auto fast_det = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
                                              K.rounds_fast * (kFastNT / 16), 1, true>;
+  static constexpr auto fast_cv = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
+                                            K.rounds_fast * (kFastNT / 16), 1, false, true>;
   static constexpr auto reload_det = spgemm_bm<K.lgw, 1, kReloadNT, kReloadPcap, 8, kReloadCcap, 2, true>;
 };
 
@@ -2465,7 +2479,8 @@ int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, int det, hipStream_t s) 
 template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, int det, hipStream_t s) {
   using K = BmKernels<C>;
-  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s);
+  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s)
+                     : (a.Bcv ? launch_bm(K::fast_cv, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s));
   if (rc) return rc;
   return det ? launch_bm(K::reload_det, K::kReloadNT, int64_t(1) << 30, a, s)
              : launch_bm(K::reload, K::kReloadNT, int64_t(1) << 30, a, s);
@@ -2525,14 +2540,17 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
 // units it deferred (novf must be zero; ovf has room for ovf_cap units).
 // det: fixed summation order (see "deterministic mode"); err bit 4 then
 // means a unit needs the CPU engine.
-SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
-                                       const uint32_t* ws, const int32_t* Bci, const float* Bv, int64_t m, int nwin,
-                                       int lg, const int64_t* uoff, int64_t cap, int32_t* Cci, float* Cv,
-                                       int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, int det,
-                                       void* stream) {
+// Bcv: optional [nnz(B)] (column, value bits) pairs for the fast kernel (not
+// with det; the reload kernel reads Bci / Bv).
+SPMM_EXPORT int spmm_spgemm_bm_numeric_cv(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                                          const uint32_t* ws, const int32_t* Bci, const float* Bv, const void* Bcv,
+                                          int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap, int32_t* Cci,
+                                          float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err,
+                                          int det, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
-  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, nullptr, err};
+  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
+           det ? nullptr : (const uint2*)Bcv, err};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * nwin;
   switch (cfg) {
@@ -2540,6 +2558,15 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_
     case 1: return bm_numeric<1>(work, a, det, s);
     default: return bm_numeric<2>(work, a, det, s);
   }
+}
+
+SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                                       const uint32_t* ws, const int32_t* Bci, const float* Bv, int64_t m, int nwin,
+                                       int lg, const int64_t* uoff, int64_t cap, int32_t* Cci, float* Cv,
+                                       int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, int det,
+                                       void* stream) {
+  return spmm_spgemm_bm_numeric_cv(cfg, Arp, Aci, Av, ws, Bci, Bv, nullptr, m, nwin, lg, uoff, cap, Cci, Cv, ovf, novf,
+                                   ovf_cap, err, det, stream);
 }
 
 // Diagnostics: on >= 0 resets the stamp accumulators and enables (1) or

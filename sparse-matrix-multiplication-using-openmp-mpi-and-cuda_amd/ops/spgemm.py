@@ -75,6 +75,8 @@ _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64,
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
                      C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
+_native.register_hip("spmm_spgemm_bm_numeric_cv", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT,
+                     c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -818,9 +820,13 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
                       "spgemm_bm_numeric_rows")
         info.rows_per_bin_num["bitmap_rows"] = 2 if pipe and not det else 1
     else:
-        _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
-                                                 nwin, lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap,
-                                                 P(err), int(det), st), "spgemm_bm_numeric")
+        # per-unit kernel: B as interleaved (column, value) pairs when enabled
+        # (SPMM_SPGEMM_BITMAP_UNIT_CV; not with det)
+        Bcv = interleaved(B) if CONFIG.spgemm_bitmap_unit_cv and not det else None
+        _native.check(lib.spmm_spgemm_bm_numeric_cv(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val),
+                                                    P(Bcv) if Bcv is not None else None, m, nwin, lg_num, P(uoff), cap,
+                                                    P(Cci), P(Cv), P(ovf), P(novf), ovf_cap, P(err), int(det), st),
+                      "spgemm_bm_numeric")
     if lazy:
         nnz, e, deferred = torch.stack([uoff[-1], z[0].long(), z[1].long()]).tolist()   # the one read-back
         if e & 8:   # ws8 lengths truncated: the count and numeric kernels stood down

@@ -57,6 +57,8 @@ class Config:
     # numeric kernels (1), or C allocated exactly after a read-back between count and numeric (0,
     # default: the two measure the same, 64k 1.564 vs 1.567 ms, 1M 75.7-76.0 vs 75.7-76.1 ms)
     spgemm_bitmap_lazy: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_LAZY", 0, int))
+    # per-unit numeric kernel reads B as interleaved (column, value) pairs (one 8-byte load per product)
+    spgemm_bitmap_unit_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_UNIT_CV", 0, int))
     # windows per row-major count unit (1: 16 KB bitmaps, 8 per CU; 2: 32 KB, 4 per CU)
     spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
     # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU
