@@ -41,8 +41,11 @@
 #define SPMM_BM_SWEEP_G 2
 #endif
 
+#ifndef SPMM_BM_ILV   // per-unit fast kernel (W <= 2^15): bitmap and rank prefixes interleaved per 32-bit word
+#define SPMM_BM_ILV 0   // ({bits, prefix} pairs: one 8-byte LDS read per rank lookup instead of two reads)
+#endif
 #ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
-#define SPMM_BM_P2_G 4
+#define SPMM_BM_P2_G 2   // 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586 (fewer empty rounds past the chunk count); 7 spills
 #endif
 #ifndef SPMM_BM_SKIP_ROUNDS   // numeric pass 2: skip register rounds past the unit's chunk count (uniform)
 #define SPMM_BM_SKIP_ROUNDS 1
@@ -286,6 +289,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   constexpr int NW = NT / 64;
   constexpr bool VALUES = MODE != 0;
   constexpr int NWORD = Gm::NWORD, WPW = Gm::WPW, WPT = Gm::WPT;
+  // ILV: 32-bit bitmap word k at bm32[2k], its exclusive rank prefix at bm32[2k + 1]
+  constexpr bool ILV = SPMM_BM_ILV && MODE == 1 && LGW <= 15 && !DET;
   constexpr int RR = MODE == 1 ? R : (MODE == 0 ? 16 : 8);   // rounds of loads in flight per block
   // deterministic fix-up list: the fast kernel defers a unit that overflows
   // it to the reload kernel, whose list is larger (it has one CU's LDS)
@@ -296,8 +301,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   // LDS.  bm: the window's column bitmap.  pre16: exclusive rank prefix of
   // every 64-bit word.  items: (column, value) of every output slot.
   // desc: chunk descriptors {first B index, valid lanes, a(i, j) bits}.
-  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
-  __shared__ __attribute__((aligned(16))) uint16_t pre16[VALUES ? NWORD : 1];
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[ILV ? 2 * NWORD : NWORD];
+  __shared__ __attribute__((aligned(16))) uint16_t pre16[VALUES && !ILV ? NWORD : 1];
   __shared__ __attribute__((aligned(16))) unsigned long long items[VALUES ? PCAP : 1];
   using Desc = typename std::conditional<VALUES, uint4, uint2>::type;
   __shared__ __attribute__((aligned(16))) Desc desc[CCAP];
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 
   // bitmap clear: 16-byte stores, consecutive lanes on consecutive slots (conflict-free)
   auto clear_bm = [&]() {
-    for (int i = tid; i < Gm::NCLR; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < (ILV ? 2 : 1) * Gm::NCLR; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
   };
   clear_bm();
   if (tid < NSUB) scnt[tid] = 0;
@@ -505,7 +510,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 #pragma unroll
       for (int d = 0; d < RR; ++d) {
         old[d] = 0u;
-        if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
+        if (c[d] >= 0) old[d] = atomicOr(bm32 + ((c[d] >> 5) << (ILV ? 1 : 0)), 1u << (c[d] & 31));
       }
 #pragma unroll
       for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
@@ -654,8 +659,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       // ---- rank prefix per 64-bit word: wave w owns words [w*WPW, (w+1)*WPW)
       // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
       // wave scan of their sum, 16-bit prefixes stored SG at a time)
-      constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+      constexpr int SG = (!ILV && SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
       constexpr bool PAIRS = SG > 1;
+      uint4* const bm4 = reinterpret_cast<uint4*>(bm);   // ILV: {bits lo, prefix lo, bits hi, prefix hi} per 64-bit word
       int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
       int wtot = 0;
       if constexpr (PAIRS) {
@@ -680,12 +686,24 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
           wtot += __builtin_amdgcn_readlane(incl, 63);
         }
       } else {
+        int lo[ILV ? WPT : 1];
 #pragma unroll
         for (int kk = 0; kk < WPT; ++kk) {
-          const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
+          int cnt;
+          if constexpr (ILV) {
+            const uint4 q = bm4[w * WPW + kk * 64 + lane];
+            lo[kk] = __popc(q.x);
+            cnt = lo[kk] + __popc(q.z);
+          } else {
+            cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
+          }
           const int incl = bm_wave_incl(cnt);
           run[kk] = wtot + incl - cnt;
           wtot += __builtin_amdgcn_readlane(incl, 63);
+        }
+        if constexpr (ILV) {   // (the prefixes are written after the block totals, below)
+#pragma unroll
+          for (int kk = 0; kk < WPT; ++kk) run[kk] |= lo[kk] << 16;
         }
       }
       const int any_dup = sdup;
@@ -719,6 +737,14 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
+      } else if constexpr (ILV) {
+#pragma unroll
+        for (int kk = 0; kk < WPT; ++kk) {
+          const uint32_t g = (uint32_t)(base + (run[kk] & 0xffff));
+          uint32_t* q = reinterpret_cast<uint32_t*>(&bm4[w * WPW + kk * 64 + lane]);
+          q[1] = g;
+          q[3] = g + ((uint32_t)run[kk] >> 16);
+        }
       } else {
 #pragma unroll
         for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
@@ -729,8 +755,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       // ---- pass 2: rank -> slot; owners store (column, value), duplicates
       // add their value after a barrier (bit set by an earlier product)
       auto rank = [&](int cc) {
-        const int wd = cc >> 6;
-        return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
+        if constexpr (ILV) {
+          const uint2 e = reinterpret_cast<const uint2*>(bm)[cc >> 5];
+          return (int)e.y + __popc(e.x & ((1u << (cc & 31)) - 1u));
+        } else {
+          const int wd = cc >> 6;
+          return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
+        }
       };
       if constexpr (MODE == 1) {
         // ranks of P2G rounds at a time (their LDS reads in flight together)
@@ -2330,7 +2361,8 @@ struct BmCfg {
 #ifndef SPMM_BM_CFG1_R   // register rounds of cfg 1's per-unit fast kernel (the 65536^2 config)
 #define SPMM_BM_CFG1_R 14   // 65536^2: 16 rounds spill 5 VGPRs; 14 = 1.64 -> 1.56 ms (384 of 131072 units deferred), 13: 1.61-1.67, 12: 1.82
 #endif
-constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12}, {15, 2, 3840, SPMM_BM_CFG1_R}, {16, 4, 3072, 16}};
+// (SPMM_BM_ILV: cfg 1's interleaved bitmap takes 3 KB more LDS, so 256 fewer product slots keep 4 per CU)
+constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12}, {15, 2, SPMM_BM_ILV ? 3584 : 3840, SPMM_BM_CFG1_R}, {16, 4, 3072, 16}};
 constexpr int kNumCfgs = 3;
 constexpr int kFastNT = 256, kReloadPcap = 12288, kReloadCcap = 2048;
 #ifndef SPMM_BM_ROWS_NT   // threads of the row-major numeric kernel's workgroups (256 or 512; 4 workgroups per CU)
