@@ -72,9 +72,37 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
         step = lambda: MS.rowblock_spgemm(prob.A, prob.B, comm)  # noqa: E731
     flops_local = info.flops
     del C
+    graph = None
+    if not comm.is_dist and comm.device.type == "cuda" and args.decomp != "inner" and args.graph == "on":
+        # one GPU: the product's kernels (splits, count, scan, numeric) replayed
+        # from a captured HIP graph, no host synchronisation inside the step
+        import torch
+
+        from spmm_amd.ops.spgemm import SpgemmGraph
+
+        try:
+            torch.cuda.empty_cache()
+            graph = SpgemmGraph(prob.A, prob.B)
+            step = lambda: graph.run()  # noqa: E731
+        except Exception as e:   # noqa: BLE001  (no graph for this product: eager steps, said so)
+            print(f"[bench] spgemm graph unavailable ({e}); eager steps", file=sys.stderr, flush=True)
+            graph = None
+            torch.cuda.empty_cache()
+
+        def verify():   # after the timed loop: the last replay's C is the eager product's
+            if graph is None:
+                return {}
+            gi = SpgemmInfo()
+            Cg = graph.result(gi)
+            if Cg is None or gi.nnz != nnz_local:
+                raise SystemExit(f"[bench] graph replay disagrees with the eager product: nnz {gi.nnz} vs {nnz_local}")
+            return dict(graph_replay_nnz=gi.nnz, bitmap_cfg=gi.rows_per_bin_num.get("bitmap_cfg"),
+                        bitmap_deferred=gi.rows_per_bin_num.get("bitmap_deferred"))
+        if graph is not None:
+            step.verify = verify
     total_flops = int(_allreduce_sum(comm, flops_local))
     total_nnz = _allreduce_sum(comm, nnz_local)
-    extra = dict(nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(total_nnz))
+    extra = dict(nnz_A=int(_allreduce_sum(comm, prob.A.nnz)), nnz_C=int(total_nnz), hip_graph=graph is not None)
     return step, total_flops, extra, dict(model=model, n=n, density=density, dtype_values="fp32",
                                           global_batch=1, seq_len=n, parallelism=f"{'innerdim' if args.decomp == 'inner' else 'rowblock'}{comm.world}")
 
@@ -136,7 +164,7 @@ def run_spmm(comm, args):
     from spmm_amd.models import spmm as MM
 
     step, flops, extra, cfg = MM.bench_setup(comm, n=args.spmm_n, density=args.spmm_density, cols=128,
-                                             seed=args.seed)
+                                             seed=args.seed, method=args.spmm_method)
     return step, flops, extra, cfg
 
 
@@ -255,6 +283,8 @@ def main() -> None:
     ap.add_argument("--matrix-density", dest="density", type=float, default=1e-4)
     ap.add_argument("--spmm-n", type=int, default=65536)
     ap.add_argument("--spmm-density", type=float, default=1e-3)
+    ap.add_argument("--spmm-method", default="auto", choices=["auto", "mfma", "sweep", "rowwise"],
+                    help="spmm workload: executor (auto: the fastest measured on the real operands)")
     ap.add_argument("--scale", type=int, default=24, help="R-MAT scale (BASELINE config 5: 24)")
     ap.add_argument("--rmat-stream", default="auto", choices=["auto", "on", "off"],
                     help="produce C in consumed row panels (auto: when its product bound does not fit)")
@@ -265,6 +295,8 @@ def main() -> None:
     ap.add_argument("--chain-preset", default="medium", choices=["small", "medium", "large"],
                     help="chain workload: report preset (one folder, any N: strong scaling)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--graph", default="on", choices=["on", "off"],
+                    help="spgemm / spgemm64k on one GPU: replay the product from a captured HIP graph")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (gloo on GPUs: rehearse several ranks on one card)")
     args = ap.parse_args()
@@ -330,17 +362,63 @@ def main() -> None:
         out = step()
         del out
         progress("warm-up", i)
+    from spmm_amd.models.spgemm import GATHER_STATS
+
+    stall = os.environ.get("SPMM_BENCH_STALL_RANK")   # fault injection (tests): this rank stops answering
+    if stall not in (None, "") and int(stall) == comm.rank:
+        time.sleep(float(os.environ.get("SPMM_BENCH_STALL_S", "600")))
+    GATHER_STATS.reset(enabled=True)
+    marks = []   # per-step boundaries on this rank: device events (no host sync) or host clock
+
+    def mark():
+        if comm.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            marks.append(ev)
+        else:
+            marks.append(time.perf_counter())
+
     _sync_barrier(comm)
     t0 = time.perf_counter()
+    mark()
     for i in range(args.steps):
         out = None
         out = step()
+        mark()
         progress("step", i)
     del out
     _sync_barrier(comm)
-    dt = comm.allreduce_max(time.perf_counter() - t0)
+    t_local = time.perf_counter() - t0
+    dt = comm.allreduce_max(t_local)
+    GATHER_STATS.enabled = False
     ms = dt / args.steps * 1e3
     value = flops * args.steps / dt / 1e9
+    # per-rank observability (after the timed region): this rank's step times
+    # (device timeline between step boundaries), wall time, and the operand
+    # all-gather's bytes and issue-to-ready time per step
+    if comm.device.type == "cuda":
+        steps_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
+    else:
+        steps_ms = [(marks[i + 1] - marks[i]) * 1e3 for i in range(args.steps)]
+    if hasattr(step, "verify"):
+        extra.update(step.verify())
+    g_bytes, g_ms = GATHER_STATS.summary()
+    mine = torch.tensor([sum(steps_ms) / len(steps_ms), min(steps_ms), max(steps_ms), t_local * 1e3 / args.steps,
+                         g_ms / args.steps, g_bytes / args.steps], dtype=torch.float64)
+    if comm.is_dist:
+        wire = torch.device("cuda", comm.device.index) if comm.device_collectives else torch.device("cpu")
+        per_rank = comm.all_gather(mine.to(wire)).view(comm.world, -1).cpu()
+    else:
+        per_rank = mine.view(1, -1)
+    import torch.distributed as dist
+
+    col = lambda j: [round(float(x), 3) for x in per_rank[:, j]]  # noqa: E731
+    observ = dict(
+        torch_dist_world=dist.get_world_size() if dist.is_initialized() else 1,
+        rank_step_ms=dict(min=round(float(per_rank[:, 0].min()), 3), mean=round(float(per_rank[:, 0].mean()), 3),
+                          max=round(float(per_rank[:, 0].max()), 3)),
+        per_rank=dict(step_ms_mean=col(0), step_ms_min=col(1), step_ms_max=col(2), wall_ms_per_step=col(3),
+                      allgather_ms_per_step=col(4), allgather_bytes_per_step=[int(x) for x in per_rank[:, 5]]))
     vs = None
     unit = "GFLOP/s"
     metric = METRIC
@@ -351,7 +429,7 @@ def main() -> None:
         if hasattr(step, "cleanup"):
             step.cleanup()
     elif args.workload == "spmm":
-        metric = "GFLOP/s (whole node), CSR x dense 128-col SpMM, bf16 MFMA"
+        metric = f"GFLOP/s (whole node), CSR x dense 128-col SpMM, bf16, {extra['spmm_kernel']}"
     if comm.rank == 0:
         rec = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": comm.world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
@@ -360,7 +438,7 @@ def main() -> None:
                    "bf16" if args.workload == "spmm" else "uint64"),
                "data": "synthetic (device RNG, random values)", "config": cfg, "flops_per_step": flops,
                "backend": comm.backend or "single-process",
-               "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu", **extra}
+               "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu", **extra, **observ}
         print(json.dumps(rec), flush=True)
     comm.close()
 

@@ -37,6 +37,43 @@ __device__ __forceinline__ uint64_t ref_mac(uint64_t acc, uint64_t a, uint64_t b
   return (s == ~0ull) ? 0ull : s;
 }
 
+// Speculative form of ref_mac: the plain wrapping acc + a*b in three VALU ops
+// (v_mad_u64_u32 folds the low product and the 64-bit add; the two cross
+// terms land in the high word), plus a conservative flag for the two events
+// where the reference's collapse could differ from wrapping arithmetic:
+// t = a*b == 2^64-1 needs t_lo == 0xffffffff (t_lo = r_lo - acc_lo), and
+// s = acc + t == 2^64-1 needs s_lo == 0xffffffff.  When no lane of a tile
+// ever raises the flag the wrapped result IS the reference's (no collapse
+// fired); otherwise the caller recomputes the tile with ref_mac.
+// v_mad_u64_u32: x*y + z (64-bit addend, 64-bit result; the carry-out is dropped)
+__device__ __forceinline__ uint64_t mad_u64_u32(uint32_t x, uint32_t y, uint64_t z) {
+  uint64_t r, carry;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
+
+// Returns s = acc + a*b (wrapping); ``m`` accumulates max(s_lo, t_lo) so the
+// caller tests a whole group of MACs with one compare (max == 0xffffffff iff
+// some s_lo or t_lo was all-ones).
+__device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t b, uint32_t& m) {
+  const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+  // four VALU ops: r = alo*blo + acc;  c = alo*bhi;  x = ahi*blo + c (its low
+  // word = the cross terms mod 2^32);  s_hi = r_hi + x_lo (32-bit add into the
+  // high half; opaque so the compiler does not rebuild it as a 64-bit add)
+  uint64_t r, c, x, k0, k1, k2;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(k0) : "v"(alo), "v"(blo), "v"(acc));
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(c), "=s"(k1) : "v"(alo), "v"(bhi));
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(x), "=s"(k2) : "v"(ahi), "v"(blo), "v"(c));
+  uint32_t hi;
+  asm("v_add_u32 %0, %1, %2" : "=v"(hi) : "v"((uint32_t)(r >> 32)), "v"((uint32_t)x));
+  const uint32_t lo = (uint32_t)r;
+  const uint64_t s = ((uint64_t)hi << 32) | lo;
+  const uint32_t tlo = lo - (uint32_t)acc;
+  const uint32_t q = lo > tlo ? lo : tlo;
+  m = m > q ? m : q;   // (one v_max3_u32)
+  return s;
+}
+
 // Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): consecutive logical ids land on the same
 // XCD so neighbouring work shares that XCD's L2.  Speed only, never correctness.

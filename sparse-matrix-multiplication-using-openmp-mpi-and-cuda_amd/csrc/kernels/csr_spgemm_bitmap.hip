@@ -41,49 +41,17 @@
 #define SPMM_BM_SWEEP_G 2
 #endif
 
-#ifndef SPMM_BM_ILV   // per-unit fast kernel (W <= 2^15): bitmap and rank prefixes interleaved per 32-bit word
-#define SPMM_BM_ILV 0   // ({bits, prefix} pairs: one 8-byte LDS read per rank lookup instead of two reads)
-#endif
 #ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
 #define SPMM_BM_P2_G 2   // 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586 (fewer empty rounds past the chunk count); 7 spills
 #endif
-#ifndef SPMM_BM_SKIP_ROUNDS   // numeric pass 2: skip register rounds past the unit's chunk count (uniform)
-#define SPMM_BM_SKIP_ROUNDS 1
-#endif
 
-#ifndef SPMM_BM_ROWS_WPS   // 512-thread row kernel: waves per SIMD its registers are sized for
-#define SPMM_BM_ROWS_WPS 6
-#endif
 
-#ifndef SPMM_BM_P1_SPLIT   // row-major numeric pass 1: straight-line bodies of RR/2, RR-2, RR rounds by the unit's need
-#define SPMM_BM_P1_SPLIT 0
-#endif
 
-#ifndef SPMM_BM_PREFETCH   // row kernels: L2 prefetch of each entry's next-unit B segment (first + last line)
-#define SPMM_BM_PREFETCH 0
-#endif
 
-#ifndef SPMM_BM_FUSED_RC   // fused row kernel: column loads in flight per thread in the count phase
-#define SPMM_BM_FUSED_RC 8
-#endif
 
-#ifndef SPMM_BM_DESC4   // row-major numeric: 16-byte chunk descriptors {B index, lanes, a(i, j), -}, padded to
-#define SPMM_BM_DESC4 0   // whole rounds (one LDS read per round, no TC clamps) instead of uint2 + float arrays
-#endif
 
-#ifndef SPMM_BM_COUNT_LGV   // row-major count: log2 columns per lane and load (1: one 8-byte load covers two
-#define SPMM_BM_COUNT_LGV 0   // consecutive products of a chunk: half the load instructions / memory requests)
-#endif
 
-#ifndef SPMM_BM_NT_STORE   // numeric write-out: non-temporal stores of C (C does not displace B in L2 / MALL;
-#define SPMM_BM_NT_STORE 1   // 1M step 76.55 -> 75.41 ms, 64k 1.755 -> 1.697 ms, same box)
-#endif
-
-#if SPMM_BM_NT_STORE
 #define BM_OUT(ptr, val) __builtin_nontemporal_store((val), (ptr))
-#else
-#define BM_OUT(ptr, val) (*(ptr) = (val))
-#endif
 
 namespace {
 
@@ -289,8 +257,6 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   constexpr int NW = NT / 64;
   constexpr bool VALUES = MODE != 0;
   constexpr int NWORD = Gm::NWORD, WPW = Gm::WPW, WPT = Gm::WPT;
-  // ILV: 32-bit bitmap word k at bm32[2k], its exclusive rank prefix at bm32[2k + 1]
-  constexpr bool ILV = SPMM_BM_ILV && MODE == 1 && LGW <= 15 && !DET;
   constexpr int RR = MODE == 1 ? R : (MODE == 0 ? 16 : 8);   // rounds of loads in flight per block
   // deterministic fix-up list: the fast kernel defers a unit that overflows
   // it to the reload kernel, whose list is larger (it has one CU's LDS)
@@ -301,8 +267,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   // LDS.  bm: the window's column bitmap.  pre16: exclusive rank prefix of
   // every 64-bit word.  items: (column, value) of every output slot.
   // desc: chunk descriptors {first B index, valid lanes, a(i, j) bits}.
-  __shared__ __attribute__((aligned(16))) unsigned long long bm[ILV ? 2 * NWORD : NWORD];
-  __shared__ __attribute__((aligned(16))) uint16_t pre16[VALUES && !ILV ? NWORD : 1];
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint16_t pre16[VALUES ? NWORD : 1];
   __shared__ __attribute__((aligned(16))) unsigned long long items[VALUES ? PCAP : 1];
   using Desc = typename std::conditional<VALUES, uint4, uint2>::type;
   __shared__ __attribute__((aligned(16))) Desc desc[CCAP];
@@ -337,7 +303,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 
   // bitmap clear: 16-byte stores, consecutive lanes on consecutive slots (conflict-free)
   auto clear_bm = [&]() {
-    for (int i = tid; i < (ILV ? 2 : 1) * Gm::NCLR; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < Gm::NCLR; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
   };
   clear_bm();
   if (tid < NSUB) scnt[tid] = 0;
@@ -510,7 +476,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 #pragma unroll
       for (int d = 0; d < RR; ++d) {
         old[d] = 0u;
-        if (c[d] >= 0) old[d] = atomicOr(bm32 + ((c[d] >> 5) << (ILV ? 1 : 0)), 1u << (c[d] & 31));
+        if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
       }
 #pragma unroll
       for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
@@ -659,9 +625,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       // ---- rank prefix per 64-bit word: wave w owns words [w*WPW, (w+1)*WPW)
       // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
       // wave scan of their sum, 16-bit prefixes stored SG at a time)
-      constexpr int SG = (!ILV && SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+      constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
       constexpr bool PAIRS = SG > 1;
-      uint4* const bm4 = reinterpret_cast<uint4*>(bm);   // ILV: {bits lo, prefix lo, bits hi, prefix hi} per 64-bit word
       int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
       int wtot = 0;
       if constexpr (PAIRS) {
@@ -686,24 +651,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
           wtot += __builtin_amdgcn_readlane(incl, 63);
         }
       } else {
-        int lo[ILV ? WPT : 1];
 #pragma unroll
         for (int kk = 0; kk < WPT; ++kk) {
-          int cnt;
-          if constexpr (ILV) {
-            const uint4 q = bm4[w * WPW + kk * 64 + lane];
-            lo[kk] = __popc(q.x);
-            cnt = lo[kk] + __popc(q.z);
-          } else {
-            cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
-          }
+          const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
           const int incl = bm_wave_incl(cnt);
           run[kk] = wtot + incl - cnt;
           wtot += __builtin_amdgcn_readlane(incl, 63);
-        }
-        if constexpr (ILV) {   // (the prefixes are written after the block totals, below)
-#pragma unroll
-          for (int kk = 0; kk < WPT; ++kk) run[kk] |= lo[kk] << 16;
         }
       }
       const int any_dup = sdup;
@@ -737,14 +690,6 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
-      } else if constexpr (ILV) {
-#pragma unroll
-        for (int kk = 0; kk < WPT; ++kk) {
-          const uint32_t g = (uint32_t)(base + (run[kk] & 0xffff));
-          uint32_t* q = reinterpret_cast<uint32_t*>(&bm4[w * WPW + kk * 64 + lane]);
-          q[1] = g;
-          q[3] = g + ((uint32_t)run[kk] >> 16);
-        }
       } else {
 #pragma unroll
         for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
@@ -755,22 +700,15 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       // ---- pass 2: rank -> slot; owners store (column, value), duplicates
       // add their value after a barrier (bit set by an earlier product)
       auto rank = [&](int cc) {
-        if constexpr (ILV) {
-          const uint2 e = reinterpret_cast<const uint2*>(bm)[cc >> 5];
-          return (int)e.y + __popc(e.x & ((1u << (cc & 31)) - 1u));
-        } else {
-          const int wd = cc >> 6;
-          return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
-        }
+        const int wd = cc >> 6;
+        return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
       };
       if constexpr (MODE == 1) {
         // ranks of P2G rounds at a time (their LDS reads in flight together)
         constexpr int P2G = SPMM_BM_P2_G;
 #pragma unroll
         for (int d0 = 0; d0 < RR; d0 += P2G) {
-#if SPMM_BM_SKIP_ROUNDS
           if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
-#endif
           int r[P2G];
 #pragma unroll
           for (int dd = 0; dd < P2G && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
@@ -899,17 +837,22 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 // loads, when every one of them has landed (a copy of a register whose load
 // is still in flight would stall the wave for the whole memory latency).
 // Per window the staging is register arithmetic + one scan.
-// ws8[j] = {first index of B row j, 16-bit lengths of windows 0..7} (uint4 x 2).
+// ws8[j] = {first index of B row j, 16-bit lengths of windows 0..7} (uint4 x 2);
+// ws8[2j + 1].y = first index of row j in the padded pair array (below).
+//
+// Padded B (``Bcv`` with ``pad`` = 1): the numeric kernel's (column, value)
+// pairs with every (row, window) segment starting on a 128-byte line (16
+// pairs), so a segment of L pairs touches ceil(L / 16) lines instead of ~1 +
+// 8L / 128: random segment gathers run at a fixed rate of LINES, and the
+// 1M config's ~13-pair segments gather 1.39x faster aligned (4.64 vs 3.35
+// TB/s useful, tools/probes/seg_gather.hip, profiles/r4/seg_gather.md).
 struct BmRowArgs {
   BmArgs a;
   const uint4* ws8;
-  int q0, q1;   // windows [q0, q1) of every row (window-major passes: the B column slice of a
-                // pass stays in the MALL while every row's products in it are formed)
-  // fused kernel only (count phase + row look-back, no count kernel):
-  int64_t* uoff_out;           // [m * nwin + 1] unit offsets, written by the kernel (for the reload kernel)
-  unsigned long long* rstat;   // [m] per-row look-back words, zeroed: flag (2 bits) | value (62 bits)
-  uint32_t* ticket;            // zeroed row ticket counter
+  int pad;   // numeric: Bcv is the padded pair array
 };
+constexpr int kPadLg = 4;    // padded segments: multiples of 2^4 pairs (128 bytes)
+constexpr int kPadCLg = 5;   // padded count segments (column groups of a count unit): 2^5 columns (128 bytes)
 
 // First B index of window q0 inside this entry's B row: the row start plus
 // the packed 16-bit lengths of windows 0 .. q0-1.
@@ -922,71 +865,24 @@ __device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb
   return b;
 }
 
-// ---- fused mode: row look-back ----------------------------------------------
-// A fused workgroup counts its row (every window) before forming any product,
-// publishes the row's nnz as an AGGREGATE, and resolves its start in C
-// (sum of all earlier rows) only when its first window is about to be
-// written: by then the earlier rows, which took smaller tickets and hence
-// started earlier, have almost always published at least their aggregate.
-// One wave reads the 64 nearest predecessors' words per memory round trip
-// and sums back to the first INCLUSIVE prefix, then publishes its own.
-constexpr unsigned long long kRsAgg = 1ull << 62, kRsInc = 2ull << 62, kRsVal = (1ull << 62) - 1;
-
-__device__ __forceinline__ int64_t bm_row_lookback(unsigned long long* rstat, int64_t row, int64_t count, int lane) {
-  int64_t pre = 0;
-  for (int64_t end = row; end > 0;) {
-    const int64_t j = end - 1 - lane;   // lane 0 = nearest predecessor
-    const unsigned long long st =
-        j >= 0 ? __hip_atomic_load(&rstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kRsInc;
-    const unsigned f = (unsigned)(st >> 62);
-    const unsigned long long inc = __ballot(f == 2), notready = __ballot(f == 0);
-    const int first = inc ? __ffsll((long long)inc) - 1 : 64;
-    const unsigned long long need = first >= 63 ? ~0ull : ((2ull << first) - 1);   // lanes 0..first
-    if (notready & need) {
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    int64_t v = lane <= first ? (int64_t)(st & kRsVal) : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    pre += v;
-    if (first < 64) break;
-    end -= 64;
-  }
-  if (lane == 0)
-    __hip_atomic_store(&rstat[row], kRsInc | (unsigned long long)(pre + count), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  return pre;
-}
-
-template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET, bool FUSED = false>
-__global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_bm_rows(BmRowArgs ra) {
+template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET>
+__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int RR = R;
-  constexpr int LCAP = DET ? (SPMM_BM_DESC4 ? 184 : 256) : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
+  constexpr int LCAP = DET ? 256 : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
   static_assert(WPW % 64 == 0 && PCAP < 65536, "geometry");
   static_assert(!DET || (CCAP << 6) <= (1 << kKeyBits), "DET keys fit 17 bits");
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
   __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
-#if SPMM_BM_DESC4
-  static_assert(!SPMM_BM_P1_SPLIT, "DESC4 with the split pass 1 is not implemented");
-  __shared__ __attribute__((aligned(16))) uint4 desc4[CCAP];   // chunk: {first B index, valid lanes, a(i, j) bits, 0}
-  uint4* const desc = desc4;                                   // (fused count phase: .x, .y only)
-#else
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];   // chunk: {first B index, valid lanes}
   __shared__ float dval[CCAP];                                 //        a(i, j)
-#endif
   __shared__ __attribute__((aligned(8))) uint2 dlist[LCAP];
   __shared__ int wsum[2 * NW];
   __shared__ int sdup, sfix, snl;
-  __shared__ int csum[FUSED ? NW : 1];          // fused count phase: per-wave popcounts
-  __shared__ uint32_t s_tk[2];                  // fused: row tickets (double-buffered by row parity)
-  __shared__ int64_t s_rs;                      // fused: resolved start of the row in C
-  __shared__ int s_cnt[8], s_cex[8];            // fused: nnz of each window of the row, exclusive prefix
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1016,15 +912,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
   const int64_t m = p.m;
 
-  // row pipeline registers.  Rows: static (me, me + NG, ...) or, fused,
-  // from a ticket counter (the look-back needs every earlier row to be owned
-  // by a running workgroup); row1 / row2 = the next two rows of this workgroup
+  // row pipeline registers: rows me, me + NG, ...; row1 / row2 = the next two
+  // rows of this workgroup
   int64_t row = me, row1 = me + NG, row2 = me + 2 * NG;
-  if constexpr (FUSED) {
-    if (tid == 0) s_tk[1] = atomicAdd(ra.ticket, 1u);
-    __syncthreads();
-    row = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)s_tk[1]);   // (uniform: scalar registers)
-  }
   int ca0 = 0, cna = 0;           // its A row (scalars after the copy)
   float cav = 0.f;                // its A value (thread = entry)
   uint4 cwa = make_uint4(0, 0, 0, 0);   // its packed window bounds
@@ -1058,11 +948,11 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       const int na = __builtin_amdgcn_readfirstlane(b) - __builtin_amdgcn_readfirstlane(a);
       if (tid < na) {
         nwa = ra.ws8[2 * (int64_t)njj];
-        nwb = ra.ws8[2 * (int64_t)njj + 1].x;
+        const uint4 x = ra.ws8[2 * (int64_t)njj + 1];
+        nwb = x.x;
+        if (ra.pad) nwa.x = x.y;   // the segment starts in the padded pair array
       }
-      if constexpr (!FUSED) {
-        if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
-      }
+      if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
     }
   };
   auto take_next = [&]() {   // next row -> current row (call only when its loads have landed)
@@ -1079,151 +969,26 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
   ld_arp(row, n1a, n1b);
   ld_entries(row, n1a, n1b);
   ld_bounds(row, n1a, n1b);
-  if constexpr (!FUSED) ld_arp(row1, n2a, n2b);
+  ld_arp(row1, n2a, n2b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   take_next();
   __syncthreads();
 
   int c[RR];
   float v[RR];
-  uint32_t pf0 = 0, pf1 = 0;   // prefetch sinks (SPMM_BM_PREFETCH)
-  int par = 0;                 // fused: ticket buffer of this row
   while (row < m) {
     const int na = cna;
-    const int q0 = ra.q0, q1 = ra.q1;
-    if constexpr (!FUSED) {
-      row1 = row + NG;
-      row2 = row + 2 * NG;
-    }
-    // ---- fused: count phase (every window's exact nnz, B columns only) ----
-    // (ccnt: lane q = nnz of window q, cex its exclusive prefix: into s_cnt / s_cex; rtot the row's nnz)
-    int64_t rtot = 0, rowstart = 0;
-    bool resolved = false;
-    if constexpr (FUSED) {
-      constexpr int RC = SPMM_BM_FUSED_RC;   // count-phase B loads in flight per thread
-      if (na > NT && tid == 0) atomicOr(p.err, 1);         // (host gate: A rows <= NT) -> host fallback
-      int ccnt = 0;
-      uint32_t cbq = bm_window_start(cwa, cwb, 0);
-      for (int q = 0; q < nwin; ++q) {
-        const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
-        int len = 0, nch = 0;
-        if (tid < na && tid < NT) {
-          len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
-          nch = (len + Gl - 1) >> lg;
-        }
-        const uint32_t b0 = cbq;
-        cbq += (uint32_t)len;
-        int pre, plen, TC, P;
-        bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-        if (P == 0) {   // uniform: nothing to OR
-          __syncthreads();   // wsum reads done before the next scan
-          continue;
-        }
-        const int clo = q << LGW;
-        for (int cb = 0; cb < TC; cb += CCAP) {
-          const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
-          const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
-          for (int kk = k0; kk < k1; ++kk) {
-            const int rem = len - (kk << lg);
-            desc[pre + kk - cb].x = b0 + ((uint32_t)kk << lg);
-            desc[pre + kk - cb].y = (uint32_t)(rem < Gl ? rem : Gl);
-          }
-          __syncthreads();
-          const int nr = (TCb + ngrp - 1) / ngrp;
-          for (int i0 = 0; i0 < nr; i0 += RC) {
-            uint2 ds[RC];
-#pragma unroll
-            for (int d = 0; d < RC; ++d) {
-              const int t = gid + (i0 + d) * ngrp;
-              ds[d] = make_uint2(desc[t < TCb ? t : TCb - 1].x, desc[t < TCb ? t : TCb - 1].y);
-            }
-            int x[RC];
-            uint32_t okm = 0;
-#pragma unroll
-            for (int d = 0; d < RC; ++d) {
-              const int t = gid + (i0 + d) * ngrp;
-              const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
-              okm |= (ok ? 1u : 0u) << d;
-              const uint32_t f = ds[d].x + (ok ? (uint32_t)gl : 0u);
-              x[d] = 0;
-              if (i0 + d < nr) {   // wave-uniform
-                // (from the interleaved pairs when the numeric phase reads them:
-                // the same lines, which are then warm for pass 1)
-                if constexpr (CV) x[d] = (int)p.Bcv[f].x;
-                else x[d] = p.Bci[f];
-              }
-            }
-#pragma unroll
-            for (int d = 0; d < RC; ++d) {
-              if ((okm >> d) & 1u) {
-                const int cc = x[d] - clo;
-                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
-              }
-            }
-          }
-          __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
-        }
-        // popcount of this wave's bitmap words, cleared as they are read
-        int cnt = 0;
-#pragma unroll
-        for (int kk = 0; kk < WPT; ++kk) {
-          const int wd = w * WPW + kk * 64 + lane;
-          cnt += __popcll(bm[wd]);
-          bm[wd] = 0ull;
-        }
-        cnt = bm_wave_sum(cnt);
-        if (lane == 0) csum[w] = cnt;
-        __syncthreads();
-        int t = 0;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) t += csum[i];
-        if (lane == q) ccnt = t;
+    row1 = row + NG;
+    row2 = row + 2 * NG;
+    uint32_t bq = cwa.x;   // first B index of window q of this thread's entry
+    for (int q = 0; q < nwin; ++q) {
+      const bool last = q == nwin - 1;
+      // ---- row pipeline hooks ------------------------------------------
+      if (q == 0) {
+        ld_entries(row1, n1a, n1b);
+        ld_arp(row2, n2a, n2b);
       }
-      const int incl = bm_wave_incl(ccnt);
-      if (w == 0 && lane < 8) {   // (read below at least one barrier)
-        s_cnt[lane] = ccnt;
-        s_cex[lane] = incl - ccnt;
-      }
-      rtot = (int64_t)(uint32_t)__builtin_amdgcn_readlane(incl, 63);
-      if (tid == 0)
-        __hip_atomic_store(&ra.rstat[row], kRsAgg | (unsigned long long)rtot, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      BM_STAMP(5);   // (fused: the count phase, stamp slot of the count kernel's ORs)
-    }
-    // fused: the row's start in C, by wave 0 before a barrier (issue) and read
-    // by every thread after it (finish); also the unit offsets for the reload kernel
-    auto resolve_issue = [&]() {
-      if (w == 0) {
-        const int64_t s0 = bm_row_lookback(ra.rstat, row, rtot, lane);
-        if (lane == 0) s_rs = s0;
-      }
-    };
-    auto resolve_finish = [&]() {
-      rowstart = bm_rfl64(s_rs);
-      resolved = true;
-      if (w == 0 && lane < nwin) ra.uoff_out[row * nwin + lane] = rowstart + (int64_t)(uint32_t)s_cex[lane];
-      if (w == 0 && lane == 0 && row == m - 1) ra.uoff_out[m * nwin] = rowstart + rtot;
-    };
-    uint32_t bq = bm_window_start(cwa, cwb, q0);   // first B index of window q of this thread's entry
-    for (int q = q0; q < q1; ++q) {
-      const bool last = q == q1 - 1;
-#if SPMM_BM_PREFETCH
-      asm volatile("" ::"v"(pf0), "v"(pf1));   // the previous unit's prefetches: a use, so their registers stay reserved
-#endif
-      // ---- pipeline hooks (every path) ---------------------------------
-      if constexpr (FUSED) {
-        // the next row's ticket only now (a ticket taken early but started
-        // late would hold up the look-back of every later row); its A row is
-        // staged during this window: Arp after the scan, entries after pass 1,
-        // bounds before the write-out, into the current registers at the row end
-        if (last && tid == 0) s_tk[par] = atomicAdd(ra.ticket, 1u);
-      } else {
-        if (q == q0) {
-          ld_entries(row1, n1a, n1b);
-          ld_arp(row2, n2a, n2b);
-        }
-        if (last) ld_bounds(row1, n1a, n1b);
-      }
+      if (last) ld_bounds(row1, n1a, n1b);
       // ---- staging from registers ---------------------------------------
       const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
       int len = 0, nch = 0;
@@ -1232,44 +997,16 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
         nch = (len + Gl - 1) >> lg;
       }
       const uint32_t b0 = bq;
-      bq += (uint32_t)len;
-#if SPMM_BM_PREFETCH
-      // the next window's segment of this entry into L2 (its first and last
-      // lines): the next unit's B loads then hit L2 instead of HBM
-      if (!last && tid < na && tid < NT) {
-        const int qn = q + 1;
-        const uint32_t wn = qn < 2 ? cwa.y : qn < 4 ? cwa.z : qn < 6 ? cwa.w : cwb;
-        const uint32_t ln = (wn >> (16 * (qn & 1))) & 0xffffu;
-        if (ln) {
-          if constexpr (CV) {
-            pf0 = p.Bcv[bq].x;
-            pf1 = p.Bcv[bq + ln - 1].x;
-          } else {
-            pf0 = (uint32_t)p.Bci[bq] ^ __float_as_uint(p.Bv[bq]);
-            pf1 = (uint32_t)p.Bci[bq + ln - 1] ^ __float_as_uint(p.Bv[bq + ln - 1]);
-          }
-        }
-      }
-#endif
+      bq += ra.pad ? (uint32_t)(((len + (1 << kPadLg) - 1) >> kPadLg) << kPadLg) : (uint32_t)len;
       const int clo = q << LGW;
       const int u = (int)(row * nwin + q);
-      int64_t off = 0;
-      int want = 0;
-      if constexpr (!FUSED) {   // (fused: both at the write-out, once the row's start is resolved)
-        // (both halves zero-extended: offsets pass 2^31 on the 1M product)
-        off = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)cuo >> 32), q)
-                         << 32) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cuo, q));
-        want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
-      }
+      // (both halves zero-extended: offsets pass 2^31 on the 1M product)
+      const int64_t off =
+          (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)cuo >> 32), q) << 32) |
+                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cuo, q));
+      const int want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
       int pre, plen, TC, P;
       bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-      if constexpr (FUSED) {
-        if (last) {
-          row1 = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)s_tk[par]);
-          ld_arp(row1, n1a, n1b);
-        }
-      }
       const bool too_big = na > NT || P > PCAP || TC > CCAP || TC > R * ngrp;
       if (P == 0 || too_big) {   // uniform
         if (too_big && P != 0 && tid == 0) {
@@ -1277,142 +1014,19 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
           if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
           else atomicOr(p.err, 4);
         }
-        if constexpr (FUSED) {
-          if (last) {   // (rare: the next row's chain back to back)
-            ld_entries(row1, n1a, n1b);
-            ld_bounds(row1, n1a, n1b);
-          }
-        } else if (last) {
-          take_next();   // (rare: waits for the next row's loads here)
-        }
+        if (last) take_next();   // (rare: waits for the next row's loads here)
         __syncthreads();         // wsum reads done before the next scan
         continue;
       }
-#if SPMM_BM_DESC4
-      for (int kk = 0; kk < nch; ++kk) {
-        const int rem = len - (kk << lg);
-        desc4[pre + kk] = make_uint4(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl), __float_as_uint(cav), 0u);
-      }
-      {   // the last round's chunks past TC: no valid lane
-        const int pad_end = ((TC + ngrp - 1) / ngrp) * ngrp;
-        if (TC + tid < pad_end) desc4[TC + tid] = make_uint4(0u, 0u, 0u, 0u);
-      }
-#else
       for (int kk = 0; kk < nch; ++kk) {
         const int rem = len - (kk << lg);
         desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
         dval[pre + kk] = cav;
       }
-#endif
       __syncthreads();
       BM_STAMP(0);
       // ---- pass 1 ----------------------------------------------------------
-      // (N = rounds compiled in: with SPMM_BM_P1_SPLIT the unit's round count
-      // picks a straight-line body of RR / 2, RR - 2 or RR rounds, so unused
-      // rounds cost no VALU; rounds >= N hold no product)
       const int nr = (TC + ngrp - 1) / ngrp;
-#if SPMM_BM_P1_SPLIT
-      auto pass1 = [&](auto NRc) -> uint32_t {
-        constexpr int N = decltype(NRc)::value;
-        uint2 ds[N];
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-          const int t = gid + d * ngrp;
-          ds[d] = desc[t < TC ? t : TC - 1];
-        }
-        uint32_t f[N];
-        uint32_t okm = 0;
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-          const int t = gid + d * ngrp;
-          const bool ok = (t < TC) & ((uint32_t)gl < ds[d].y);
-          okm |= (ok ? 1u : 0u) << d;
-          f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
-        }
-        int x[N];
-        float b[N];
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-          x[d] = 0;
-          b[d] = 0.f;
-          if (d < nr) {   // wave-uniform
-            if constexpr (CV) {   // one 8-byte load: a chunk's products share cache lines
-              const uint2 e = p.Bcv[f[d]];
-              x[d] = (int)e.x;
-              b[d] = __uint_as_float(e.y);
-            } else {
-              x[d] = p.Bci[f[d]];
-              b[d] = p.Bv[f[d]];
-            }
-          }
-        }
-        // A values while the B loads are in flight
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-          const int t = gid + d * ngrp;
-          v[d] = dval[t < TC ? t : TC - 1];
-        }
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-          c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
-          v[d] *= b[d];
-        }
-#pragma unroll
-        for (int d = N; d < RR; ++d) {
-          c[d] = -1;
-          v[d] = 0.f;
-        }
-        uint32_t dm = 0;
-        uint32_t old[N];
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
-          old[d] = 0u;
-          if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
-        }
-#pragma unroll
-        for (int d = 0; d < N; ++d) dm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
-        return dm;
-      };
-      const uint32_t dupm = nr <= RR / 2 ? pass1(std::integral_constant<int, RR / 2>{})
-                            : nr <= RR - 2 ? pass1(std::integral_constant<int, RR - 2>{})
-                                           : pass1(std::integral_constant<int, RR>{});
-#elif SPMM_BM_DESC4
-      {
-        uint4 ds[RR];
-#pragma unroll
-        for (int d = 0; d < RR; ++d) ds[d] = desc4[gid + d * ngrp];   // (rounds >= nr: stale, masked below)
-        uint32_t f[RR];
-        uint32_t okm = 0;
-#pragma unroll
-        for (int d = 0; d < RR; ++d) {
-          const bool ok = (d < nr) & ((uint32_t)gl < ds[d].y);
-          okm |= (ok ? 1u : 0u) << d;
-          f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
-        }
-        int x[RR];
-        float b[RR];
-#pragma unroll
-        for (int d = 0; d < RR; ++d) {
-          x[d] = 0;
-          b[d] = 0.f;
-          if (d < nr) {   // wave-uniform
-            if constexpr (CV) {
-              const uint2 e = p.Bcv[f[d]];
-              x[d] = (int)e.x;
-              b[d] = __uint_as_float(e.y);
-            } else {
-              x[d] = p.Bci[f[d]];
-              b[d] = p.Bv[f[d]];
-            }
-          }
-        }
-#pragma unroll
-        for (int d = 0; d < RR; ++d) {
-          c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
-          v[d] = __uint_as_float(ds[d].z) * b[d];
-        }
-      }
-#else
       {
         uint2 ds[RR];
 #pragma unroll
@@ -1458,8 +1072,6 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
           v[d] *= b[d];
         }
       }
-#endif
-#if !SPMM_BM_P1_SPLIT
       uint32_t dupm = 0;
       {
         uint32_t old[RR];
@@ -1471,28 +1083,11 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
 #pragma unroll
         for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
       }
-#endif
       // this unit's B loads have landed, and with them every older load:
       // the next row's registers are ready to be taken
-      if constexpr (FUSED) {
-        if (last) ld_entries(row1, n1a, n1b);
-      } else if (last) {
-        take_next();
-      }
+      if (last) take_next();
       if (dupm) sdup = 1;
-      if constexpr (FUSED) {
-        if (!resolved) {   // uniform
-          BM_STAMP(1);
-          resolve_issue();
-        }
-      }
       __syncthreads();
-      if constexpr (FUSED) {
-        if (!resolved) {
-          resolve_finish();
-          BM_STAMP(6);   // (fused: the look-back, stamp slot of the count kernel's popcount)
-        }
-      }
       BM_STAMP(1);
       // ---- rank prefix per 64-bit word ---------------------------------
       // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
@@ -1576,9 +1171,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       };
 #pragma unroll
       for (int d0 = 0; d0 < RR; d0 += 4) {
-#if SPMM_BM_SKIP_ROUNDS
         if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
-#endif
         int r[4];
 #pragma unroll
         for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
@@ -1640,11 +1233,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       }
       BM_STAMP(3);
       // ---- write-out -----------------------------------------------------
-      if constexpr (FUSED) {
-        if (last) ld_bounds(row1, n1a, n1b);
-        want = __builtin_amdgcn_readfirstlane(s_cnt[q]);
-        off = rowstart + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_cex[q]);
-      }
+      
       int lim = skip ? 0 : total;
       if (!skip && (want != total || off < 0 || off + total > p.cap)) {   // never write outside the unit or C
         if (tid == 0) atomicOr(p.err, 2);
@@ -1660,366 +1249,10 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : SPMM_BM_ROWS_WPS) void spgemm_b
       BM_STAMP(4);
       BM_STAMP_UNIT();
     }
-    if constexpr (FUSED) {
-      if (!resolved) {   // uniform: no window of the row reached pass 1 (empty or deferred windows)
-        resolve_issue();
-        __syncthreads();
-        resolve_finish();
-      }
-      take_next();   // (the next row's bounds: loaded during the last write-out)
-      row = row1;
-      par ^= 1;
-    } else {
-      row += NG;
-    }
+    row += NG;
+  
   }
   BM_STAMP_FLUSH();
-}
-
-// ---- software-pipelined row-major numeric kernel (4 <= nwin <= 8) ----------
-// The row-major kernel with the B loads of unit k+1 in flight during unit k:
-//   1. issue unit k's B values; OR its columns (loaded one unit ago)   (barrier)
-//   2. unit k+1's descriptor scan; unit k's wave-local rank prefixes    (barrier)
-//   3. unit k+1's descriptors; unit k's pass 2 (slot owners)           (barrier)
-//   4. ISSUE unit k+1's B columns; unit k's duplicate adds            (barrier)
-//   5. unit k's C slots out (a FIXED number of buffer stores per thread:
-//      lanes past the unit's count fall outside the buffer range and are
-//      dropped) and the bitmap clear                                   (barrier)
-// Two register sets alternate through a 2x unrolled body, so an in-flight
-// register is never copied, and the fixed store count lets the compiler wait
-// for unit k+1's loads with a counted vmcnt instead of waiting for the
-// stores too.  The row pipeline is the row-major kernel's, one window earlier.
-template <int LGW, int NT, int PCAP, int R, int CCAP>
-__global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
-  if (*ra.a.err & 8) return;   // ws8 lengths truncated (see spgemm_bm_rows)
-  const BmArgs& p = ra.a;
-  constexpr int NW = NT / 64;
-  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
-  constexpr int NWO = PCAP / NT;   // write-out rounds
-  static_assert(WPW % 64 == 0 && PCAP < 65536 && PCAP % NT == 0, "geometry");
-
-  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
-  __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
-  __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
-  __shared__ uint32_t desc[CCAP];   // chunk: first B index << 5 | (valid lanes - 1)   (B.nnz < 2^27, lanes <= 32)
-  __shared__ int64_t suo[16];       // uoff of the current row's windows
-  __shared__ float dval[2][CCAP];   // by unit parity: unit k's survive unit k+1's staging
-  __shared__ int wsum[3 * NW];
-  __shared__ int sdup;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lg = p.lg;
-  const int Gl = 1 << lg;
-  const int ngrp = NW << (6 - lg);
-  const int gid = (w << (6 - lg)) + (lane >> lg);
-  const int gl = lane & (Gl - 1);
-  const int nwin = p.nwin;
-  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
-  int vz;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-
-  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
-  if (tid == 0) sdup = 0;
-
-  const int64_t NG = gridDim.x;
-  const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
-  const int64_t m = p.m;
-
-  // row pipeline (see spgemm_bm_rows)
-  int cna = 0;
-  float cav = 0.f;
-  uint32_t cw1 = 0, cw2 = 0, cw3 = 0, cw4 = 0;   // packed 16-bit window lengths of the current row
-  int n1a = 0, n1b = 0, n2a = 0, n2b = 0, njj = 0;
-  float nav = 0.f;
-  uint4 nwa = make_uint4(0, 0, 0, 0);
-  uint32_t nwb = 0;
-  int64_t nuo = 0;
-  auto ld_arp = [&](int64_t r, int& a, int& b) {
-    if (r < m) {
-      a = (int)p.Arp[r + vz];
-      b = (int)p.Arp[r + 1 + vz];
-    }
-  };
-  auto ld_entries = [&](int64_t r) {
-    if (r < m) {
-      const int a0 = __builtin_amdgcn_readfirstlane(n1a), na = __builtin_amdgcn_readfirstlane(n1b) - a0;
-      if (tid < na) {
-        njj = p.Aci[a0 + tid];
-        nav = p.Av[a0 + tid];
-      }
-    }
-  };
-  auto ld_bounds = [&](int64_t r) {
-    if (r < m) {
-      const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
-      if (tid < na) {
-        nwa = ra.ws8[2 * (int64_t)njj];
-        nwb = ra.ws8[2 * (int64_t)njj + 1].x;
-      }
-      if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
-    }
-  };
-  uint32_t bq = 0;   // first B index of the next window to stage (this thread's entry)
-  // next row -> current row; the row's offsets go to LDS (read after the
-  // next barrier: every reader of the old ones has passed it)
-  auto take_next = [&]() {
-    cna = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
-    cav = nav;
-    bq = nwa.x;
-    cw1 = nwa.y;
-    cw2 = nwa.z;
-    cw3 = nwa.w;
-    cw4 = nwb;
-    if (w == 0 && lane <= nwin) suo[lane] = nuo;
-    n1a = n2a;
-    n1b = n2b;
-  };
-
-  struct U {          // wave-uniform state of a unit
-    int64_t row;
-    int q, u, clo, want, TC, nr, valid, par;
-    int64_t off;
-  };
-  auto next_unit = [&](const U& x) {
-    U y{};
-    y.row = x.q + 1 < nwin ? x.row : x.row + NG;
-    y.q = x.q + 1 < nwin ? x.q + 1 : 0;
-    y.par = x.par ^ 1;
-    return y;
-  };
-  // per-thread staging of unit y (row registers current for y.row)
-  auto stage_local = [&](const U& y, int& len, int& nch, uint32_t& b0) {
-    len = 0;
-    nch = 0;
-    b0 = bq;
-    if (y.row < m && tid < cna && tid < NT) {
-      // (select VALUES: a ternary over the captured lvalues selects their
-      // addresses and pins them to the scratch stack)
-      const uint32_t a1 = cw1, a2 = cw2, a3 = cw3, a4 = cw4;
-      const uint32_t wl = y.q < 4 ? (y.q < 2 ? a1 : a2) : (y.q < 6 ? a3 : a4);
-      len = (int)((wl >> (16 * (y.q & 1))) & 0xffffu);
-      nch = (len + Gl - 1) >> lg;
-    }
-    bq += (uint32_t)len;
-  };
-  // after the scan: descriptors, offsets, deferral
-  auto stage_finish = [&](U& y, int len, int nch, uint32_t b0, int pre, int TC, int P) {
-    y.u = (int)(y.row * nwin + y.q);
-    y.clo = y.q << LGW;
-    y.TC = TC;
-    y.nr = (TC + ngrp - 1) / ngrp;
-    y.valid = 0;
-    if (y.row >= m) return;
-    y.off = bm_rfl64(suo[y.q]);
-    y.want = (int)(bm_rfl64(suo[y.q + 1]) - y.off);
-    const bool too_big = cna > NT || P > PCAP || TC > CCAP || TC > R * ngrp;
-    if (P == 0) return;
-    if (too_big) {
-      if (tid == 0) {
-        const uint32_t at = atomicAdd(p.novf, 1u);
-        if ((int64_t)at < p.ovf_cap) p.ovf[at] = y.u;
-        else atomicOr(p.err, 4);
-      }
-      return;
-    }
-    y.valid = 1;
-    for (int kk = 0; kk < nch; ++kk) {
-      const int rem = len - (kk << lg);
-      desc[pre + kk] = ((b0 + ((uint32_t)kk << lg)) << 5) | (uint32_t)((rem < Gl ? rem : Gl) - 1);
-      dval[y.par][pre + kk] = cav;
-    }
-  };
-  // B index of round d of unit y for this lane (ok: a valid product)
-  auto addr = [&](const U& y, uint32_t (&f)[R], uint32_t& okm) {
-    okm = 0;
-#pragma unroll
-    for (int d = 0; d < R; ++d) {
-      const int t = gid + d * ngrp;
-      const uint32_t ds = desc[t < y.TC ? t : y.TC - 1];
-      const bool ok = (t < y.TC) & ((uint32_t)gl <= (ds & 31u));
-      okm |= (ok ? 1u : 0u) << d;
-      f[d] = (ds >> 5) + (ok ? (uint32_t)gl : 0u);
-    }
-  };
-  // unit y's B columns (one unit ahead) / B values (at the top of its own unit)
-  auto issue_cols = [&](const U& y, int (&cc)[R], uint32_t& okm) {
-    uint32_t f[R];
-    addr(y, f, okm);
-#pragma unroll
-    for (int d = 0; d < R; ++d) {
-      cc[d] = 0;
-      if (d < y.nr) cc[d] = p.Bci[f[d]];   // wave-uniform guard
-    }
-  };
-  auto issue_vals = [&](const U& y, float (&vv)[R]) {
-    uint32_t f[R], okm;
-    addr(y, f, okm);
-#pragma unroll
-    for (int d = 0; d < R; ++d) {
-      vv[d] = 0.f;
-      if (d < y.nr) vv[d] = p.Bv[f[d]];
-    }
-  };
-
-  // ---- prologue: the row pipeline, then stage + issue the first unit ------
-  ld_arp(me, n1a, n1b);
-  ld_entries(me);
-  ld_bounds(me);
-  ld_arp(me + NG, n2a, n2b);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  take_next();
-  U X{};
-  X.row = me;
-  X.q = 0;
-  X.par = 0;
-  int cA[R], cB[R];
-  float vC[R];
-  uint32_t okA = 0, okB = 0;
-  {
-    int len, nch, pre, plen, TC, P;
-    uint32_t b0;
-    stage_local(X, len, nch, b0);
-    bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-    stage_finish(X, len, nch, b0, pre, TC, P);
-    __syncthreads();
-    okA = 0;
-    if (X.valid) issue_cols(X, cA, okA);
-  }
-
-  auto body = [&](U& X, int (&cC)[R], uint32_t okC, int (&cN)[R], uint32_t& okN) {
-    const bool lastq = X.q == nwin - 1;
-    if (X.q == 0) {
-      ld_entries(X.row + NG);
-      ld_arp(X.row + 2 * NG, n2a, n2b);
-    }
-    if (X.q == nwin - 2) ld_bounds(X.row + NG);
-    // ---- 1. unit X: its B values in flight, OR its columns ---------------
-    uint32_t dupm = 0;
-    if (X.valid) {
-      issue_vals(X, vC);   // used in pass 2, two barriers later
-      uint32_t old[R];
-#pragma unroll
-      for (int d = 0; d < R; ++d) cC[d] = ((okC >> d) & 1u) ? cC[d] - X.clo : -1;
-#pragma unroll
-      for (int d = 0; d < R; ++d) {
-        old[d] = 0u;
-        if (cC[d] >= 0) old[d] = atomicOr(bm32 + (cC[d] >> 5), 1u << (cC[d] & 31));
-      }
-#pragma unroll
-      for (int d = 0; d < R; ++d) dupm |= (cC[d] >= 0 ? (old[d] >> (cC[d] & 31)) & 1u : 0u) << d;
-    }
-    if (lastq) take_next();   // the next row's loads were issued before unit X's: landed
-    if (dupm) sdup = 1;
-    __syncthreads();   // (a) X's bitmap complete
-    // ---- 2. unit Y's staging scan; unit X's wave-local rank prefixes ---------
-    U Y = next_unit(X);
-    int len, nch;
-    uint32_t b0;
-    stage_local(Y, len, nch, b0);
-    const int xa = bm_wave_incl(nch), xb = bm_wave_incl(len);
-    int wtot = 0;
-    if (X.valid) {
-#pragma unroll
-      for (int kk = 0; kk < WPT; ++kk) {
-        const int wd = w * WPW + kk * 64 + lane;
-        const int cnt = __popcll(bm[wd]);
-        const int incl = bm_wave_incl(cnt);
-        pre16[wd] = (uint16_t)(wtot + incl - cnt);
-        wtot += __builtin_amdgcn_readlane(incl, 63);
-      }
-    }
-    if (lane == 63) {
-      wsum[w] = xa;
-      wsum[NW + w] = xb;
-    }
-    if (lane == 0) wsum[2 * NW + w] = wtot;
-    __syncthreads();   // (b) scans + X's prefixes visible
-    // ---- 3. unit Y's descriptors; unit X's pass 2 (owners) -----------------
-    int qa = 0, TC = 0, P = 0, total = 0;
-    int wt[NW];   // rank total of every wave's bitmap block (uniform)
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      const int sa = wsum[i], sb = wsum[NW + i], sc = __builtin_amdgcn_readfirstlane(wsum[2 * NW + i]);
-      qa += (i < w) ? sa : 0;
-      TC += sa;
-      P += sb;
-      wt[i] = sc;
-      total += sc;
-    }
-    const int any_dup = sdup;
-    stage_finish(Y, len, nch, b0, qa + xa - nch, TC, P);
-    static_assert((WPW & (WPW - 1)) == 0, "power-of-two wave blocks");
-    // (the base is a sum of compares over scalars: a select chain over an
-    // array gets folded into a dynamically indexed stack load)
-    auto rank = [&](int c) {
-      const int wd = c >> 6;
-      const int blk = wd / WPW;
-      int base = 0;
-#pragma unroll
-      for (int i = 0; i < NW - 1; ++i) base += blk > i ? wt[i] : 0;
-      return base + (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (c & 63)) - 1ull));
-    };
-    if (X.valid) {
-      // B values times a(i, j) (this unit's parity buffer survived unit Y's staging)
-#pragma unroll
-      for (int d = 0; d < R; ++d) {
-        const int t = gid + d * ngrp;
-        vC[d] *= dval[X.par][t < X.TC ? t : X.TC - 1];
-      }
-#pragma unroll
-      for (int d0 = 0; d0 < R; d0 += 4) {
-        int r[4];
-#pragma unroll
-        for (int dd = 0; dd < 4 && d0 + dd < R; ++dd) r[dd] = rank(cC[d0 + dd] >= 0 ? cC[d0 + dd] : 0);
-#pragma unroll
-        for (int dd = 0; dd < 4 && d0 + dd < R; ++dd) {
-          const int d = d0 + dd;
-          if (cC[d] >= 0 && !((dupm >> d) & 1u))
-            items[r[dd]] = ((unsigned long long)__float_as_uint(vC[d]) << 32) | (uint32_t)(cC[d] + X.clo);
-        }
-      }
-    }
-    __syncthreads();   // (c) Y's descriptors visible, X's owner slots written
-    // ---- 4. unit X's duplicates; ISSUE unit Y's B columns ------------------
-    // (the duplicates first: any wait in their code would otherwise also wait
-    // for Y's loads)
-    if (tid == 0) sdup = 0;
-    if (X.valid && any_dup) {
-#pragma unroll
-      for (int d = 0; d < R; ++d)
-        if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(cC[d])]) + 1, vC[d]);
-    }
-    okN = 0;
-    if (Y.valid) issue_cols(Y, cN, okN);
-    __syncthreads();   // (d) X's slots final
-    // ---- 5. unit X's slots to C: NWO rounds, 2 buffer stores each ---------
-    if (X.valid) {
-      int lim = total;
-      if (X.want != total || X.off < 0 || X.off + total > p.cap) {   // never write outside the unit or C
-        if (tid == 0) atomicOr(p.err, 2);
-        lim = (X.off < 0 || X.off + total > p.cap) ? 0 : (total < X.want ? total : X.want);
-      }
-      const auto rc = __builtin_amdgcn_make_buffer_rsrc(p.Cci + X.off, (short)0, lim * 4, 0x00020000);
-      const auto rv = __builtin_amdgcn_make_buffer_rsrc(p.Cv + X.off, (short)0, lim * 4, 0x00020000);
-#pragma unroll
-      for (int it = 0; it < NWO; ++it) {
-        const int i = tid + it * NT;
-        const unsigned long long x = items[i];
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, rc, i * 4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(x >> 32), rv, i * 4, 0, 0);
-      }
-      for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();   // (e) bitmap clear, items read
-    X = Y;
-  };
-
-  while (X.row < m) {
-    body(X, cA, okA, cB, okB);
-    if (X.row >= m) break;
-    body(X, cB, okB, cA, okA);
-  }
 }
 
 // ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
@@ -2028,7 +1261,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_pipe(BmRowArgs ra) {
 // hide each other's B-load latency (the 8-window, 128 KB-bitmap count kernel
 // runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
 // wave's own bitmap rows, clear of the same rows, one barrier.
-template <int LGW, int NSUB, int NT, int RR, int CCAP>
+template <int LGW, int NSUB, int NT, int RR, int CCAP, bool PADC>
 #ifndef SPMM_BM_COUNT_WPS   // row count kernel: waves per SIMD its registers are sized for (8: <= 64 VGPRs)
 #define SPMM_BM_COUNT_WPS 8   // (64k: 8 = 1.547-1.551 ms with 2 spills, 7 = 1.547-1.565, 6 = 1.641)
 #endif
@@ -2038,8 +1271,7 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int WORDS_PER_WIN = NWORD / NSUB;
   static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
-  constexpr int LGV = SPMM_BM_COUNT_LGV;
-  static_assert(LGV == 0 || LGV == 1, "one or two columns per lane and load");
+  constexpr int SH = PADC ? 1 : 0;   // log2 columns per lane and load
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
@@ -2088,7 +1320,9 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
       const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
       if (tid < na) {
         nwa = ra.ws8[2 * (int64_t)njj];
-        nwb = ra.ws8[2 * (int64_t)njj + 1].x;
+        const uint4 x = ra.ws8[2 * (int64_t)njj + 1];
+        nwb = x.x;
+        if constexpr (PADC) nwa.x = x.z;   // the row's first column in the padded column array
       }
     }
   };
@@ -2107,17 +1341,12 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   take_next();
   __syncthreads();
 
-  uint32_t pf0 = 0, pf1 = 0;   // prefetch sinks (SPMM_BM_PREFETCH)
   for (; row < m; row += NG) {
     const int na = cna;
-    const int q0 = ra.q0, q1 = ra.q1;   // (q0 a multiple of NSUB)
-    uint32_t bq = bm_window_start(cwa, cwb, q0);
-    for (int q = q0; q < q1; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
-      const bool last = q + NSUB >= q1;
-#if SPMM_BM_PREFETCH
-      asm volatile("" ::"v"(pf0), "v"(pf1));
-#endif
-      if (q == q0) {
+    uint32_t bq = cwa.x;
+    for (int q = 0; q < nwin; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
+      const bool last = q + NSUB >= nwin;
+      if (q == 0) {
         ld_entries(row + NG);
         ld_arp(row + 2 * NG, n2a, n2b);
       }
@@ -2127,26 +1356,21 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
       if (tid < na && tid < NT) {
         if constexpr (NSUB == 1) {
           len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
-        } else {   // q even: windows q and q + 1 share one 32-bit word of lengths
-          static_assert(NSUB == 2, "count units of one or two windows");
-          len = (int)(wl & 0xffffu) + (q + 1 < nwin ? (int)(wl >> 16) : 0);
+        } else if constexpr (NSUB == 2) {   // q even: windows q and q + 1 share one 32-bit word of lengths
+          len = (int)(wl & 0xffffu) + (int)(wl >> 16);   // (lengths past nwin are packed as 0)
+        } else {   // q a multiple of NSUB: the unit's lengths are whole 32-bit words of ws8
+          static_assert(NSUB == 4 || NSUB == 8, "count units of 1, 2, 4 or 8 windows");
+          const uint32_t wq[4] = {cwa.y, cwa.z, cwa.w, cwb};
+#pragma unroll
+          for (int k = 0; k < NSUB / 2; ++k) {
+            const uint32_t x = wq[(q >> 1) + k < 4 ? (q >> 1) + k : 3];
+            len += (int)(x & 0xffffu) + (int)(x >> 16);
+          }
         }
-        nch = (len + (Gl << LGV) - 1) >> (lg + LGV);
+        nch = (len + (Gl << SH) - 1) >> (lg + SH);
       }
       const uint32_t b0 = bq;
-      bq += (uint32_t)len;
-#if SPMM_BM_PREFETCH
-      if (!last && tid < na && tid < NT) {   // the next unit's column segment of this entry into L2
-        const int qn = q + NSUB;
-        const uint32_t wn = qn < 2 ? cwa.y : qn < 4 ? cwa.z : qn < 6 ? cwa.w : cwb;
-        uint32_t ln = (wn >> (16 * (qn & 1))) & 0xffffu;
-        if (NSUB == 2 && qn + 1 < nwin) ln += wn >> 16;
-        if (ln) {
-          pf0 = (uint32_t)p.Bci[bq];
-          pf1 = (uint32_t)p.Bci[bq + ln - 1];
-        }
-      }
-#endif
+      bq += PADC ? (uint32_t)(((len + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg) : (uint32_t)len;
       const int clo = q << LGW;
       const int64_t u = row * nwin + q;
       int pre, plen, TC, P;
@@ -2155,9 +1379,9 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
         const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
         const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
         for (int kk = k0; kk < k1; ++kk) {
-          const int rem = len - (kk << (lg + LGV));
+          const int rem = len - (kk << (lg + SH));
           desc[pre + kk - cb] =
-              make_uint2(b0 + ((uint32_t)kk << (lg + LGV)), (uint32_t)(rem < (Gl << LGV) ? rem : (Gl << LGV)));
+              make_uint2(b0 + ((uint32_t)kk << (lg + SH)), (uint32_t)(rem < (Gl << SH) ? rem : (Gl << SH)));
         }
         __syncthreads();
         const int nr = (TCb + ngrp - 1) / ngrp;
@@ -2168,56 +1392,53 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
             const int t = gid + (i0 + d) * ngrp;
             ds[d] = desc[t < TCb ? t : TCb - 1];
           }
-#if SPMM_BM_COUNT_LGV == 1
-          // two consecutive products per lane, one 8-byte load (4-byte aligned);
-          // the last element of B is never the first of a pair load
-          typedef int i2a4 __attribute__((ext_vector_type(2), aligned(4)));
-          i2a4 x2[RR];
-          uint32_t okm = 0, ok2m = 0, hi1m = 0;
+          if constexpr (PADC) {
+            // two columns per lane: one 8-byte load (aligned: chunks start on
+            // 32-column boundaries of the padded array); the second column
+            // may be past the segment (padding)
+            uint2 x[RR];
+            uint32_t okm = 0, ok2m = 0;
 #pragma unroll
-          for (int d = 0; d < RR; ++d) {
-            const int t = gid + (i0 + d) * ngrp;
-            const int nv = (int)ds[d].y - 2 * gl;
-            const bool ok = (t < TCb) & (nv > 0);
-            okm |= (ok ? 1u : 0u) << d;
-            ok2m |= (ok & (nv > 1) ? 1u : 0u) << d;
-            uint32_t f = ds[d].x + (ok ? 2u * (uint32_t)gl : 0u);
-            const bool atend = (int64_t)f + 1 >= p.cap;   // (a single product at B's last element)
-            hi1m |= (atend ? 1u : 0u) << d;
-            f -= atend ? 1u : 0u;
-            x2[d] = i2a4{0, 0};
-            if (i0 + d < nr) x2[d] = *reinterpret_cast<const i2a4*>(p.Bci + f);   // wave-uniform guard
-          }
-#pragma unroll
-          for (int d = 0; d < RR; ++d) {
-            if ((okm >> d) & 1u) {
-              const int cc = (((hi1m >> d) & 1u) ? x2[d].y : x2[d].x) - clo;
-              atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+            for (int d = 0; d < RR; ++d) {
+              const int t = gid + (i0 + d) * ngrp;
+              const int nv = (int)ds[d].y - 2 * gl;
+              const bool ok = (t < TCb) & (nv > 0);
+              okm |= (ok ? 1u : 0u) << d;
+              ok2m |= (ok & (nv > 1) ? 1u : 0u) << d;
+              x[d] = make_uint2(0u, 0u);
+              if (i0 + d < nr)   // wave-uniform guard
+                x[d] = *reinterpret_cast<const uint2*>(p.Bci + ds[d].x + (ok ? 2u * (uint32_t)gl : 0u));
             }
-            if ((ok2m >> d) & 1u) {
-              const int cc = x2[d].y - clo;
-              atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+#pragma unroll
+            for (int d = 0; d < RR; ++d) {
+              if ((okm >> d) & 1u) {
+                const int cc = (int)x[d].x - clo;
+                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+              }
+              if ((ok2m >> d) & 1u) {
+                const int cc = (int)x[d].y - clo;
+                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+              }
             }
-          }
-#else
-          int x[RR];
-          uint32_t okm = 0;
+          } else {
+            int x[RR];
+            uint32_t okm = 0;
 #pragma unroll
-          for (int d = 0; d < RR; ++d) {
-            const int t = gid + (i0 + d) * ngrp;
-            const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
-            okm |= (ok ? 1u : 0u) << d;
-            x[d] = 0;
-            if (i0 + d < nr) x[d] = p.Bci[ds[d].x + (ok ? (uint32_t)gl : 0u)];   // wave-uniform guard
-          }
+            for (int d = 0; d < RR; ++d) {
+              const int t = gid + (i0 + d) * ngrp;
+              const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
+              okm |= (ok ? 1u : 0u) << d;
+              x[d] = 0;
+              if (i0 + d < nr) x[d] = p.Bci[ds[d].x + (ok ? (uint32_t)gl : 0u)];   // wave-uniform guard
+            }
 #pragma unroll
-          for (int d = 0; d < RR; ++d) {
-            if ((okm >> d) & 1u) {
-              const int cc = x[d] - clo;
-              atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+            for (int d = 0; d < RR; ++d) {
+              if ((okm >> d) & 1u) {
+                const int cc = x[d] - clo;
+                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+              }
             }
           }
-#endif
         }
         __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
       }
@@ -2261,22 +1482,76 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
 }
 
 // ws8[j] from ws (nwin <= 8): first index + 16-bit window lengths; err bit 3
-// if a window segment of some B row is 65536 entries or longer.
+// if a window segment of some B row is 65536 entries or longer.  plen (if
+// given): the row's length in the padded pair array (segments rounded up to
+// 2^kPadLg pairs).
 __global__ __launch_bounds__(256) void bm_pack_ws8(const uint32_t* __restrict__ ws, int64_t mb, int nwin,
-                                                   uint4* __restrict__ ws8, int32_t* __restrict__ err) {
+                                                   uint4* __restrict__ ws8, int32_t* __restrict__ err,
+                                                   int64_t* __restrict__ plen, int64_t* __restrict__ plen_c, int gc) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= mb) return;
   const uint32_t* wr = ws + j * (nwin + 1);
   uint32_t l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   bool bad = false;
+  int64_t pl = 0, pc = 0;
   for (int q = 0; q < nwin; ++q) {
     const uint32_t d = wr[q + 1] - wr[q];
     bad |= d > 0xffffu;
     l[q] = d & 0xffffu;
+    pl += (((int64_t)d + (1 << kPadLg) - 1) >> kPadLg) << kPadLg;
+  }
+  for (int q = 0; q < nwin; q += gc) {   // count groups of gc windows
+    const int64_t d = (int64_t)wr[q + gc < nwin ? q + gc : nwin] - wr[q];
+    pc += ((d + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg;
   }
   if (bad) atomicOr(err, 8);
   ws8[2 * j] = make_uint4(wr[0], l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16));
   ws8[2 * j + 1] = make_uint4(l[6] | (l[7] << 16), 0u, 0u, 0u);
+  if (plen) plen[j] = pl;
+  if (plen_c) plen_c[j] = pc;
+}
+
+// Padded pair array: one wave per B row copies its (column, value) pairs to
+// row base pbase[j] + the padded start of each window (padding slots are left
+// as they are: the kernels never read a padded slot as a product), and stores
+// the base in ws8[2j + 1].y.
+__global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__ ws, const int32_t* __restrict__ col,
+                                                    const uint32_t* __restrict__ val, int64_t mb, int nwin,
+                                                    const int64_t* __restrict__ pbase, uint4* __restrict__ ws8,
+                                                    uint2* __restrict__ out, const int64_t* __restrict__ cbase,
+                                                    int gc, int32_t* __restrict__ outc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (j >= mb) return;
+  const uint32_t* wr = ws + j * (nwin + 1);
+  const uint32_t w = lane <= nwin ? wr[lane] : 0u;   // lane q: first index of window q (q = nwin: row end)
+  const int64_t base = out ? pbase[j] : 0, cb = outc ? cbase[j] : 0;
+  if (lane == 0) {
+    uint32_t* x = reinterpret_cast<uint32_t*>(&ws8[2 * j + 1]);
+    if (out) x[1] = (uint32_t)base;
+    if (outc) x[2] = (uint32_t)cb;
+  }
+  // padded start of window q (lane q): exclusive scan of the rounded lengths
+  const uint32_t wn = __shfl_down(w, 1);
+  const uint32_t rl = lane < nwin ? ((wn - w + (1u << kPadLg) - 1) >> kPadLg) << kPadLg : 0u;
+  const uint32_t ps = (uint32_t)bm_wave_incl((int)rl) - rl;
+  // padded start of count group g (lane g): windows [g gc, (g + 1) gc)
+  const int ng = (nwin + gc - 1) / gc;
+  const uint32_t g0 = (uint32_t)__shfl(w, lane * gc < nwin ? lane * gc : nwin);
+  const uint32_t g1 = (uint32_t)__shfl(w, (lane + 1) * gc < nwin ? (lane + 1) * gc : nwin);
+  const uint32_t rc = lane < ng ? ((g1 - g0 + (1u << kPadCLg) - 1) >> kPadCLg) << kPadCLg : 0u;
+  const uint32_t pc = (uint32_t)bm_wave_incl((int)rc) - rc;
+  const uint32_t r0 = __builtin_amdgcn_readfirstlane(w), r1 = __builtin_amdgcn_readlane(w, nwin);
+  for (uint32_t e = r0 + lane; e < r1; e += 64) {
+    int q = 0;
+    for (int k = 1; k < nwin; ++k) q += e >= (uint32_t)__shfl(w, k) ? 1 : 0;
+    const uint32_t c = (uint32_t)col[e];
+    if (out) out[base + (uint32_t)__shfl(ps, q) + (e - (uint32_t)__shfl(w, q))] = make_uint2(c, val[e]);
+    if (outc) {
+      const int g = q / gc;
+      outc[cb + (uint32_t)__shfl(pc, g) + (e - (uint32_t)__shfl(w, g * gc))] = (int32_t)c;
+    }
+  }
 }
 
 // ws[j * (nwin + 1) + q] = first index of B row j whose column >= q * 2^lgw
@@ -2355,20 +1630,33 @@ __global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __rest
 //          count 2 windows (8 KB, 512 threads); fast <= 3840 products, SPMM_BM_CFG1_R (14) rounds
 //   cfg 2: W = 2^16: count 4 windows (32 KB, 1024 threads); fast <= 3072, 16 rounds
 // Reload (deferred units): min(1024, W / 64) threads, <= 12288 products, 2048 chunks.
+//   cfg 3: W = 2^18 (1M columns: 4 windows per row, ~2.7k products per window):
+//          row kernel 512 threads, <= 4096 products (2 workgroups per CU);
+//          row count 2 windows per unit (64 KB bitmap, 512 threads)
+// Wider windows mean longer contiguous B segments per (A entry, unit): random
+// segment gathers run at ~7 TB/s of 128-byte LINES, so 100-byte segments
+// deliver ~3.2 TB/s of useful bytes and 200-byte ones ~4.4
+// (tools/probes/seg_gather.hip, profiles/r4/seg_gather.csv).
 struct BmCfg {
-  int lgw, nsub_count, pcap_fast, rounds_fast;
+  int lgw, nsub_count, pcap_fast, rounds_fast, rows_nt, rows_r;
 };
 #ifndef SPMM_BM_CFG1_R   // register rounds of cfg 1's per-unit fast kernel (the 65536^2 config)
 #define SPMM_BM_CFG1_R 14   // 65536^2: 16 rounds spill 5 VGPRs; 14 = 1.64 -> 1.56 ms (384 of 131072 units deferred), 13: 1.61-1.67, 12: 1.82
 #endif
-// (SPMM_BM_ILV: cfg 1's interleaved bitmap takes 3 KB more LDS, so 256 fewer product slots keep 4 per CU)
-constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12}, {15, 2, SPMM_BM_ILV ? 3584 : 3840, SPMM_BM_CFG1_R}, {16, 4, 3072, 16}};
-constexpr int kNumCfgs = 3;
-constexpr int kFastNT = 256, kReloadPcap = 12288, kReloadCcap = 2048;
-#ifndef SPMM_BM_ROWS_NT   // threads of the row-major numeric kernel's workgroups (256 or 512; 4 workgroups per CU)
-#define SPMM_BM_ROWS_NT 256
+#ifndef SPMM_BM_CFG3_R   // register rounds of cfg 3's 512-thread row kernel
+#define SPMM_BM_CFG3_R 9
 #endif
-constexpr int kRowsNT = SPMM_BM_ROWS_NT;
+#ifndef SPMM_BM_CFG3_PCAP
+#define SPMM_BM_CFG3_PCAP 4096
+#endif
+constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12, 256, SPMM_BM_ROWS_R},
+                           {15, 2, 3840, SPMM_BM_CFG1_R, 256, SPMM_BM_ROWS_R},
+                           {16, 4, 3072, 16, 256, SPMM_BM_ROWS_R},
+                           {18, 2, SPMM_BM_CFG3_PCAP, SPMM_BM_CFG3_R, 512, SPMM_BM_CFG3_R}};
+constexpr int kNumCfgs = 4;
+constexpr int kFastNT = 256, kReloadCcap = 2048;
+// reload product slots: 96 KB of items (80 KB next to W = 2^18's 32 KB bitmap + 8 KB prefixes)
+constexpr int reload_pcap(int lgw) { return lgw >= 18 ? 10112 : 12288; }
 // reload workgroup: up to 1024 threads (the longest A row it can stage), at
 // most one wave per 64 bitmap words
 constexpr int reload_nt(int lgw) { return ((1 << lgw) / 64) < 1024 ? ((1 << lgw) / 64) : 1024; }
@@ -2381,12 +1669,10 @@ struct BmKernels {
   static constexpr auto fast = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
                                          K.rounds_fast * (kFastNT / 16), 1>;
   static constexpr int kReloadNT = reload_nt(K.lgw);
-  static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, kReloadPcap, 8, kReloadCcap, 2>;
+  static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2>;
   static constexpr auto fast_det = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
                                              K.rounds_fast * (kFastNT / 16), 1, true>;
-  static constexpr auto fast_cv = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
-                                            K.rounds_fast * (kFastNT / 16), 1, false, true>;
-  static constexpr auto reload_det = spgemm_bm<K.lgw, 1, kReloadNT, kReloadPcap, 8, kReloadCcap, 2, true>;
+  static constexpr auto reload_det = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2, true>;
 };
 
 template <typename K>
@@ -2411,17 +1697,13 @@ int bm_count(int64_t work, const BmArgs& a, hipStream_t s) {
 template <int C>
 struct BmRowKernel {
   static constexpr BmCfg K = kCfgs[C];
-  static constexpr int NT = kRowsNT;
-  // register rounds: the same products per workgroup round at any width (the
-  // row pipeline's registers cost rounds)
-  static constexpr int R0 = K.rounds_fast > SPMM_BM_ROWS_R ? SPMM_BM_ROWS_R : K.rounds_fast;
-  static constexpr int R = (R0 * kFastNT + NT - 1) / NT;
+  static constexpr int NT = K.rows_nt;
+  // register rounds (the row pipeline's registers cost rounds)
+  static constexpr int R = K.rounds_fast > K.rows_r ? K.rows_r : K.rounds_fast;
   static constexpr auto k = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, false>;
   static constexpr auto kcv = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false>;
   static constexpr auto k_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, true>;
   static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, true>;
-  static constexpr auto k_fused = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, false, true>;
-  static constexpr auto kcv_fused = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false, true>;
 };
 
 
@@ -2438,16 +1720,6 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastN
   return 0;
 }
 
-// fused row kernel (count phase + row look-back) over every row, then the
-// reload kernel over the deferred units (which reads the offsets it wrote)
-template <int C>
-int bm_fused_rows(BmRowArgs ra, hipStream_t s) {
-  using K = BmRowKernel<C>;
-  const int rc = ra.a.Bcv ? launch_rows(K::kcv_fused, ra, s, K::NT) : launch_rows(K::k_fused, ra, s, K::NT);
-  if (rc) return rc;
-  return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
-}
-
 // count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
 // per unit (32 KB, 4 per CU: a B row's column segment read once for both)
 #ifndef SPMM_BM_COUNT_RR   // B loads in flight per thread (diagnostic builds: tools/bm_variants.py)
@@ -2456,54 +1728,36 @@ int bm_fused_rows(BmRowArgs ra, hipStream_t s) {
 #ifndef SPMM_BM_COUNT_NT   // threads per count workgroup (the host gates A rows <= this)
 #define SPMM_BM_COUNT_NT 256
 #endif
-constexpr int kCountNT = SPMM_BM_COUNT_NT;
+// workgroup size by bitmap bytes: 32 KB -> 256 threads (4 per CU), 64 KB -> 512 (2 per CU)
+constexpr int count_nt(int lgw, int nsub) {
+  return ((nsub << lgw) / 8) > (64 << 10) ? 1024 : ((nsub << lgw) / 8) > (32 << 10) ? 512 : SPMM_BM_COUNT_NT;
+}
 template <int C, int NSUB>
 struct BmRowCountKernel {
-  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, kCountNT, SPMM_BM_COUNT_RR, 256>;
+  static constexpr int NT = count_nt(kCfgs[C].lgw, NSUB);
+  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, false>;
+  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, true>;
 };
 
-// passes > 0: window-major, one launch per `passes` windows (a multiple of nsub)
 template <int C>
-int bm_count_rows(BmRowArgs ra, int nsub, int passes, hipStream_t s) {
-  const int nwin = ra.a.nwin;
-  const int step = passes > 0 ? ((passes + nsub - 1) / nsub) * nsub : nwin;
-  for (int q = 0; q < nwin; q += step) {
-    ra.q0 = q;
-    ra.q1 = q + step < nwin ? q + step : nwin;
-    const int rc = nsub == 2 ? launch_rows(BmRowCountKernel<C, 2>::k, ra, s, kCountNT)
-                             : launch_rows(BmRowCountKernel<C, 1>::k, ra, s, kCountNT);
-    if (rc) return rc;
-  }
-  return 0;
+int bm_count_rows(BmRowArgs ra, int nsub, hipStream_t s) {
+  using K1 = BmRowCountKernel<C, 1>;
+  using K2 = BmRowCountKernel<C, 2>;
+  using K4 = BmRowCountKernel<C, 4>;
+  if (ra.pad)
+    return nsub == 4 ? launch_rows(K4::kp, ra, s, K4::NT)
+                     : (nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT));
+  return nsub == 4 ? launch_rows(K4::k, ra, s, K4::NT)
+                   : (nsub == 2 ? launch_rows(K2::k, ra, s, K2::NT) : launch_rows(K1::k, ra, s, K1::NT));
 }
 
+// det: the deterministic kernels (fixed summation order)
 template <int C>
-struct BmPipeKernel {
-  static constexpr BmCfg K = kCfgs[C];
-  static constexpr int R = K.rounds_fast > 10 ? 10 : K.rounds_fast;
-  static constexpr auto k = spgemm_bm_pipe<K.lgw, kFastNT, K.pcap_fast, R, R * (kFastNT / 16)>;
-};
-
-
-// pipe: the software-pipelined kernel (needs nwin >= 4 for its row pipeline);
-// det: the deterministic kernels (fixed summation order; not with pipe)
-template <int C>
-int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, int det, hipStream_t s) {
-  if (pipe && !det) {
-    const int rc = launch_rows(BmPipeKernel<C>::k, ra, s);
-    if (rc) return rc;
-  } else {   // passes > 0: window-major, one launch per `passes` windows
-    const int nwin = ra.a.nwin;
-    const int step = passes > 0 ? passes : nwin;
-    for (int q = 0; q < nwin; q += step) {
-      ra.q0 = q;
-      ra.q1 = q + step < nwin ? q + step : nwin;
-      using K = BmRowKernel<C>;
-      const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
-                         : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT));
-      if (rc) return rc;
-    }
-  }
+int bm_numeric_rows(BmRowArgs ra, int det, hipStream_t s) {
+  using K = BmRowKernel<C>;
+  const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
+                     : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT));
+  if (rc) return rc;
   return det ? launch_bm(BmKernels<C>::reload_det, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s)
              : launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
 }
@@ -2511,18 +1765,12 @@ int bm_numeric_rows(BmRowArgs ra, int pipe, int passes, int det, hipStream_t s) 
 template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, int det, hipStream_t s) {
   using K = BmKernels<C>;
-  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s)
-                     : (a.Bcv ? launch_bm(K::fast_cv, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s));
+  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s);
   if (rc) return rc;
   return det ? launch_bm(K::reload_det, K::kReloadNT, int64_t(1) << 30, a, s)
              : launch_bm(K::reload, K::kReloadNT, int64_t(1) << 30, a, s);
 }
 
-// integer knob from the environment (read once per name by the caller's static)
-int bm_env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
 
 }  // namespace
 
@@ -2564,7 +1812,8 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
   switch (cfg) {
     case 0: return bm_count<0>(work, a, s);
     case 1: return bm_count<1>(work, a, s);
-    default: return bm_count<2>(work, a, s);
+    case 2: return bm_count<2>(work, a, s);
+    default: return bm_count<3>(work, a, s);
   }
 }
 
@@ -2572,33 +1821,22 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
 // units it deferred (novf must be zero; ovf has room for ovf_cap units).
 // det: fixed summation order (see "deterministic mode"); err bit 4 then
 // means a unit needs the CPU engine.
-// Bcv: optional [nnz(B)] (column, value bits) pairs for the fast kernel (not
-// with det; the reload kernel reads Bci / Bv).
-SPMM_EXPORT int spmm_spgemm_bm_numeric_cv(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
-                                          const uint32_t* ws, const int32_t* Bci, const float* Bv, const void* Bcv,
-                                          int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap, int32_t* Cci,
-                                          float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err,
-                                          int det, void* stream) {
-  if (m <= 0) return 0;
-  if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
-  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
-           det ? nullptr : (const uint2*)Bcv, err};
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t work = m * nwin;
-  switch (cfg) {
-    case 0: return bm_numeric<0>(work, a, det, s);
-    case 1: return bm_numeric<1>(work, a, det, s);
-    default: return bm_numeric<2>(work, a, det, s);
-  }
-}
-
 SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                        const uint32_t* ws, const int32_t* Bci, const float* Bv, int64_t m, int nwin,
                                        int lg, const int64_t* uoff, int64_t cap, int32_t* Cci, float* Cv,
                                        int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, int det,
                                        void* stream) {
-  return spmm_spgemm_bm_numeric_cv(cfg, Arp, Aci, Av, ws, Bci, Bv, nullptr, m, nwin, lg, uoff, cap, Cci, Cv, ovf, novf,
-                                   ovf_cap, err, det, stream);
+  if (m <= 0) return 0;
+  if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
+  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, nullptr, err};
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t work = m * nwin;
+  switch (cfg) {
+    case 0: return bm_numeric<0>(work, a, det, s);
+    case 1: return bm_numeric<1>(work, a, det, s);
+    case 2: return bm_numeric<2>(work, a, det, s);
+    default: return bm_numeric<3>(work, a, det, s);
+  }
 }
 
 // Diagnostics: on >= 0 resets the stamp accumulators and enables (1) or
@@ -2620,11 +1858,28 @@ SPMM_EXPORT int spmm_spgemm_bm_stamps(int on, unsigned long long* out8) {
 // ws8 for the row-major numeric kernel (nwin <= 8); err bit 3: a window
 // segment too long for 16 bits (use spmm_spgemm_bm_numeric instead).
 SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin, void* ws8, int32_t* err,
-                                        void* stream) {
+                                        int64_t* plen, int64_t* plen_c, int gc, void* stream) {
   if (mb <= 0) return 0;
-  if (nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
+  if (nwin < 1 || nwin > 8 || gc < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bm_pack_ws8, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, mb, nwin,
-                     (uint4*)ws8, err);
+                     (uint4*)ws8, err, plen, plen_c, gc);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Padded arrays of B (either may be null): the (column, value) pair array of
+// the row-major numeric kernel (pass pad = 1 to it; pbase = exclusive scan of
+// the plen from spmm_spgemm_bm_pack_ws8) and the column array of the row
+// count kernel with count groups of gc windows padded to 32 columns (pad = 1
+// to it; cbase = exclusive scan of plen_c); totals < 2^32.  Also stores each
+// row's bases in ws8.
+SPMM_EXPORT int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb,
+                                         int nwin, const int64_t* pbase, void* ws8, void* out, const int64_t* cbase,
+                                         int gc, int32_t* outc, void* stream) {
+  if (mb <= 0) return 0;
+  if (nwin < 1 || nwin > 8 || gc < 1 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bm_pad_pairs, dim3((unsigned)((mb * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, col,
+                     (const uint32_t*)val, mb, nwin, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -2637,71 +1892,41 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
                                             const void* Bcv,
                                             int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap,
                                             int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                                            int32_t* err, int pipe, int det, void* stream) {
+                                            int32_t* err, int det, int pad, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
-  if (pipe && (nwin < 4 || lg > 5)) return (int)hipErrorInvalidValue;   // (+ B.nnz < 2^27: host)
+  if (pad && !Bcv) return (int)hipErrorInvalidValue;
   BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
                       (const uint2*)Bcv, err},
-               (const uint4*)ws8, 0, nwin};
+               (const uint4*)ws8, pad ? 1 : 0};
   hipStream_t s = (hipStream_t)stream;
-  const int passes = bm_env_int("SPMM_BM_NUM_PASS_WINDOWS", 0);
   switch (cfg) {
-    case 0: return bm_numeric_rows<0>(ra, pipe, passes, det, s);
-    case 1: return bm_numeric_rows<1>(ra, pipe, passes, det, s);
-    default: return bm_numeric_rows<2>(ra, pipe, passes, det, s);
-  }
-}
-
-// Fused row-major SpGEMM (nwin <= 8, every A row <= 256 entries, ws8 packed):
-// no count kernel and no host read-back between count and numeric.  Each
-// workgroup counts its row (all windows), publishes the count, resolves the
-// row's start in C by a decoupled look-back over the rows (tickets give the
-// order) and writes its windows there.  C must hold cap >= nnz(C) entries
-// (the product count is a bound).  uoff[m * nwin + 1] is OUTPUT (unit
-// offsets; uoff[m * nwin] = nnz(C)); ws_rows: device scratch of m + 1 u64
-// (zeroed here: row look-back words + the ticket counter).  err as in
-// spmm_spgemm_bm_numeric; bit 3 set on entry (ws8 truncated) makes the kernel
-// return at once and the host takes the per-unit kernels.
-SPMM_EXPORT int spmm_spgemm_bm_fused_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
-                                          const void* ws8, const uint32_t* ws, const int32_t* Bci, const float* Bv,
-                                          const void* Bcv, int64_t m, int nwin, int lg, int64_t* uoff, int64_t cap,
-                                          int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                                          int32_t* err, void* ws_rows, void* stream) {
-  if (m <= 0) return 0;
-  if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
-  if (m >= (int64_t)UINT32_MAX / 2 || m * nwin >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
-  hipStream_t s = (hipStream_t)stream;
-  unsigned long long* rstat = (unsigned long long*)ws_rows;
-  hipError_t e = hipMemsetAsync(rstat, 0, (size_t)(m + 1) * sizeof(unsigned long long), s);
-  if (e != hipSuccess) return (int)e;
-  BmRowArgs ra{BmArgs{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
-                      (const uint2*)Bcv, err},
-               (const uint4*)ws8, 0, nwin, uoff, rstat, (uint32_t*)(rstat + m)};
-  switch (cfg) {
-    case 0: return bm_fused_rows<0>(ra, s);
-    case 1: return bm_fused_rows<1>(ra, s);
-    default: return bm_fused_rows<2>(ra, s);
+    case 0: return bm_numeric_rows<0>(ra, det, s);
+    case 1: return bm_numeric_rows<1>(ra, det, s);
+    case 2: return bm_numeric_rows<2>(ra, det, s);
+    default: return bm_numeric_rows<3>(ra, det, s);
   }
 }
 
 // Row-major count (nwin <= 8, every A row <= 256 entries, ws8 packed): same
 // output as spmm_spgemm_bm_count.  Returns without counting when err bit 3
 // is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
+// pad: Bci is the padded column array of spmm_spgemm_bm_pad_pairs (gc = nsub).
 SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
                                           const int32_t* Bci, int64_t m, int nwin, int lg, int nsub, int32_t* ucnt,
-                                          int32_t* err, int64_t nnzb, void* stream) {
+                                          int32_t* err, int64_t nnzb, int pad, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   BmRowArgs ra{BmArgs{Arp, Aci, nullptr, nullptr, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr,
-                      nullptr, 0, nnzb, nullptr, err},   // (cap = nnz(B): the pair loads stay inside B)
-               (const uint4*)ws8, 0, nwin};
+                      nullptr, 0, nnzb, nullptr, err},
+               (const uint4*)ws8, pad ? 1 : 0};
   hipStream_t s = (hipStream_t)stream;
-  const int passes = bm_env_int("SPMM_BM_COUNT_PASS_WINDOWS", 0);
+  if (nsub != 1 && nsub != 2 && nsub != 4) return (int)hipErrorInvalidValue;
   switch (cfg) {
-    case 0: return bm_count_rows<0>(ra, nsub, passes, s);
-    case 1: return bm_count_rows<1>(ra, nsub, passes, s);
-    default: return bm_count_rows<2>(ra, nsub, passes, s);
+    case 0: return bm_count_rows<0>(ra, nsub, s);
+    case 1: return bm_count_rows<1>(ra, nsub, s);
+    case 2: return bm_count_rows<2>(ra, nsub, s);
+    default: return bm_count_rows<3>(ra, nsub, s);
   }
 }
 

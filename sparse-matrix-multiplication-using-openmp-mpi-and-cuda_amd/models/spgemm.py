@@ -71,6 +71,47 @@ class OperandReady:
         return self._cols() if self._cols is not None else self._full()
 
 
+class GatherStats:
+    """Observability of the right operand's all-gather (``bench.py`` JSON):
+    bytes received per call and the time from issuing the payload
+    collectives to the moment the compute stream may read the operand (device
+    events on the current stream, read after the timed loop; host clock for
+    host panels).  Off unless ``enabled``; recording adds no host sync."""
+
+    def __init__(self):
+        self.enabled = False
+        self.calls = []   # (bytes, start, end): torch.cuda.Event pairs or perf_counter floats
+
+    def reset(self, enabled: bool = True) -> None:
+        self.enabled = enabled
+        self.calls = []
+
+    def mark(self, dev: torch.device):
+        if dev.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        import time
+        return time.perf_counter()
+
+    def summary(self):
+        """(total bytes, total ms) over the recorded calls (synchronises)."""
+        tot_b, tot_ms = 0, 0.0
+        for b, t0, t1 in self.calls:
+            tot_b += b
+            if t1 is None:
+                continue
+            if isinstance(t0, float):
+                tot_ms += (t1 - t0) * 1e3
+            else:
+                t1.synchronize()
+                tot_ms += t0.elapsed_time(t1)
+        return tot_b, tot_ms
+
+
+GATHER_STATS = GatherStats()
+
+
 def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], CSR]]:
     """Right operand of the row-block SpGEMM (every rank's B row panel), in
     stages so the gather overlaps the SpGEMM's setup.
@@ -125,6 +166,10 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
         cb[:panel.nnz] = panel.col
         vb = torch.zeros(emax, dtype=torch.int32, device=dev)
         vb[:panel.nnz] = panel.val.view(torch.int32)
+        rec = None
+        if GATHER_STATS.enabled:   # bytes this rank receives: row counts + columns + values
+            rec = [W * (mmax * 8 + 2 * emax * 4), GATHER_STATS.mark(dev), None]
+            GATHER_STATS.calls.append(rec)
         pay_c = comm.all_gather_async(cb)
         pay_v = comm.all_gather_async(vb)
         base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=dev)
@@ -155,6 +200,8 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
                     raise RuntimeError(f"operand gather: {g.numel()} value words, expected {W * emax}")
                 val = torch.empty(nnz, dtype=torch.float32, device=dev)
                 cv = torch.empty((nnz, 2), dtype=torch.int32, device=dev)
+                if rec is not None:
+                    rec[2] = GATHER_STATS.mark(dev)   # the compute stream may read the payload from here
                 unpack(None, g, col, val, cv)
                 B = CSR(m, panel.n, rowptr, col, val)
                 B._bcv = cv
@@ -169,6 +216,10 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
     cb[:panel.nnz] = panel.col
     vb = torch.zeros(emax, dtype=vbits, device=dev)
     vb[:panel.nnz] = panel.val.view(vbits)
+    rec = None
+    if GATHER_STATS.enabled:
+        rec = [W * (mmax * 8 + emax * (cb.element_size() + vb.element_size())), GATHER_STATS.mark(dev), None]
+        GATHER_STATS.calls.append(rec)
     pay_c = comm.all_gather_async(cb)
     pay_v = comm.all_gather_async(vb)
 
@@ -178,6 +229,8 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
         if not done:
             Gc = pay_c().view(W, emax)
             Gv = pay_v().view(W, emax)
+            if rec is not None:
+                rec[2] = GATHER_STATS.mark(dev)
             col = torch.cat([Gc[r, :nnzs[r]] for r in range(W)])
             val = torch.cat([Gv[r, :nnzs[r]] for r in range(W)]).view(panel.val.dtype)
             done.append(CSR(m, panel.n, rowptr, col, val))

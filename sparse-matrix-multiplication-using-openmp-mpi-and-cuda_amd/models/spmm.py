@@ -86,6 +86,8 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     plan, inspector_ms, inspector_first_ms = None, None, None
     import time
 
+    if method not in ("auto", "mfma", "sweep", "rowwise"):
+        raise ValueError(f"unknown SpMM method {method!r}")
     if comm.device.type == "cuda" and method in ("auto", "mfma"):
         times = []
         for _ in range(2):   # first call: includes loading the kernels; second: the steady state
@@ -105,7 +107,9 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
             # the fastest; all times are reported.  Panel reuse decides the
             # order (tools/probes/spmm_reuse.py: MFMA from reuse ~1.6 up, the
             # sweep / row kernels near 1), but the measured time decides.
-            Xfull = torch.zeros((n, cols), dtype=torch.bfloat16, device=comm.device)
+            # Timed on the real X (the step's all-gathered operand): an
+            # all-zero X would flatter kernels whose cost depends on the data.
+            Xfull = allgather_rows(Xp, comm, counts)
             cands = (("mfma",) if plan is not None and cols % 128 == 0 else ()) + ("rowwise",) + (
                 ("sweep",) if cols == 128 and sweep_ok(A) else ())
             for meth in cands:
@@ -130,9 +134,12 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     if comm.is_dist:
         nnz_a = sum(comm.gather_ints(nnz_a))
     flops = 2 * nnz_a * cols
-    extra = dict(nnz_A=nnz_a, spmm_method=method, panel_reuse=(plan.reuse if plan is not None else None),
+    kernel = {"mfma": "MFMA panel kernel (v_mfma_f32_16x16x32_bf16)", "sweep": "VALU row-owning sweep kernel",
+              "rowwise": "VALU row-gather kernel"}[method]
+    extra = dict(nnz_A=nnz_a, spmm_method=method, spmm_kernel=kernel,
+                 panel_reuse=(plan.reuse if plan is not None else None),
                  inspector_ms=inspector_ms, inspector_first_ms=inspector_first_ms,
                  autotune_ms=kernel_ms or None, hip_graph=not comm.is_dist and comm.device.type == "cuda")
-    cfg = dict(model=f"{n}x{n} CSR SpMM (sparse x dense {cols}-col) at {density * 100:g}% density, bf16 MFMA",
+    cfg = dict(model=f"{n}x{n} CSR SpMM (sparse x dense {cols}-col) at {density * 100:g}% density, bf16, {kernel}",
                n=n, density=density, cols=cols, global_batch=1, seq_len=n, parallelism=f"rowblock{comm.world}")
     return step, flops, extra, cfg

@@ -61,13 +61,13 @@ _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_
 _native.register_hip("spmm_spgemm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_stamps", C_INT, c_vp)
-_native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, C_INT, c_vp, c_vp,
-                     C_I64, c_vp)
+                     C_I64, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, c_vp)
-_native.register_hip("spmm_spgemm_bm_fused_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
+                     c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp,
@@ -75,8 +75,6 @@ _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64,
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
                      C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
-_native.register_hip("spmm_spgemm_bm_numeric_cv", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT,
-                     c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -690,7 +688,7 @@ def _bm_pick(mean_row_products: float, ncols: int) -> Optional[int]:
     """The configuration with the widest window whose mean products per window
     fit BM_FILL of its fast capacity (widest = fewest units per row)."""
     best = None
-    for cfg in (0, 2, 1):   # widest window first
+    for cfg in (0, 2, 1):   # widest window first (cfg 3 by request only: 82 vs 76 ms on the 1M step)
         lgw, _, pcap, _, _ = _bm_config(cfg)
         W = 1 << lgw
         per_window = mean_row_products * min(W, ncols) / max(ncols, 1)
@@ -721,15 +719,26 @@ def _bitmap_ok(A: CSR, B: CSR, total_products: int, pre: dict) -> bool:
     return _FreeMem(A.device).fits(total_products * 8 + A.m * 64)
 
 
-def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional[dict] = None,
-                   _eager: bool = False) -> Optional[CSR]:
-    """Bitmap-rank SpGEMM (csr_spgemm_bitmap.hip): a count kernel gives the
-    exact nnz of every (row, column window) unit, one scan gives every unit's
-    final offset, and the numeric kernel writes each unit there once (no
-    look-back, no staging buffer, no compaction).  Returns None when a unit
-    does not fit even the reload kernel; the caller then runs the binned
-    path."""
-    dev = A.device
+@dataclass
+class BitmapPlan:
+    """Host decisions of one bitmap-rank product (``_bitmap_plan``): window
+    configuration, lane groups, which kernels run, and C's capacity in the
+    lazy flow.  Everything the kernels need besides the operands, so a plan
+    made once can drive a captured HIP graph (``SpgemmGraph``)."""
+    cfg: int
+    nwin: int
+    nsub: int
+    lg_count: int      # per-unit count kernel lane groups
+    lg_c: int          # row count kernel lane groups
+    nsub_c: int        # windows per row-count unit
+    lg_num: int
+    count_rows: bool   # row count kernel (A rows <= 256, ws8 packed)
+    rows: bool         # row-major numeric kernel
+    det: bool
+    tot: int           # intermediate products (C's capacity in the lazy flow)
+
+
+def _bitmap_plan(A: CSR, B: CSR, info: SpgemmInfo, pre: Optional[dict]) -> Optional[BitmapPlan]:
     m = A.m
     tot = info.flops // 2
     nz = max(pre["nonempty"], 1) if pre is not None else max(m, 1)
@@ -740,176 +749,239 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     nwin = max(1, -(-B.n // (1 << lgw)))
     if m * nwin >= (1 << 31):
         return None
+    seg = info.mean_seg if info.mean_seg > 0 else _true_nnz(B) / max(B.m, 1)
+    rows_mode = CONFIG.spgemm_bitmap_rows
+    ws8_ok = nwin <= 8 and rows_mode != "off"
+    nsub_c = CONFIG.spgemm_bitmap_count_windows if nwin >= 2 else 1
+    sl = seg * nsub_c / nwin   # B-segment length per row-count unit
+    return BitmapPlan(cfg=cfg, nwin=nwin, nsub=nsub, lg_count=_group_log2(seg * min(nsub, nwin) / nwin),
+                      lg_c=4 if sl < 48 else (5 if sl < 96 else 6), nsub_c=nsub_c,
+                      lg_num=4 if seg / nwin < 48 else (5 if seg / nwin < 96 else 6),
+                      count_rows=ws8_ok and pre is not None and pre.get("amax", 1 << 30) <= 256,
+                      rows=ws8_ok and (rows_mode == "on" or cfg in (0, 3)),
+                      det=CONFIG.spgemm_deterministic > 0, tot=tot)
+
+
+def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, info: Optional[SpgemmInfo] = None,
+                   use_ws8: bool = True) -> dict:
+    """The kernels of one bitmap-rank product.  ``lazy``: C at the product
+    bound, no host synchronisation at all (capturable into a HIP graph; the
+    nnz and error bits stay on the device in ``out["z"]`` / ``out["uoff"]``).
+    Eager: one read-back between count and numeric sizes C exactly."""
+    dev = A.device
+    m = A.m
+    cfg, nwin = plan.cfg, plan.nwin
+    lgw = _bm_config(cfg)[0]
     if B_ready is not None:   # columns only: the values may still be in flight (two-stage gather)
         B = getattr(B_ready, "cols", B_ready)()
-    det = CONFIG.spgemm_deterministic > 0
     lib = _native.hip()
     P = _native.ptr
     st = _native.stream_ptr(dev)
     ws = torch.empty(B.m * (nwin + 1), dtype=torch.int32, device=dev)
     _native.check(lib.spmm_spgemm_bm_splits(P(B.rowptr), P(B.col), B.m, lgw, nwin, P(ws), st), "spgemm_bm_splits")
-    seg = info.mean_seg if info.mean_seg > 0 else B.nnz / max(B.m, 1)
-    lg_count = _group_log2(seg * min(nsub, nwin) / nwin)
-    lg_num = 4 if seg / nwin < 48 else (5 if seg / nwin < 96 else 6)
     nunits = m * nwin
     z = torch.zeros(2, dtype=torch.int32, device=dev)   # err, deferred count
     err, novf = z[0:1], z[1:2]
     ucnt = torch.empty(nunits, dtype=torch.int32, device=dev)
     # row-major kernels (a row's windows back to back): <= 8 windows, packed
-    # 16-bit window lengths (ws8); the count kernel also needs A rows <= 256
-    rows_mode = CONFIG.spgemm_bitmap_rows
+    # 16-bit window lengths (ws8)
     ws8 = None
-    if nwin <= 8 and rows_mode != "off":
+    # padded layouts for the row kernels: every (row, window) segment of the
+    # numeric kernel's pairs and every (row, count group) segment of the count
+    # kernel's columns starts on a 128-byte line; sized by bounds (no read-back)
+    nnzb = _true_nnz(B)
+    ngc = -(-nwin // plan.nsub_c)
+    pad = CONFIG.spgemm_bitmap_pad > 0 and use_ws8
+    pad_num = pad and plan.rows and CONFIG.spgemm_bitmap_cv and nnzb + 15 * nwin * B.m < (1 << 32)
+    pad_cnt = pad and plan.count_rows and nnzb + 31 * ngc * B.m < (1 << 32)
+    plen = torch.empty(B.m, dtype=torch.int64, device=dev) if pad_num else None
+    plen_c = torch.empty(B.m, dtype=torch.int64, device=dev) if pad_cnt else None
+    if use_ws8 and (plan.count_rows or plan.rows):
         ws8 = torch.empty(B.m * 8, dtype=torch.int32, device=dev)
-        _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err), st), "spgemm_bm_pack_ws8")
-    count_rows = ws8 is not None and pre is not None and pre.get("amax", 1 << 30) <= 256
-    if count_rows and not det and _fused_ok(cfg, rows_mode, tot, m, dev):
-        C_ = _bitmap_fused(A, B, info, B_ready, cfg, nwin, lg_num, ws8, ws, err, novf, z)
-        if C_ is not None:
-            return C_ if C_ is not _FALLBACK else None
-        ws8, count_rows = None, False   # err bit 3 (ws8 lengths truncated): the per-unit kernels below
-
-    def count(use_rows: bool):
-        if use_rows:
-            nsub_c = CONFIG.spgemm_bitmap_count_windows if nwin >= 2 else 1
-            sl = seg * nsub_c / nwin   # B-segment length per count unit
-            lg_c = 4 if sl < 48 else (5 if sl < 96 else 6)
-            _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8), P(B.col), m, nwin,
-                                                        lg_c, nsub_c, P(ucnt), P(err), B.col.numel(), st),
-                          "spgemm_bm_count_rows")
-        else:
-            _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, lg_count,
-                                                   P(ucnt), P(err), st), "spgemm_bm_count")
-        uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
-        uoff[0] = 0
-        torch.cumsum(ucnt, 0, out=uoff[1:])
-        if lazy:
-            return uoff, (None, 0)
-        return uoff, torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
-
-    # lazy (SPMM_SPGEMM_BITMAP_LAZY=1): C at the product-count bound (what _bitmap_ok admitted), so the
-    # numeric kernels follow the count in stream order and the nnz / error bits are
-    # read once, after the product; the kernels using ws8 exit on err bit 3 (its
-    # lengths truncated), which sends the product through the eager path below
-    lazy = CONFIG.spgemm_bitmap_lazy > 0 and not det and not _eager
-    uoff, (nnz, e0) = count(count_rows)
-    if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
-        ws8 = None
-        if count_rows:
-            uoff, (nnz, e0) = count(False)
+        _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err),
+                                                  P(plen) if plen is not None else None,
+                                                  P(plen_c) if plen_c is not None else None, plan.nsub_c, st),
+                      "spgemm_bm_pack_ws8")
+    if ws8 is not None and plan.count_rows:
+        colp = None
+        if plen_c is not None:   # (columns only: B's values may still be in flight)
+            cbase = torch.cumsum(plen_c, 0)
+            cbase -= plen_c
+            colp = torch.empty(nnzb + 31 * ngc * B.m, dtype=torch.int32, device=dev)
+            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), None, B.m, nwin, None, P(ws8), None, P(cbase),
+                                                       plan.nsub_c, P(colp), st), "spgemm_bm_pad_pairs(columns)")
+            del cbase, plen_c
+        _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8),
+                                                    P(colp) if colp is not None else P(B.col), m, nwin, plan.lg_c,
+                                                    plan.nsub_c, P(ucnt), P(err), B.col.numel(), int(colp is not None),
+                                                    st),
+                      "spgemm_bm_count_rows")
+        del colp
+    else:
+        _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, plan.lg_count,
+                                               P(ucnt), P(err), st), "spgemm_bm_count")
+    uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
+    uoff[:1].zero_()   # (a fill kernel: capturable, unlike a host scalar copy)
+    torch.cumsum(ucnt, 0, out=uoff[1:])
     del ucnt
+    out = dict(uoff=uoff, z=z, nunits=nunits, ws8=ws8 is not None)
+    if not lazy:
+        nnz, e0 = torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
+        out.update(nnz=nnz)
+        if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
+            out.update(truncated=True)
+            return out
+        err.zero_()
+    cap = max(plan.tot, 1) if lazy else out["nnz"]
     if B_ready is not None:   # the numeric kernels read the values
         B = B_ready()
-    if not lazy:
-        err.zero_()
-        info.nnz = nnz
-    cap = max(tot, 1) if lazy else nnz
     Cci = torch.empty(cap, dtype=torch.int32, device=dev)
     Cv = torch.empty(cap, dtype=torch.float32, device=dev)
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
-    if ws8 is not None and (rows_mode in ("on", "pipe", "nopipe") or cfg == 0):
-        pipe = rows_mode == "pipe" and nwin >= 4 and lg_num <= 5 and B.nnz < (1 << 27)
+    det = int(plan.det)
+    if ws8 is not None and plan.rows:
         # the row-major kernel reads B as interleaved (column, value) pairs: one
-        # 8-byte stream per chunk instead of two 4-byte ones (fewer partial lines)
-        Bcv = None if pipe or not CONFIG.spgemm_bitmap_cv else interleaved(B)
+        # 8-byte stream per chunk instead of two 4-byte ones; padded, each
+        # window segment starts on a 128-byte line
+        if plen is not None:
+            pbase = torch.cumsum(plen, 0)
+            pbase -= plen
+            Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
+            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, P(pbase), P(ws8),
+                                                       P(Bcv), None, 1, None, st), "spgemm_bm_pad_pairs")
+            del pbase
+        else:
+            Bcv = interleaved(B) if CONFIG.spgemm_bitmap_cv else None
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
-                                                      lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf),
-                                                      P(novf), ovf_cap, P(err), int(pipe and not det), int(det), st),
+                                                      plan.lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf),
+                                                      P(novf), ovf_cap, P(err), det, int(plen is not None), st),
                       "spgemm_bm_numeric_rows")
-        info.rows_per_bin_num["bitmap_rows"] = 2 if pipe and not det else 1
+        if info is not None:
+            info.rows_per_bin_num["bitmap_rows"] = 1
     else:
-        # per-unit kernel: B as interleaved (column, value) pairs when enabled
-        # (SPMM_SPGEMM_BITMAP_UNIT_CV; not with det)
-        Bcv = interleaved(B) if CONFIG.spgemm_bitmap_unit_cv and not det else None
-        _native.check(lib.spmm_spgemm_bm_numeric_cv(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val),
-                                                    P(Bcv) if Bcv is not None else None, m, nwin, lg_num, P(uoff), cap,
-                                                    P(Cci), P(Cv), P(ovf), P(novf), ovf_cap, P(err), int(det), st),
+        _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
+                                                 nwin, plan.lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf),
+                                                 ovf_cap, P(err), det, st),
                       "spgemm_bm_numeric")
+    out.update(Cci=Cci, Cv=Cv, cap=cap, n=B.n)
+    return out
+
+
+def _bitmap_finish(A: CSR, B: CSR, plan: BitmapPlan, out: dict, info: SpgemmInfo, lazy: bool):
+    """Read back (once) the nnz and error bits of a launched product and
+    return its CSR, ``None`` (binned fallback), or ``"eager"`` (ws8 lengths
+    truncated in the lazy flow: rerun eagerly on the per-unit kernels)."""
+    z, uoff = out["z"], out["uoff"]
     if lazy:
         nnz, e, deferred = torch.stack([uoff[-1], z[0].long(), z[1].long()]).tolist()   # the one read-back
         if e & 8:   # ws8 lengths truncated: the count and numeric kernels stood down
-            del Cci, Cv
-            return onepass_bitmap(A, B, info, None, pre, _eager=True)
-        info.nnz = nnz
+            return "eager"
     else:
+        nnz = out["nnz"]
         e, deferred = z.tolist()
-    info.rows_per_bin_num["bitmap_units"] = nunits
-    info.rows_per_bin_num["bitmap_cfg"] = cfg
+    info.nnz = nnz
+    info.rows_per_bin_num["bitmap_units"] = out["nunits"]
+    info.rows_per_bin_num["bitmap_cfg"] = plan.cfg
     info.rows_per_bin_num["bitmap_deferred"] = deferred
     if e & 2:
         raise RuntimeError("spgemm bitmap: numeric and count kernels disagree (kernel invariant violated)")
-    if det and e & 21:
+    if plan.det and e & 21:
         # a unit beyond every deterministic kernel's budget (adversarial column
         # collisions): the CPU engine sums in the same (Gustavson) order
         info.rows_per_bin_num["det_cpu_fallback"] = 1
-        del Cci, Cv
         return _det_cpu(A, B, info)
     if e & 5:
         info.rows_per_bin_num["bitmap_fallback"] = 1
         return None
-    info.deterministic = bool(det)
+    info.deterministic = bool(plan.det)
+    nwin = plan.nwin
     rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
-    return CSR(m, B.n, rowptr, Cci[:nnz] if lazy else Cci, Cv[:nnz] if lazy else Cv)
+    Cci, Cv = out["Cci"], out["Cv"]
+    return CSR(A.m, out["n"], rowptr, Cci[:nnz] if lazy else Cci, Cv[:nnz] if lazy else Cv)
 
 
-_FALLBACK = object()   # _bitmap_fused: the product needs the binned path
-
-
-def _fused_ok(cfg: int, rows_mode: str, total_products: int, m: int, dev: torch.device) -> bool:
-    """Fused row kernel (count phase + row look-back in the numeric kernel):
-    C is allocated at the product count (a bound on nnz), so it must fit."""
-    mode = CONFIG.spgemm_bitmap_fused
-    if mode == "off" or rows_mode in ("pipe", "off"):
-        return False
-    if int(os.environ.get("SPMM_BM_NUM_PASS_WINDOWS", "0") or 0) > 0:   # window-major passes: the two-kernel path
-        return False
-    if mode == "auto" and not (cfg == 0 or rows_mode in ("on", "nopipe")):
-        return False
-    return _FreeMem(dev).fits(total_products * 8 + m * 16)
-
-
-def _bitmap_fused(A: CSR, B: CSR, info: SpgemmInfo, B_ready, cfg: int, nwin: int, lg: int, ws8, ws, err, novf, z):
-    """One kernel instead of count + scan + numeric (csr_spgemm_bitmap.hip
-    ``spmm_spgemm_bm_fused_rows``): every row is counted by the workgroup that
-    then forms it, rows find their start in C by a decoupled look-back, and the
-    one read-back (nnz, error bits) comes after the product.  Returns the CSR,
-    ``_FALLBACK`` (binned path), or None when the ws8 window lengths were
-    truncated (the caller's per-unit kernels then run)."""
-    dev = A.device
-    m = A.m
-    if B_ready is not None:   # the fused kernel reads the values from the start
-        B = B_ready()
-    lib = _native.hip()
-    P = _native.ptr
-    cap = max(info.flops // 2, 1)
-    nunits = m * nwin
-    Cci = torch.empty(cap, dtype=torch.int32, device=dev)
-    Cv = torch.empty(cap, dtype=torch.float32, device=dev)
-    uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
-    wsr = torch.empty(m + 1, dtype=torch.int64, device=dev)
-    ovf_cap = min(nunits, 1 << 20)
-    ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
-    Bcv = interleaved(B) if CONFIG.spgemm_bitmap_cv else None
-    _native.check(lib.spmm_spgemm_bm_fused_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
-                                                P(B.val), P(Bcv) if Bcv is not None else None, m, nwin, lg,
-                                                P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf), ovf_cap, P(err), P(wsr),
-                                                _native.stream_ptr(dev)), "spgemm_bm_fused_rows")
-    nnz, e, deferred = torch.stack([uoff[-1], z[0].long(), z[1].long()]).tolist()   # one read-back
-    if e & 8:
+def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional[dict] = None,
+                   _eager: bool = False) -> Optional[CSR]:
+    """Bitmap-rank SpGEMM (csr_spgemm_bitmap.hip): a count kernel gives the
+    exact nnz of every (row, column window) unit, one scan gives every unit's
+    final offset, and the numeric kernel writes each unit there once (no
+    look-back, no staging buffer, no compaction).  Returns None when a unit
+    does not fit even the reload kernel; the caller then runs the binned
+    path.  Lazy flow (``SPMM_SPGEMM_BITMAP_LAZY=1``): C at the product-count
+    bound (what ``_bitmap_ok`` admitted), no host sync between the kernels,
+    one read-back after the product."""
+    plan = _bitmap_plan(A, B, info, pre)
+    if plan is None:
         return None
-    info.rows_per_bin_num.update(bitmap_units=nunits, bitmap_cfg=cfg, bitmap_deferred=deferred, bitmap_rows=1,
-                                 bitmap_fused=1)
-    if e & 2:
-        raise RuntimeError("spgemm bitmap (fused): numeric and count phases disagree (kernel invariant violated)")
-    if e & 5:
-        info.rows_per_bin_num["bitmap_fallback"] = 1
-        return _FALLBACK
-    info.nnz = nnz
-    info.deterministic = False
-    rowptr = uoff[::nwin].contiguous() if nwin > 1 else uoff
-    return CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz])
+    lazy = CONFIG.spgemm_bitmap_lazy > 0 and not plan.det and not _eager
+    out = _bitmap_launch(A, B, plan, lazy, B_ready, info)
+    if out.get("truncated"):   # eager: per-unit count and numeric kernels
+        out = _bitmap_launch(A, B, plan, False, B_ready, info, use_ws8=False)
+    if B_ready is not None:
+        B = B_ready()
+    C_ = _bitmap_finish(A, B, plan, out, info, lazy)
+    if isinstance(C_, str):
+        del out
+        return onepass_bitmap(A, B, info, None, pre, _eager=True)
+    return C_
+
+
+class SpgemmGraph:
+    """C = A . B (bitmap-rank path) replayed from a captured HIP graph: the
+    window splits, ws8 pack, count kernel, unit-offset scan, B interleave and
+    numeric + reload kernels of one product, with NO host synchronisation
+    inside (lazy flow: C allocated once at the product-count bound; the nnz
+    and error bits are read only by :meth:`result`).  The host plan (row
+    statistics -> window configuration, lane groups, capacities) is made once
+    at construction from the operands' row plan, as a library's SpGEMM
+    inspector does; every replay recomputes the whole product.  A replay on
+    operands whose structure changed beyond the plan cannot write out of
+    bounds (the kernels clamp to C's capacity and raise error bits), and
+    :meth:`result` reports it.  Replaces the three read-backs of the eager
+    flow (row plan, count total, error words) that leave the GPU idle on
+    small products (BASELINE config 2)."""
+
+    def __init__(self, A: CSR, B: CSR):
+        if A.device.type != "cuda":
+            raise ValueError("SpgemmGraph needs GPU operands")
+        self.A, self.B = A, B
+        info = SpgemmInfo()
+        nprod, nsl, st = row_plan(A, B)
+        tot, mx, nz, light, h1, h2, h4, h8, amax = st.tolist()[:9]
+        pre = dict(max=mx, nonempty=nz, light=light, amax=amax)
+        info.flops = 2 * tot
+        info.mean_seg = tot / max(A.nnz, 1)
+        if not _bitmap_ok(A, B, tot, pre):
+            raise ValueError("SpgemmGraph: the product does not take the bitmap-rank path")
+        self.plan = _bitmap_plan(A, B, info, pre)
+        if self.plan is None or self.plan.det:
+            raise ValueError("SpgemmGraph: no lazy bitmap plan for this product")
+        self.flops = info.flops
+        dev = A.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):   # warm-up outside the capture (allocator, lazy library state)
+            for _ in range(2):
+                warm = _bitmap_launch(A, B, self.plan, True)
+                del warm
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = _bitmap_launch(A, B, self.plan, True)
+
+    def run(self) -> dict:
+        self.graph.replay()
+        return self.out
+
+    def result(self, info: Optional[SpgemmInfo] = None) -> Optional[CSR]:
+        """The last replay's C (one read-back of nnz and error bits)."""
+        info = info if info is not None else SpgemmInfo()
+        C_ = _bitmap_finish(self.A, self.B, self.plan, self.out, info, True)
+        if isinstance(C_, str):
+            raise RuntimeError("SpgemmGraph: B's window segments no longer fit the packed 16-bit lengths")
+        return C_
 
 
 def _det_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:

@@ -140,17 +140,27 @@ def _plan_panels_torch(A: CSR) -> PanelPlan:
 
 def sweep_ok(A: CSR) -> bool:
     """Whether the row-owning sweep kernel (``method="sweep"``,
-    csr_spmm.hip spmm_sweep) can take A on this GPU: its resident grid holds
-    every row (<= 16 rows per wave) and no wave's rows hold more entries than
-    its LDS stage.  One read-back; done once per operand (an inspector step,
-    like :func:`plan_panels`)."""
+    csr_spmm.hip spmm_sweep) can take A on this GPU: every row's columns are
+    non-decreasing (the kernel splits a row into column slices by counting
+    its entries below each slice boundary, which assumes sorted columns; CSR
+    does not guarantee that), its resident grid holds every row (<= 16 rows
+    per wave) and no wave's rows hold more entries than its LDS stage.  One
+    read-back; done once per operand (an inspector step, like
+    :func:`plan_panels`)."""
     if A.device.type != "cuda" or A.m == 0:
         return False
     cached = getattr(A, "_sweep_ok", None)
     if cached is not None:
         return cached
-    A._sweep_ok = _sweep_fits(A)
+    A._sweep_ok = _cols_nondecreasing(A) and _sweep_fits(A)
     return A._sweep_ok
+
+
+def _cols_nondecreasing(A: CSR) -> bool:
+    if A.nnz < 2:
+        return True
+    code = A.row_ids() * A.n + A.col.long()
+    return bool((code[1:] >= code[:-1]).all())
 
 
 def _sweep_fits(A: CSR) -> bool:

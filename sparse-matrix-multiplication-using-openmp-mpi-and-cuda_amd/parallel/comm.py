@@ -222,13 +222,30 @@ class Comm:
             dist.destroy_process_group()
 
 
-def init(backend: str = "auto", device: str = "auto", timeout_s: float = 600.0) -> Comm:
+def init(backend: str = "auto", device: str = "auto", timeout_s: Optional[float] = None) -> Comm:
     """Create the process group for this launch.
 
     backend: ``auto`` (nccl when GPUs are visible, else gloo), ``nccl``,
     ``gloo``.  device: ``auto`` (cuda:LOCAL_RANK when available, else cpu),
     ``cuda`` or ``cpu``.
+
+    timeout_s (default ``CONFIG.comm_timeout_s``, env ``SPMM_COMM_TIMEOUT``,
+    120 s): a collective that has not completed by then raises (gloo) or
+    aborts the communicator and the process (RCCL watchdog), so a stuck rank
+    names itself instead of hanging the job past a launcher's silence window.
+    The reference's blocking MPI calls have no timeout at all
+    (sparse_matrix_mult.cu:474-537).
+
+    Single-node jobs rendezvous on the loopback interface: gloo binds to
+    ``lo`` (``GLOO_SOCKET_IFNAME``) unless the caller chose an interface,
+    because its default resolves the host name, which a container may not
+    resolve or may map to an address its peers cannot reach (a pair connect
+    then waits out the whole timeout).
     """
+    from ..utils.config import CONFIG
+
+    if timeout_s is None:
+        timeout_s = CONFIG.comm_timeout_s
     rank, world, local = launcher_env()
     use_gpu = torch.cuda.is_available() if device == "auto" else device.startswith("cuda")
     if use_gpu:
@@ -245,6 +262,9 @@ def init(backend: str = "auto", device: str = "auto", timeout_s: float = 600.0) 
         backend = "nccl" if use_gpu else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
+    if backend == "gloo" and os.environ["MASTER_ADDR"] in ("127.0.0.1", "localhost") and \
+            not os.environ.get("GLOO_SOCKET_IFNAME"):
+        os.environ["GLOO_SOCKET_IFNAME"] = "lo"
     kw = dict(backend=backend, rank=rank, world_size=world,
               timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":

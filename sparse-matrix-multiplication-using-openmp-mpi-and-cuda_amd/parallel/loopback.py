@@ -126,11 +126,14 @@ class LoopbackComm(Comm):
     def all_gather_async(self, t: torch.Tensor) -> Callable[[], torch.Tensor]:
         flat = t.reshape(-1)
         dev = t.device
-        got = self._post(_mark(flat))
+        # posted as a copy: a rank returns once every rank has POSTED, not once
+        # every peer has read, so the caller may reuse its buffer right away
+        # (RCCL's stream-ordered collective gives the caller the same freedom)
+        got = self._post(_mark(flat.clone()))
         return lambda: torch.cat([_take(x, dev) for x in got()])
 
     def all_to_all_v(self, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
-        got = self._exchange((_mark(x), list(send)))
+        got = self._exchange((_mark(x.clone()), list(send)))   # (a copy: see all_gather_async)
         parts = []
         for src, (item, ssend) in enumerate(got):
             off = sum(ssend[:self.rank])

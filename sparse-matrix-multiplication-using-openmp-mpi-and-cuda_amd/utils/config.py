@@ -45,21 +45,17 @@ class Config:
     # its window configuration (csr_spgemm_bitmap.hip kCfgs), -1 = chosen from the row statistics
     spgemm_bitmap_cfg: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CFG", -1, int))
     # row-major numeric kernel of the bitmap path (a row's windows back to back, <= 8 windows):
-    # "auto" = for the widest-window configuration, "on", "off"
+    # "auto" = for the widest-window configurations (0, 3), "on", "off" (per-unit kernel)
     spgemm_bitmap_rows: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_ROWS", "auto", str))
     # row-major numeric kernel reads an interleaved (column, value) copy of B (1) or the two arrays (0)
     spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
-    # fused row kernel on the bitmap path (count phase + row look-back inside the numeric kernel, no
-    # count kernel, C allocated at the product-count bound): "auto" = where the row kernel is the
-    # default (widest windows), "on" = whenever the row kernels run, "off"
-    spgemm_bitmap_fused: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_FUSED", "off", str))
+    # ... with every (row, window) segment of those pairs starting on a 128-byte line (1) or packed (0)
+    spgemm_bitmap_pad: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_PAD", 1, int))
     # bitmap path: C allocated at the product-count bound and the nnz read back once, after the
     # numeric kernels (1), or C allocated exactly after a read-back between count and numeric (0,
     # default: the two measure the same, 64k 1.564 vs 1.567 ms, 1M 75.7-76.0 vs 75.7-76.1 ms)
     spgemm_bitmap_lazy: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_LAZY", 0, int))
-    # per-unit numeric kernel reads B as interleaved (column, value) pairs (one 8-byte load per product)
-    spgemm_bitmap_unit_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_UNIT_CV", 0, int))
-    # windows per row-major count unit (1: 16 KB bitmaps, 8 per CU; 2: 32 KB, 4 per CU)
+    # windows per row-major count unit (1, 2 or 4; cfg 0: 1 = 16 KB bitmaps, 8 per CU; 2 = 32 KB, 4 per CU)
     spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
     # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU
     # engine) on the bitmap-rank path: 0 = off, 1 = on (other GPU paths stay unordered), 2 = strict
@@ -76,7 +72,8 @@ class Config:
     # (65536^2 @ 0.1 % x 128 cols, BASELINE config 3, which names the MFMA path)
     # the two kernels are within 5 %: MFMA 149 us, row kernel 142 us (PERF_LOG)
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.0, float))
-    comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))
+    # seconds before a pending collective raises / aborts (below the launchers' ~180 s silence window)
+    comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 120.0, float))
 
     def as_dict(self) -> dict:
         return {f.name: getattr(self, f.name) for f in fields(self)}

@@ -51,3 +51,25 @@ def test_a4_cli_loopback(tmp_path):
     assert r.stdout.count("multiplying") == 8 and r.stdout.count("time taken") == 4
     with open(out) as f:
         assert f.read() == golden.to_text(golden.chain([golden.from_bsr(m) for m in mats], p=4))
+
+
+def test_loopback_collectives_let_the_caller_reuse_its_buffer():
+    """A rank may overwrite its input as soon as a collective returns (as
+    under RCCL's stream order): peers still receive the posted values."""
+    import torch
+
+    def body(comm):
+        x = torch.full((4,), float(comm.rank))
+        fin = comm.all_gather_async(x)
+        x.fill_(-1.0)   # reuse right after posting
+        g = fin()
+        y = torch.arange(2 * comm.world, dtype=torch.float32) + 10 * comm.rank
+        out = comm.all_to_all_v(y, [2] * comm.world, [2] * comm.world)
+        y.fill_(-1.0)
+        comm.barrier()
+        return g, out
+
+    res = run_loopback(3, body, timeout_s=30)
+    for r, (g, out) in enumerate(res):
+        assert torch.equal(g, torch.tensor([0.0] * 4 + [1.0] * 4 + [2.0] * 4))
+        assert torch.equal(out, torch.tensor([10.0 * s + 2 * r + i for s in range(3) for i in range(2)]))

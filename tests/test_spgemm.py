@@ -582,52 +582,46 @@ def test_spgemm_gpu_bitmap_matches_binned(monkeypatch, cfg, m, k, n, da, db):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("num,count", [(1, 2), (2, 4), (3, 1)])
-def test_spgemm_gpu_bitmap_window_passes(monkeypatch, num, count):
-    """Window-major launches of the row kernels (SPMM_BM_NUM_PASS_WINDOWS /
-    SPMM_BM_COUNT_PASS_WINDOWS; 5 windows per row, so passes end ragged) give
-    the single-launch product exactly."""
+@pytest.mark.parametrize("count_windows,n", [(2, 700000), (4, 700000), (2, 1 << 20), (4, 1 << 20)])
+def test_spgemm_gpu_bitmap_wide_windows(monkeypatch, count_windows, n):
+    """cfg 3 (2^18-column windows, 512-thread row kernel, the 1M config's
+    pick): ragged last window (n = 700000: 3 windows, the count unit's second
+    window past the end), count units of 2 and 4 windows, n below one window."""
+    from spmm_amd.utils.config import CONFIG
+
     dev = torch.device("cuda")
-    A = gen_csr.uniform_csr(1500, 20000, 0.002, seed=95, device=dev)
-    B = gen_csr.uniform_csr(20000, 600000, 1.4e-4, seed=96, device=dev)
-    C1 = SG.spgemm(A, B)
-    monkeypatch.setenv("SPMM_BM_NUM_PASS_WINDOWS", str(num))
-    monkeypatch.setenv("SPMM_BM_COUNT_PASS_WINDOWS", str(count))
-    info = SG.SpgemmInfo()
-    C2 = SG.spgemm(A, B, info)
-    assert info.rows_per_bin_num.get("bitmap_rows") == 1
-    assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
-    # (duplicates are summed with LDS float atomics: the order, and so the last bit, may differ run to run)
-    assert torch.allclose(C1.val, C2.val, atol=1e-6, rtol=1e-5)
+    A = gen_csr.uniform_csr(3000, 20000, 0.004, seed=61, device=dev)
+    B = gen_csr.uniform_csr(20000, n, 100.0 / n, seed=62, device=dev)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_count_windows", count_windows)
+    info = _bitmap_vs_binned(monkeypatch, A, B, 3)
+    assert info.rows_per_bin_num.get("bitmap_cfg") == 3 and info.rows_per_bin_num.get("bitmap_rows") == 1, \
+        info.rows_per_bin_num
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows", ["pipe", "nopipe", "off"])
-def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows):
-    """The three numeric kernels of the widest-window configuration on a
-    product with 5 windows per row (ragged last window): software-pipelined
-    row-major, row-major, per-unit; all equal the binned path."""
+@pytest.mark.parametrize("rows,pad", [("on", 1), ("on", 0), ("off", 1)])
+def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows, pad):
+    """The two numeric kernels of the widest-window configuration on a
+    product with 5 windows per row (ragged last window): row-major (reading
+    B's pairs with every window segment padded to a 128-byte line, or
+    packed) and per-unit; all equal the binned path."""
     from spmm_amd.utils.config import CONFIG
 
     dev = torch.device("cuda")
     A = gen_csr.uniform_csr(1500, 20000, 0.002, seed=95, device=dev)
     B = gen_csr.uniform_csr(20000, 600000, 1.4e-4, seed=96, device=dev)
     monkeypatch.setattr(CONFIG, "spgemm_bitmap_rows", rows)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_pad", pad)
     info = _bitmap_vs_binned(monkeypatch, A, B, 0)
-    assert info.rows_per_bin_num.get("bitmap_rows", 0) == {"pipe": 2, "nopipe": 1, "off": 0}[rows]
+    assert info.rows_per_bin_num.get("bitmap_rows", 0) == {"on": 1, "off": 0}[rows]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["uniform", "empty_rows", "deferred", "tiny", "off"])
-def test_spgemm_gpu_bitmap_fused(monkeypatch, case):
-    """Fused row kernel (each workgroup counts its row, then a decoupled
-    look-back over rows gives its start in C; C allocated at the product
-    bound, no count kernel) equals the binned path: 20000 rows (look-back
-    over many 64-row rounds), runs of empty rows (rows that never reach pass
-    1), units deferred to the reload kernel (which reads the offsets the fused
-    kernel wrote), a 5-row product, and the knob off (two-kernel path)."""
-    from spmm_amd.utils.config import CONFIG
-
+@pytest.mark.parametrize("case", ["uniform", "empty_rows", "deferred", "tiny"])
+def test_spgemm_gpu_bitmap_row_kernel_cases(monkeypatch, case):
+    """Row count + row-major numeric kernels equal the binned path: 20000
+    rows (many rows per workgroup), runs of empty rows (rows that never reach
+    pass 1), units deferred to the reload kernel, and a 5-row product."""
     dev = torch.device("cuda")
     k, n = 20000, 600000
     if case == "deferred":
@@ -649,9 +643,8 @@ def test_spgemm_gpu_bitmap_fused(monkeypatch, case):
     else:
         A = gen_csr.uniform_csr(5 if case == "tiny" else 20000, k, 0.002, seed=97, device=dev)
         B = gen_csr.uniform_csr(k, n, 1.4e-4, seed=98, device=dev)
-    monkeypatch.setattr(CONFIG, "spgemm_bitmap_fused", "off" if case == "off" else "on")
     info = _bitmap_vs_binned(monkeypatch, A, B, 0)
-    assert info.rows_per_bin_num.get("bitmap_fused", 0) == (0 if case == "off" else 1)
+    assert info.rows_per_bin_num.get("bitmap_rows", 0) == 1
     if case == "deferred":
         assert info.rows_per_bin_num["bitmap_deferred"] >= 16
 
@@ -1150,3 +1143,23 @@ def test_spgemm_bench_scale_deterministic_bitwise(monkeypatch):
     torch.cuda.empty_cache()
     C = SG.spgemm(A, B)
     assert torch.equal(C.rowptr, rp1) and _digest(C.col) == dc1 and _digest(C.val) == d1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d", [(65536, 1e-3), (300000, 3e-4)])
+def test_spgemm_graph_replay_matches_eager(n, d):
+    """SpgemmGraph (the bitmap product captured into one HIP graph, no host
+    sync inside, C at the product bound) gives the eager product on every
+    replay, and reports the same nnz."""
+    dev = torch.device("cuda")
+    A = gen_csr.uniform_csr(n, n, d, seed=3, device=dev)
+    B = gen_csr.uniform_csr(n, n, d, seed=4, device=dev)
+    C1 = SG.spgemm(A, B)
+    g = SG.SpgemmGraph(A, B)
+    for _ in range(2):
+        g.run()
+        info = SG.SpgemmInfo()
+        C2 = g.result(info)
+        assert info.nnz == C1.nnz
+        assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+        assert torch.allclose(C1.val, C2.val, atol=1e-6, rtol=1e-5)

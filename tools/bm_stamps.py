@@ -10,8 +10,11 @@ import os  # noqa: E402
 # the stamps are compiled in only in a diagnostic variant of the library
 from spmm_amd import _build  # noqa: E402
 
-os.environ["SPMM_HIP_LIB"] = _build.build_hip(out=os.path.join(_build.LIB_DIR, "diag", "libspmm_hip_stamps.so"),
-                                              extra=["-DSPMM_BM_STAMPS"])
+_stamps_lib = os.path.join(_build.LIB_DIR, "diag", "libspmm_hip_stamps.so")
+if os.environ.get("SPMM_STAMPS_PREBUILT") and os.path.exists(_stamps_lib):   # built on the CPU host beforehand
+    os.environ["SPMM_HIP_LIB"] = _stamps_lib
+else:
+    os.environ["SPMM_HIP_LIB"] = _build.build_hip(out=_stamps_lib, extra=["-DSPMM_BM_STAMPS"])
 import torch  # noqa: E402
 
 import spmm_amd  # noqa: E402,F401
