@@ -1519,7 +1519,8 @@ __global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ val, int64_t mb, int nwin,
                                                     const int64_t* __restrict__ pbase, uint4* __restrict__ ws8,
                                                     uint2* __restrict__ out, const int64_t* __restrict__ cbase,
-                                                    int gc, int32_t* __restrict__ outc) {
+                                                    int gc, int32_t* __restrict__ outc, int64_t cap, int64_t cap_c,
+                                                    int32_t* __restrict__ err) {
   const int lane = threadIdx.x & 63;
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (j >= mb) return;
@@ -1541,15 +1542,46 @@ __global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__
   const uint32_t g1 = (uint32_t)__shfl(w, (lane + 1) * gc < nwin ? (lane + 1) * gc : nwin);
   const uint32_t rc = lane < ng ? ((g1 - g0 + (1u << kPadCLg) - 1) >> kPadCLg) << kPadCLg : 0u;
   const uint32_t pc = (uint32_t)bm_wave_incl((int)rc) - rc;
-  const uint32_t r0 = __builtin_amdgcn_readfirstlane(w), r1 = __builtin_amdgcn_readlane(w, nwin);
+  // every bound into wave-uniform registers BEFORE the entry loop: a lane
+  // shuffle inside it would read lanes that have left the loop (their values
+  // are not delivered), so short rows would scatter to wrong places
+  uint32_t wb[9], pw[8], pg[8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wb[k] = __builtin_amdgcn_readlane(w, k);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    pw[k] = __builtin_amdgcn_readlane(ps, k);
+    pg[k] = __builtin_amdgcn_readlane(pc, k);
+  }
+  const uint32_t r0 = wb[0], r1 = __builtin_amdgcn_readlane(w, nwin);
   for (uint32_t e = r0 + lane; e < r1; e += 64) {
     int q = 0;
-    for (int k = 1; k < nwin; ++k) q += e >= (uint32_t)__shfl(w, k) ? 1 : 0;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) q += (k < nwin && e >= wb[k]) ? 1 : 0;
+    uint32_t sw = 0, sp = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k == q) {
+        sw = wb[k];
+        sp = pw[k];
+      }
     const uint32_t c = (uint32_t)col[e];
-    if (out) out[base + (uint32_t)__shfl(ps, q) + (e - (uint32_t)__shfl(w, q))] = make_uint2(c, val[e]);
+    if (out) {
+      const int64_t d = base + sp + (e - sw);
+      if (d < cap) out[d] = make_uint2(c, val[e]);
+      else atomicOr(err, 32);   // (a layout bug, never a write out of bounds)
+    }
     if (outc) {
-      const int g = q / gc;
-      outc[cb + (uint32_t)__shfl(pc, g) + (e - (uint32_t)__shfl(w, g * gc))] = (int32_t)c;
+      const int g = q / gc, gi = g * gc;
+      uint32_t gw = 0, gp = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (k == gi) gw = wb[k];
+        if (k == g) gp = pg[k];
+      }
+      const int64_t d = cb + gp + (e - gw);
+      if (d < cap_c) outc[d] = (int32_t)c;
+      else atomicOr(err, 32);
     }
   }
 }
@@ -1873,13 +1905,17 @@ SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin
 // count kernel with count groups of gc windows padded to 32 columns (pad = 1
 // to it; cbase = exclusive scan of plen_c); totals < 2^32.  Also stores each
 // row's bases in ws8.
+// cap / cap_c: entries allocated for out / outc; err bit 5 if a row would
+// not fit (a layout invariant; nothing is written out of bounds).
 SPMM_EXPORT int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb,
                                          int nwin, const int64_t* pbase, void* ws8, void* out, const int64_t* cbase,
-                                         int gc, int32_t* outc, void* stream) {
+                                         int gc, int32_t* outc, int64_t cap, int64_t cap_c, int32_t* err,
+                                         void* stream) {
   if (mb <= 0) return 0;
-  if (nwin < 1 || nwin > 8 || gc < 1 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  if (nwin < 1 || nwin > 8 || gc < 1 || gc > 8 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX)
+    return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bm_pad_pairs, dim3((unsigned)((mb * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, col,
-                     (const uint32_t*)val, mb, nwin, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc);
+                     (const uint32_t*)val, mb, nwin, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc, cap, cap_c, err);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -27,7 +27,7 @@
 //   --metrics-json PATH   rank-0 JSON with phase times, tile pairs, bytes
 //   --save-partials DIR   write this rank's partial product (checkpoint)
 //   --load-partials DIR   resume from saved partials, skipping load + local tree
-//   --timeout S           RCCL transfer timeout (fail fast, default 600)
+//   --timeout S           RCCL transfer timeout (fail fast, default 120)
 //   --no-split            cross-rank products on one rank each (no row-panel split)
 //   --format ref|mtx      input format: the reference folder (default) or a
 //                         chain of Matrix Market files / a folder of them
@@ -62,7 +62,7 @@ struct Options {
   std::vector<std::string> inputs;
   int threads = 0, streams = 4;
   bool quiet = false, dump = false, split = true, fast = false;
-  double timeout = 600.0;
+  double timeout = 120.0;
 };
 
 [[noreturn]] void usage(const char* why) {
@@ -809,6 +809,8 @@ int run(const Options& o, int rank, int world, double t_start) {
     m.threads = o.threads;
     m.local_rank = local_rank();
     m.quiet = o.quiet;
+    m.comm = o.comm;
+    m.timeout = o.timeout;
     return run_mtx(m, rank, world);
   }
   // size file: "N k" (:412-418)

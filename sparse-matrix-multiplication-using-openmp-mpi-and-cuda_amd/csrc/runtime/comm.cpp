@@ -88,6 +88,34 @@ class MpiComm : public Comm {
     if (r_ != ncclSuccess) throw ::a4::Error(std::string("RCCL error ") + ncclGetErrorString(r_) + " in " #call); \
   } while (0)
 
+}  // namespace
+
+void Comm::allgatherv_dev(const void* send, void* recv, const std::vector<size_t>& bytes, hipStream_t s) {
+  size_t tot = 0;
+  for (size_t b : bytes) tot += b;
+  std::vector<char> h(std::max<size_t>(tot, 1));
+  size_t at = 0;
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_ && bytes[r]) A4_HIP(hipMemcpyAsync(h.data() + at, send, bytes[r], hipMemcpyDeviceToHost, s));
+    at += bytes[r];
+  }
+  A4_HIP(hipStreamSynchronize(s));
+  at = 0;
+  for (int r = 0; r < world_; ++r) {
+    for (size_t o = 0; o < bytes[r]; o += (size_t(1) << 30)) {
+      const size_t n = std::min(bytes[r] - o, size_t(1) << 30);
+      A4_MPI(MPI_Bcast(h.data() + at + o, (int)n, MPI_BYTE, r, MPI_COMM_WORLD));
+    }
+    at += bytes[r];
+  }
+  if (tot) A4_HIP(hipMemcpyAsync(recv, h.data(), tot, hipMemcpyHostToDevice, s));
+  A4_HIP(hipStreamSynchronize(s));
+  bytes_recv += tot - bytes[rank_];
+  bytes_sent += bytes[rank_];
+}
+
+namespace {
+
 class RcclComm : public Comm {
  public:
   explicit RcclComm(double timeout_s) : timeout_s_(timeout_s) {
@@ -200,6 +228,19 @@ class RcclComm : public Comm {
   Mat recv_host(int src) override {
     DevMat d = recv_dev(src, own_);
     return dev_download(d, own_);
+  }
+  void allgatherv_dev(const void* send, void* recv, const std::vector<size_t>& bytes, hipStream_t s) override {
+    maybe_inject_fault("send");
+    size_t at = 0;
+    A4_NCCL(ncclGroupStart());
+    for (int r = 0; r < world_; ++r) {
+      if (bytes[r]) A4_NCCL(ncclBroadcast(send, (char*)recv + at, bytes[r], ncclUint8, r, comm_, s));
+      at += bytes[r];
+    }
+    A4_NCCL(ncclGroupEnd());
+    wait(s);
+    bytes_recv += at - bytes[rank_];
+    bytes_sent += bytes[rank_] * (world_ - 1);
   }
   void barrier() override { A4_MPI(MPI_Barrier(MPI_COMM_WORLD)); }
   double allreduce_max(double x) override {

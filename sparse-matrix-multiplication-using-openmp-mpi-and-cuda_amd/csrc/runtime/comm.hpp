@@ -54,6 +54,11 @@ class Comm {
     for (int r : srcs) out.push_back(recv_host(r));
     return out;
   }
+  // all-gather of variable-size device byte buffers: rank r's `send` lands at
+  // recv + (bytes[0] + .. + bytes[r - 1]).  Default: staged through host
+  // memory with MPI broadcasts (1 GiB pieces, no 2^31 count limit); RCCL:
+  // one grouped set of device broadcasts over xGMI and a bounded wait.
+  virtual void allgatherv_dev(const void* send, void* recv, const std::vector<size_t>& bytes, hipStream_t s);
   virtual void barrier() = 0;
   virtual double allreduce_max(double x) = 0;
   virtual void abort(int code) = 0;

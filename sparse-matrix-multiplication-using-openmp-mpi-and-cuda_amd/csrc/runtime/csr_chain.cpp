@@ -14,11 +14,14 @@
 //             entries past it are ignored); entries go to their row owner
 //             (MPI_Alltoallv), which builds its CSR row panel (sorted,
 //             duplicates summed in fp32, symmetric storage expanded)
-//   multiply  the right factor's row panels are all-gathered (MPI), the
-//             local panel product runs on the GPU's bitmap-rank kernels
-//             (csr_spgemm_bitmap.hip, through their C ABI: window splits ->
-//             count -> scan -> numeric) when the product fits them, else on
-//             the OpenMP Gustavson engine (libspmm_host)
+//   multiply  device-resident (GPU): each factor's row panel is uploaded once,
+//             the right factor's panels are all-gathered device to device
+//             (RCCL broadcasts over xGMI; --comm mpi stages through host MPI),
+//             and the running product's row panel never leaves HBM between
+//             products: csr_engine.cpp runs the bitmap-rank kernels for
+//             uniform products and the binned LDS + long-row kernels for
+//             skewed ones (R-MAT hubs), so no product falls back to the CPU.
+//             --device cpu: the OpenMP Gustavson engine (libspmm_host).
 //   write     C's panels go to rank 0 point to point, in rank order, and are
 //             appended to the output as they arrive (spmm_mtx_write_*)
 // stdout: "multiplying i i+1" per product (rank 0) and "time taken" per rank.
@@ -33,7 +36,9 @@
 #include <regex>
 #include <sstream>
 
+#include "comm.hpp"
 #include "csr_chain.hpp"
+#include "csr_engine.hpp"
 #include "rt.hpp"
 
 extern "C" {
@@ -53,27 +58,9 @@ int64_t spmm_cpu_csr_spgemm_symbolic(int64_t m, int64_t n, const int64_t* Arp, c
 int spmm_cpu_csr_spgemm_numeric(int64_t m, int64_t n, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* Crp,
                                 int32_t* Cci, float* Cv, int nthreads);
-// libspmm_hip.so (csr_spgemm_bitmap.hip, prim.hip)
-int spmm_spgemm_bm_config(int cfg, int* lgw, int* nsub_count, int* pcap_fast, int* rounds_fast, int* reload_rows);
-int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin, uint32_t* ws,
-                          void* stream);
-int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const uint32_t* ws, const int32_t* Bci,
-                         int64_t m, int nwin, int lg, int32_t* ucnt, int32_t* err, void* stream);
-int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av, const uint32_t* ws,
-                           const int32_t* Bci, const float* Bv, int64_t m, int nwin, int lg, const int64_t* uoff,
-                           int64_t cap, int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                           int32_t* err, int det, void* stream);
 }
 
 namespace a4 {
-
-struct Csr {
-  int64_t m = 0, n = 0;
-  std::vector<int64_t> rp{0};
-  std::vector<int32_t> ci;
-  std::vector<float> v;
-  int64_t nnz() const { return (int64_t)ci.size(); }
-};
 
 namespace {
 
@@ -266,94 +253,71 @@ Csr cpu_spgemm(const Csr& A, const Csr& B, int nthreads) {
   return C;
 }
 
-template <typename T>
-DevBuf<T> upload(const std::vector<T>& h, hipStream_t s) {
-  DevBuf<T> d(std::max<size_t>(h.size(), 1), s);
-  if (!h.empty()) A4_HIP(hipMemcpyAsync(d.get(), h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
-  return d;
+// Every rank's device row panel of B, concatenated in rank order: the row
+// counts through host MPI (small), columns and values device to device
+// (Comm::allgatherv_dev: RCCL broadcasts over xGMI).
+DCsr allgather_rows_dev(const DCsr& panel, Comm& comm, hipStream_t s) {
+  const int world = comm.world();
+  if (world == 1) {
+    DCsr B;
+    B.m = panel.m;
+    B.n = panel.n;
+    B.nnz = panel.nnz;
+    B.rp = DevBuf<int64_t>(panel.m + 1, s);
+    B.ci = DevBuf<int32_t>(std::max<int64_t>(panel.nnz, 1), s);
+    B.v = DevBuf<float>(std::max<int64_t>(panel.nnz, 1), s);
+    A4_HIP(hipMemcpyAsync(B.rp.get(), panel.rp.get(), (panel.m + 1) * 8, hipMemcpyDeviceToDevice, s));
+    if (panel.nnz) {
+      A4_HIP(hipMemcpyAsync(B.ci.get(), panel.ci.get(), panel.nnz * 4, hipMemcpyDeviceToDevice, s));
+      A4_HIP(hipMemcpyAsync(B.v.get(), panel.v.get(), panel.nnz * 4, hipMemcpyDeviceToDevice, s));
+    }
+    return B;
+  }
+  const int64_t mine[2] = {panel.m, panel.nnz};
+  std::vector<int64_t> meta(2 * world);
+  MPI_Allgather(mine, 2, MPI_INT64_T, meta.data(), 2, MPI_INT64_T, MPI_COMM_WORLD);
+  std::vector<int> cm(world), dm(world);
+  int64_t M = 0, E = 0;
+  std::vector<size_t> cb(world);
+  for (int r = 0; r < world; ++r) {
+    A4_CHECK(M + meta[2 * r] < INT32_MAX, "right factor has too many rows");
+    cm[r] = (int)meta[2 * r];
+    dm[r] = (int)M;
+    M += meta[2 * r];
+    cb[r] = (size_t)meta[2 * r + 1] * 4;
+    E += meta[2 * r + 1];
+  }
+  std::vector<int64_t> rp_local(panel.m + 1);
+  A4_HIP(hipMemcpyAsync(rp_local.data(), panel.rp.get(), (panel.m + 1) * 8, hipMemcpyDeviceToHost, s));
+  A4_HIP(hipStreamSynchronize(s));
+  std::vector<int64_t> cnt(panel.m), all(M);
+  for (int64_t i = 0; i < panel.m; ++i) cnt[i] = rp_local[i + 1] - rp_local[i];
+  MPI_Allgatherv(cnt.data(), (int)panel.m, MPI_INT64_T, all.data(), cm.data(), dm.data(), MPI_INT64_T, MPI_COMM_WORLD);
+  std::vector<int64_t> rp(M + 1, 0);
+  for (int64_t i = 0; i < M; ++i) rp[i + 1] = rp[i] + all[i];
+  DCsr B;
+  B.m = M;
+  B.n = panel.n;
+  B.nnz = E;
+  B.rp = DevBuf<int64_t>(M + 1, s);
+  A4_HIP(hipMemcpyAsync(B.rp.get(), rp.data(), (M + 1) * 8, hipMemcpyHostToDevice, s));
+  B.ci = DevBuf<int32_t>(std::max<int64_t>(E, 1), s);
+  B.v = DevBuf<float>(std::max<int64_t>(E, 1), s);
+  comm.allgatherv_dev(panel.ci.get(), B.ci.get(), cb, s);
+  comm.allgatherv_dev(panel.v.get(), B.v.get(), cb, s);
+  return B;
 }
 
-int group_log2(double seg) { return seg >= 40 ? 6 : (seg >= 16 ? 5 : 4); }   // ops/spgemm.py _group_log2
-
-// The bitmap-rank path of ops/spgemm.py (onepass_bitmap, per-unit kernels)
-// from C++: false when the product does not fit it (the caller runs the CPU
-// engine).
-bool gpu_spgemm(const Csr& A, const Csr& B, hipStream_t s, Csr* out) {
-  if (A.m == 0 || A.nnz() == 0 || B.nnz() == 0) return false;
-  if (B.nnz() >= (int64_t(1) << 31) || B.n >= (int64_t(1) << 30) || A.nnz() >= (int64_t(1) << 31)) return false;
-  // product statistics on the host (the operands are host-resident here)
-  int64_t tot = 0, nz = 0, mx = 0, amax = 0;
-  for (int64_t i = 0; i < A.m; ++i) {
-    int64_t p = 0;
-    for (int64_t e = A.rp[i]; e < A.rp[i + 1]; ++e) p += B.rp[A.ci[e] + 1] - B.rp[A.ci[e]];
-    tot += p;
-    nz += p > 0;
-    mx = std::max(mx, p);
-    amax = std::max(amax, A.rp[i + 1] - A.rp[i]);
-  }
-  if (tot == 0) return false;
-  const double mean = (double)tot / (double)nz;
-  if (mx > 4 * mean || nz < A.m / 2) return false;   // skewed rows: the binned engine's job (CPU here)
-  int cfg = -1, lgw = 0, nsub = 0, pcap = 0, rounds = 0, reload_rows = 0;
-  for (int c : {0, 2, 1}) {   // widest window whose mean products per window fit 70 % of the fast capacity
-    A4_HIP((hipError_t)spmm_spgemm_bm_config(c, &lgw, &nsub, &pcap, &rounds, &reload_rows));
-    const double W = (double)(int64_t(1) << lgw);
-    if (mean * std::min(W, (double)B.n) / std::max<double>((double)B.n, 1) <= 0.7 * pcap) {
-      cfg = c;
-      break;
-    }
-  }
-  if (cfg < 0) return false;
-  A4_HIP((hipError_t)spmm_spgemm_bm_config(cfg, &lgw, &nsub, &pcap, &rounds, &reload_rows));
-  if (amax > reload_rows) return false;
-  const int nwin = (int)std::max<int64_t>(1, (B.n + (int64_t(1) << lgw) - 1) >> lgw);
-  const int64_t nunits = A.m * nwin;
-  if (nunits >= (int64_t(1) << 31)) return false;
-  const double seg = (double)tot / (double)A.nnz();   // B-segment length per A entry
-  const int lg_count = group_log2(seg * std::min(nsub, nwin) / nwin);
-  const int lg_num = seg / nwin < 48 ? 4 : (seg / nwin < 96 ? 5 : 6);
-  DevBuf<int64_t> Arp = upload(A.rp, s), Brp = upload(B.rp, s);
-  DevBuf<int32_t> Aci = upload(A.ci, s), Bci = upload(B.ci, s);
-  DevBuf<float> Av = upload(A.v, s), Bv = upload(B.v, s);
-  DevBuf<uint32_t> ws((size_t)B.m * (nwin + 1), s);
-  DevBuf<int32_t> ucnt((size_t)nunits, s), err(4, s);
-  DevBuf<int64_t> uoff((size_t)nunits + 1, s);
-  DevBuf<uint8_t> scan_ws(std::max<size_t>(spmm_prim_scan_ws(nunits), 1), s);
-  A4_HIP(hipMemsetAsync(err.get(), 0, 16, s));
-  A4_HIP(hipMemsetAsync(uoff.get(), 0, 8, s));
-  A4_HIP((hipError_t)spmm_spgemm_bm_splits(Brp.get(), Bci.get(), B.m, lgw, nwin, ws.get(), s));
-  A4_HIP((hipError_t)spmm_spgemm_bm_count(cfg, Arp.get(), Aci.get(), ws.get(), Bci.get(), A.m, nwin, lg_count,
-                                          ucnt.get(), err.get(), s));
-  A4_HIP((hipError_t)spmm_prim_scan(ucnt.get(), 4, nunits, uoff.get() + 1, 1, scan_ws.get(), s));
-  int64_t nnz = 0;
-  int32_t e0[2] = {0, 0};
-  A4_HIP(hipMemcpyAsync(&nnz, uoff.get() + nunits, 8, hipMemcpyDeviceToHost, s));
-  A4_HIP(hipMemcpyAsync(e0, err.get(), 8, hipMemcpyDeviceToHost, s));
-  A4_HIP(hipStreamSynchronize(s));
-  if (e0[0] != 0) return false;
-  const int64_t ovf_cap = std::min<int64_t>(nunits, 1 << 20);
-  DevBuf<int32_t> Cci((size_t)std::max<int64_t>(nnz, 1), s), ovf((size_t)ovf_cap, s);
-  DevBuf<float> Cv((size_t)std::max<int64_t>(nnz, 1), s);
-  A4_HIP((hipError_t)spmm_spgemm_bm_numeric(cfg, Arp.get(), Aci.get(), Av.get(), ws.get(), Bci.get(), Bv.get(), A.m,
-                                            nwin, lg_num, uoff.get(), nnz, Cci.get(), Cv.get(), ovf.get(),
-                                            (uint32_t*)(err.get() + 1), ovf_cap, err.get(), 0, s));
-  std::vector<int64_t> uo(nunits + 1);
-  out->m = A.m;
-  out->n = B.n;
-  out->ci.resize(nnz);
-  out->v.resize(nnz);
-  A4_HIP(hipMemcpyAsync(e0, err.get(), 4, hipMemcpyDeviceToHost, s));
-  A4_HIP(hipMemcpyAsync(uo.data(), uoff.get(), uo.size() * 8, hipMemcpyDeviceToHost, s));
-  if (nnz) {
-    A4_HIP(hipMemcpyAsync(out->ci.data(), Cci.get(), nnz * 4, hipMemcpyDeviceToHost, s));
-    A4_HIP(hipMemcpyAsync(out->v.data(), Cv.get(), nnz * 4, hipMemcpyDeviceToHost, s));
-  }
-  A4_HIP(hipStreamSynchronize(s));
-  A4_CHECK((e0[0] & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
-  if (e0[0] & 5) return false;   // a unit beyond the reload kernel's budget
-  out->rp.resize(A.m + 1);
-  for (int64_t i = 0; i <= A.m; ++i) out->rp[i] = uo[i * nwin];
-  return true;
+// Point-to-point transfers in pieces of < 2^31 elements (MPI counts are int).
+constexpr int64_t kMsg = int64_t(1) << 28;
+template <typename T>
+void send_big(const T* p, int64_t n, MPI_Datatype t, int dst, int tag) {
+  for (int64_t o = 0; o < n; o += kMsg) MPI_Send(p + o, (int)std::min(kMsg, n - o), t, dst, tag, MPI_COMM_WORLD);
+}
+template <typename T>
+void recv_big(T* p, int64_t n, MPI_Datatype t, int src, int tag) {
+  for (int64_t o = 0; o < n; o += kMsg)
+    MPI_Recv(p + o, (int)std::min(kMsg, n - o), t, src, tag, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
 }
 
 // Rows row0.. of C from every rank to rank 0, appended to the file in rank order.
@@ -363,10 +327,10 @@ void write_rows(const std::string& path, const Csr& P, int64_t row0, int rank, i
   if (rank != 0) {
     const int64_t hdr[3] = {row0, P.m, P.nnz()};
     MPI_Send(hdr, 3, MPI_INT64_T, 0, 10, MPI_COMM_WORLD);
-    if (P.m) MPI_Send(P.rp.data(), (int)(P.m + 1), MPI_INT64_T, 0, 11, MPI_COMM_WORLD);
+    if (P.m) send_big(P.rp.data(), P.m + 1, MPI_INT64_T, 0, 11);
     if (P.nnz()) {
-      MPI_Send(P.ci.data(), (int)P.nnz(), MPI_INT32_T, 0, 12, MPI_COMM_WORLD);
-      MPI_Send(P.v.data(), (int)P.nnz(), MPI_FLOAT, 0, 13, MPI_COMM_WORLD);
+      send_big(P.ci.data(), P.nnz(), MPI_INT32_T, 0, 12);
+      send_big(P.v.data(), P.nnz(), MPI_FLOAT, 0, 13);
     }
     return;
   }
@@ -381,10 +345,10 @@ void write_rows(const std::string& path, const Csr& P, int64_t row0, int rank, i
     Q.rp.assign(Q.m + 1, 0);
     Q.ci.resize(hdr[2]);
     Q.v.resize(hdr[2]);
-    if (Q.m) MPI_Recv(Q.rp.data(), (int)(Q.m + 1), MPI_INT64_T, r, 11, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+    if (Q.m) recv_big(Q.rp.data(), Q.m + 1, MPI_INT64_T, r, 11);
     if (hdr[2]) {
-      MPI_Recv(Q.ci.data(), (int)hdr[2], MPI_INT32_T, r, 12, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
-      MPI_Recv(Q.v.data(), (int)hdr[2], MPI_FLOAT, r, 13, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+      recv_big(Q.ci.data(), hdr[2], MPI_INT32_T, r, 12);
+      recv_big(Q.v.data(), hdr[2], MPI_FLOAT, r, 13);
     }
     rc = spmm_mtx_write_panel(w, hdr[0], Q.m, Q.rp.data(), Q.ci.data(), Q.v.data(), nthreads);
   }
@@ -402,30 +366,49 @@ int run_mtx(const MtxOptions& o, int rank, int world) {
   const bool gpu = o.device == "hip" || (o.device == "auto" && ndev > 0);
   A4_CHECK(!gpu || ndev > 0, "--device hip but no GPU is visible");
   hipStream_t s = nullptr;
+  std::unique_ptr<Comm> comm;
+  std::string comm_kind = "mpi";
   if (gpu) {
     A4_HIP(hipSetDevice(o.local_rank % ndev));
     A4_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    comm_kind = o.comm;
+    if (comm_kind == "auto") {
+      int local_size = world;
+      if (const char* x = std::getenv("MPI_LOCALNRANKS")) local_size = std::atoi(x);
+      comm_kind = (world > 1 && local_size <= ndev) ? "rccl" : "mpi";
+    }
+    comm = comm_kind == "rccl" ? make_rccl_comm(o.timeout) : make_mpi_comm();
   }
-  int64_t row0 = 0, gpu_products = 0, cpu_products = 0;
+  int64_t row0 = 0, cpu_products = 0;
   int64_t flops = 0;
+  EngineStats es;
   const double t0 = now_s();
   Csr P = read_rowblock(paths[0], rank, world, o.threads, &row0);
+  DCsr Pd;
+  if (gpu) Pd = dcsr_upload(P, s);   // the running product stays in HBM from here on
   for (size_t i = 1; i < paths.size(); ++i) {
     if (rank == 0 && !o.quiet) std::cout << "multiplying " << i << " " << i + 1 << std::endl;
     int64_t brow0 = 0;
     const Csr Bp = read_rowblock(paths[i], rank, world, o.threads, &brow0);
-    const Csr B = allgather_rows(Bp, world);
-    A4_CHECK(B.m == P.n, paths[i] + ": " + std::to_string(B.m) + " rows, the product so far has " +
-                             std::to_string(P.n) + " columns");
-    for (int64_t e = 0; e < P.nnz(); ++e) flops += 2 * (B.rp[P.ci[e] + 1] - B.rp[P.ci[e]]);
-    Csr C;
-    if (gpu && gpu_spgemm(P, B, s, &C)) ++gpu_products;
-    else {
-      C = cpu_spgemm(P, B, o.threads);
+    if (gpu) {
+      const DCsr Bpd = dcsr_upload(Bp, s);
+      const DCsr B = allgather_rows_dev(Bpd, *comm, s);
+      A4_CHECK(B.m == Pd.n, paths[i] + ": " + std::to_string(B.m) + " rows, the product so far has " +
+                               std::to_string(Pd.n) + " columns");
+      int64_t products = 0;
+      DCsr C = dev_spgemm(Pd, B, s, &es, &products);
+      flops += 2 * products;
+      Pd = std::move(C);
+    } else {
+      const Csr B = allgather_rows(Bp, world);
+      A4_CHECK(B.m == P.n, paths[i] + ": " + std::to_string(B.m) + " rows, the product so far has " +
+                               std::to_string(P.n) + " columns");
+      for (int64_t e = 0; e < P.nnz(); ++e) flops += 2 * (B.rp[P.ci[e] + 1] - B.rp[P.ci[e]]);
+      P = cpu_spgemm(P, B, o.threads);
       ++cpu_products;
     }
-    P = std::move(C);
   }
+  if (gpu) P = dcsr_download(Pd, s);
   const double t1 = now_s();
   write_rows(o.out, P, row0, rank, world, o.threads);
   const double t2 = now_s();
@@ -434,10 +417,15 @@ int run_mtx(const MtxOptions& o, int rank, int world) {
   if (rank == 0 && !o.metrics.empty()) {
     std::ofstream m(o.metrics);
     m << "{\"engine\": \"native\", \"format\": \"mtx\", \"device\": \"" << (gpu ? "hip" : "cpu")
+      << "\", \"device_resident\": " << (gpu ? "true" : "false") << ", \"comm\": \"" << comm_kind
       << "\", \"ranks\": " << world << ", \"n_files\": " << paths.size() << ", \"flops\": " << fl_all
-      << ", \"gpu_products\": " << gpu_products << ", \"cpu_products\": " << cpu_products
-      << ", \"t_chain_s\": " << (t1 - t0) << ", \"t_write_s\": " << (t2 - t1) << "}\n";
+      << ", \"gpu_products\": " << (es.bitmap + es.binned) << ", \"gpu_bitmap_products\": " << es.bitmap
+      << ", \"gpu_binned_products\": " << es.binned << ", \"gpu_long_rows\": " << es.long_rows
+      << ", \"cpu_products\": " << cpu_products << ", \"t_chain_s\": " << (t1 - t0)
+      << ", \"t_write_s\": " << (t2 - t1) << "}\n";
   }
+  Pd = DCsr();
+  comm.reset();
   if (s) (void)hipStreamDestroy(s);
   MPI_Barrier(MPI_COMM_WORLD);
   return 0;

@@ -8,8 +8,9 @@ namespace a4 {
 
 struct MtxOptions {
   std::vector<std::string> inputs;   // .mtx files in chain order, or one folder of them
-  std::string out = "matrix.mtx", device = "auto", metrics;
+  std::string out = "matrix.mtx", device = "auto", metrics, comm = "auto";
   int threads = 0, local_rank = 0;
+  double timeout = 120.0;   // bounded RCCL waits
   bool quiet = false;
 };
 

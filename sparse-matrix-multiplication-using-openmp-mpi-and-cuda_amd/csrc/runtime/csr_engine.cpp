@@ -1,0 +1,414 @@
+// Device-resident CSR SpGEMM for the native Matrix-Market chain (see
+// csr_engine.hpp).  Host orchestration of the gfx950 kernels, mirroring
+// ops/spgemm.py: the row plan (one 16-word read-back) picks the bitmap-rank
+// path for uniform products; everything else takes the binned two-phase path
+// (LDS tables by product count, hub rows through the long-row pipeline), so
+// no product falls back to the CPU.  Per-row host arrays (product counts,
+// flags, the long rows' chunk counts) are the only device->host traffic.
+#include "csr_engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+
+extern "C" {
+// csr_spgemm.hip
+int spmm_spgemm_row_plan(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, int64_t m, int64_t cap1,
+                         int64_t cap2, int64_t cap4, int64_t esc_min, int64_t* nprod, int64_t* nsl, int64_t* part,
+                         int64_t* stats, void* stream);
+int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int ncols, int64_t* bsplit,
+                           void* stream);
+int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av, const int64_t* Brp,
+                    const int32_t* Bci, const float* Bv, const int64_t* bsplit, const int32_t* rows, int64_t nrows,
+                    int ncols, int lg, int32_t* row_nnz, int32_t* out_nnz, const int64_t* Crp, int32_t* Cci, float* Cv,
+                    int32_t* flags, void* stream);
+int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp, const int32_t* Bci,
+                           const float* Bv, const int64_t* wg_e0, const int64_t* wg_e1, int64_t nwg, int nch,
+                           int32_t* wg_hist, const int32_t* wg_row, const int64_t* row_off, void* scratch,
+                           const int32_t* lidx, const uint32_t* btab, int32_t* wg_dhist, int32_t* wg_nlong,
+                           const uint8_t* rt_mode, void* dl, const int64_t* dl_off, void* stream);
+int spmm_spgemm_long_wg_scan(int32_t* wg_hist, const int64_t* wg0, const int64_t* nwg, int64_t R, int nch,
+                             int64_t* cnt, const int32_t* dhist, int64_t* dcnt, uint8_t* mode, void* stream);
+int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_cnt, int64_t nrt, int nch,
+                           void* scratch, int64_t* rt_nnz, int32_t* ws, const int64_t* dt_cnt, const void* dl,
+                           const int64_t* dl_rp, const uint32_t* btab, const int32_t* Bci, const float* Bv,
+                           void* stream);
+int spmm_spgemm_long_place(const int64_t* src, const int64_t* dst, const int64_t* cnt, int64_t nrt,
+                           const void* scratch, int32_t* Cci, float* Cv, void* stream);
+int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch);
+// csr_spgemm_bitmap.hip
+int spmm_spgemm_bm_config(int cfg, int* lgw, int* nsub_count, int* pcap_fast, int* rounds_fast, int* reload_rows);
+int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin, uint32_t* ws,
+                          void* stream);
+int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const uint32_t* ws, const int32_t* Bci,
+                         int64_t m, int nwin, int lg, int32_t* ucnt, int32_t* err, void* stream);
+int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av, const uint32_t* ws,
+                           const int32_t* Bci, const float* Bv, int64_t m, int nwin, int lg, const int64_t* uoff,
+                           int64_t cap, int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
+                           int32_t* err, int det, void* stream);
+}
+
+namespace a4 {
+
+namespace {
+
+// ops/spgemm.py constants (LOAD, ESC_MIN, ESC_PCAP, ESC_LOAD, GLOBAL_WS_BYTES)
+constexpr double kLoad = 0.5, kEscLoad = 0.9;
+constexpr int64_t kEscMin = 2048, kEscPcap = 7680, kPlanBlocks = 1024, kPlanStats = 16;
+constexpr int64_t kWsProducts = (int64_t(8) << 30) / 8;
+
+template <typename T>
+DevBuf<T> up(const std::vector<T>& h, hipStream_t s) {
+  DevBuf<T> d(std::max<size_t>(h.size(), 1), s);
+  if (!h.empty()) A4_HIP(hipMemcpyAsync(d.get(), h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  return d;
+}
+
+template <typename T>
+std::vector<T> down(const T* d, size_t n, hipStream_t s) {
+  std::vector<T> h(n);
+  if (n) A4_HIP(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+  A4_HIP(hipStreamSynchronize(s));
+  return h;
+}
+
+int group_log2(double seg) { return seg >= 40 ? 6 : (seg >= 16 ? 5 : 4); }   // ops/spgemm.py _group_log2
+
+struct Plan {
+  int64_t tot = 0, mx = 0, nz = 0, amax = 0;
+  DevBuf<int64_t> nprod;
+};
+
+Plan row_plan(const DCsr& A, const DCsr& B, hipStream_t s) {
+  Plan p;
+  p.nprod = DevBuf<int64_t>(std::max<int64_t>(A.m, 1), s);
+  DevBuf<int64_t> nsl(std::max<int64_t>(A.m, 1), s), part((kPlanBlocks + 1) * kPlanStats, s);
+  const int64_t c1 = (int64_t)(kEscLoad * kEscPcap);
+  A4_HIP((hipError_t)spmm_spgemm_row_plan(A.rp.get(), A.ci.get(), B.rp.get(), A.m, c1, 2 * c1, 4 * c1, kEscMin,
+                                          p.nprod.get(), nsl.get(), part.get(), part.get() + kPlanBlocks * kPlanStats,
+                                          s));
+  const std::vector<int64_t> st = down(part.get() + kPlanBlocks * kPlanStats, kPlanStats, s);
+  p.tot = st[0];
+  p.mx = st[1];
+  p.nz = st[2];
+  p.amax = st[8];
+  return p;
+}
+
+DCsr empty_product(const DCsr& A, const DCsr& B, hipStream_t s) {
+  DCsr C;
+  C.m = A.m;
+  C.n = B.n;
+  C.rp = DevBuf<int64_t>(A.m + 1, s);
+  A4_HIP(hipMemsetAsync(C.rp.get(), 0, (A.m + 1) * sizeof(int64_t), s));
+  C.ci = DevBuf<int32_t>(1, s);
+  C.v = DevBuf<float>(1, s);
+  return C;
+}
+
+// ---- bitmap-rank path (ops/spgemm.py onepass_bitmap, per-unit kernels) ------
+bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s, DCsr* out) {
+  if (B.nnz >= (int64_t(1) << 31) || B.n >= (int64_t(1) << 30) || A.nnz >= (int64_t(1) << 31)) return false;
+  const double mean = (double)pl.tot / (double)std::max<int64_t>(pl.nz, 1);
+  if (pl.mx > 4 * mean || pl.nz < A.m / 2) return false;   // skewed rows: the binned path's job
+  int cfg = -1, lgw = 0, nsub = 0, pcap = 0, rounds = 0, reload_rows = 0;
+  for (int c : {0, 2, 1}) {   // widest window whose mean products per window fit 70 % of the fast capacity
+    A4_HIP((hipError_t)spmm_spgemm_bm_config(c, &lgw, &nsub, &pcap, &rounds, &reload_rows));
+    const double W = (double)(int64_t(1) << lgw);
+    if (mean * std::min(W, (double)B.n) / std::max<double>((double)B.n, 1) <= 0.7 * pcap) {
+      cfg = c;
+      break;
+    }
+  }
+  if (cfg < 0) return false;
+  A4_HIP((hipError_t)spmm_spgemm_bm_config(cfg, &lgw, &nsub, &pcap, &rounds, &reload_rows));
+  if (pl.amax > reload_rows) return false;
+  const int nwin = (int)std::max<int64_t>(1, (B.n + (int64_t(1) << lgw) - 1) >> lgw);
+  const int64_t nunits = A.m * nwin;
+  if (nunits >= (int64_t(1) << 31)) return false;
+  const double seg = (double)pl.tot / (double)std::max<int64_t>(A.nnz, 1);   // B-segment length per A entry
+  const int lg_count = group_log2(seg * std::min(nsub, nwin) / nwin);
+  const int lg_num = seg / nwin < 48 ? 4 : (seg / nwin < 96 ? 5 : 6);
+  DevBuf<uint32_t> ws((size_t)B.m * (nwin + 1), s);
+  DevBuf<int32_t> ucnt((size_t)nunits, s), err(4, s);
+  DevBuf<int64_t> uoff((size_t)nunits + 1, s);
+  DevBuf<uint8_t> scan_ws(std::max<size_t>(spmm_prim_scan_ws(nunits), 1), s);
+  A4_HIP(hipMemsetAsync(err.get(), 0, 16, s));
+  A4_HIP(hipMemsetAsync(uoff.get(), 0, 8, s));
+  A4_HIP((hipError_t)spmm_spgemm_bm_splits(B.rp.get(), B.ci.get(), B.m, lgw, nwin, ws.get(), s));
+  A4_HIP((hipError_t)spmm_spgemm_bm_count(cfg, A.rp.get(), A.ci.get(), ws.get(), B.ci.get(), A.m, nwin, lg_count,
+                                          ucnt.get(), err.get(), s));
+  A4_HIP((hipError_t)spmm_prim_scan(ucnt.get(), 4, nunits, uoff.get() + 1, 1, scan_ws.get(), s));
+  const std::vector<int64_t> nnzv = down(uoff.get() + nunits, 1, s);   // the one sizing read-back
+  const int64_t nnz = nnzv[0];
+  if (down(err.get(), 1, s)[0] != 0) return false;
+  const int64_t ovf_cap = std::min<int64_t>(nunits, 1 << 20);
+  DCsr C;
+  C.m = A.m;
+  C.n = B.n;
+  C.nnz = nnz;
+  C.ci = DevBuf<int32_t>((size_t)std::max<int64_t>(nnz, 1), s);
+  C.v = DevBuf<float>((size_t)std::max<int64_t>(nnz, 1), s);
+  DevBuf<int32_t> ovf((size_t)ovf_cap, s);
+  A4_HIP((hipError_t)spmm_spgemm_bm_numeric(cfg, A.rp.get(), A.ci.get(), A.v.get(), ws.get(), B.ci.get(), B.v.get(),
+                                            A.m, nwin, lg_num, uoff.get(), nnz, C.ci.get(), C.v.get(), ovf.get(),
+                                            (uint32_t*)(err.get() + 1), ovf_cap, err.get(), 0, s));
+  const int e = down(err.get(), 1, s)[0];
+  A4_CHECK((e & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
+  if (e & 5) return false;   // a unit beyond the reload kernel's budget: the binned path redoes the product
+  // row pointer: every nwin-th unit offset
+  const std::vector<int64_t> uo = down(uoff.get(), nunits + 1, s);
+  std::vector<int64_t> rp(A.m + 1);
+  for (int64_t i = 0; i <= A.m; ++i) rp[i] = uo[i * nwin];
+  C.rp = up(rp, s);
+  *out = std::move(C);
+  return true;
+}
+
+// ---- long rows (ops/spgemm.py _long_rows, routed mode) -----------------------
+// values = 0: per-row nnz into cnt_out; 1: the rows written at Crp_h[row].
+void long_rows(int values, const DCsr& A, const DCsr& B, const std::vector<int32_t>& rows,
+               const std::vector<int64_t>& nprod_h, const std::vector<int64_t>& Arp_h, hipStream_t s,
+               std::vector<int64_t>* cnt_out, const std::vector<int64_t>* Crp_h, int32_t* Cci, float* Cv) {
+  if (rows.empty()) return;
+  int lgw = 0, epw = 0, maxch = 0;
+  A4_HIP((hipError_t)spmm_spgemm_long_params(&lgw, &epw, &maxch));
+  const int nch = (int)((B.n + (int64_t(1) << lgw) - 1) >> lgw);
+  A4_CHECK(nch <= maxch, "long-row path: too many columns");
+  const int64_t nrows = (int64_t)rows.size();
+  int64_t maxp = 0;
+  for (int32_t r : rows) maxp = std::max(maxp, nprod_h[r]);
+  const int64_t cap = std::max(kWsProducts, maxp);
+  for (int64_t start = 0; start < nrows;) {
+    int64_t end = start, acc = 0;   // batch: the longest run of rows whose products fit cap (at least one row)
+    while (end < nrows && (end == start || acc + nprod_h[rows[end]] <= cap)) acc += nprod_h[rows[end++]];
+    const int64_t R = end - start;
+    std::vector<int64_t> first(R), nwg_r(R), e0, e1;
+    std::vector<int32_t> wrow;
+    for (int64_t i = 0; i < R; ++i) {
+      const int32_t r = rows[start + i];
+      const int64_t a0 = Arp_h[r], na = Arp_h[r + 1] - a0;
+      nwg_r[i] = std::max<int64_t>(1, (na + epw - 1) / epw);
+      first[i] = (int64_t)e0.size();
+      for (int64_t k = 0; k < nwg_r[i]; ++k) {
+        e0.push_back(a0 + k * epw);
+        e1.push_back(std::min(a0 + (k + 1) * epw, a0 + na));
+        wrow.push_back((int32_t)i);
+      }
+    }
+    const int64_t nwg = (int64_t)e0.size();
+    DevBuf<int64_t> de0 = up(e0, s), de1 = up(e1, s), dfirst = up(first, s), dnwg = up(nwg_r, s);
+    DevBuf<int32_t> dwrow = up(wrow, s);
+    DevBuf<int32_t> hist((size_t)nwg * nch, s);
+    A4_HIP((hipError_t)spmm_spgemm_long_route(0, A.ci.get(), A.v.get(), B.rp.get(), B.ci.get(), B.v.get(), de0.get(),
+                                              de1.get(), nwg, nch, hist.get(), nullptr, nullptr, nullptr, nullptr,
+                                              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s));
+    DevBuf<int64_t> T((size_t)R * nch, s);
+    A4_HIP((hipError_t)spmm_spgemm_long_wg_scan(hist.get(), dfirst.get(), dnwg.get(), R, nch, T.get(), nullptr, nullptr,
+                                                nullptr, s));
+    const std::vector<int64_t> Th = down(T.get(), (size_t)R * nch, s);
+    std::vector<int64_t> rt_off((size_t)R * nch);
+    int64_t base = 0;
+    for (int64_t i = 0; i < R; ++i) {
+      int64_t rowtot = 0;
+      for (int t = 0; t < nch; ++t) {
+        rt_off[i * nch + t] = base + rowtot;
+        rowtot += Th[i * nch + t];
+      }
+      A4_CHECK(rowtot == nprod_h[rows[start + i]], "long rows: routing histogram disagrees with the product counts");
+      base += rowtot;
+    }
+    DevBuf<int64_t> drt_off = up(rt_off, s);
+    DevBuf<unsigned long long> scratch((size_t)std::max<int64_t>(base, 1), s);
+    A4_HIP((hipError_t)spmm_spgemm_long_route(1, A.ci.get(), A.v.get(), B.rp.get(), B.ci.get(), B.v.get(), de0.get(),
+                                              de1.get(), nwg, nch, hist.get(), dwrow.get(), drt_off.get(),
+                                              scratch.get(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                              nullptr, s));
+    DevBuf<int64_t> rt_nnz((size_t)R * nch, s);
+    DevBuf<int32_t> lists((size_t)2 * R * nch + 2, s);
+    A4_HIP((hipError_t)spmm_spgemm_long_dense(values, drt_off.get(), T.get(), R * nch, nch, scratch.get(), rt_nnz.get(),
+                                              lists.get(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s));
+    const std::vector<int64_t> nz = down(rt_nnz.get(), (size_t)R * nch, s);
+    if (!values) {
+      for (int64_t i = 0; i < R; ++i) {
+        int64_t t = 0;
+        for (int c = 0; c < nch; ++c) t += nz[i * nch + c];
+        (*cnt_out)[start + i] = t;
+      }
+    } else {
+      std::vector<int64_t> dst((size_t)R * nch);
+      for (int64_t i = 0; i < R; ++i) {
+        int64_t at = (*Crp_h)[rows[start + i]];
+        for (int c = 0; c < nch; ++c) {
+          dst[i * nch + c] = at;
+          at += nz[i * nch + c];
+        }
+        A4_CHECK(at == (*Crp_h)[rows[start + i] + 1], "long rows: numeric count disagrees with the symbolic count");
+      }
+      DevBuf<int64_t> ddst = up(dst, s);
+      A4_HIP((hipError_t)spmm_spgemm_long_place(drt_off.get(), ddst.get(), rt_nnz.get(), R * nch, scratch.get(), Cci,
+                                                Cv, s));
+      A4_HIP(hipStreamSynchronize(s));
+    }
+    start = end;
+  }
+}
+
+// ---- binned two-phase path (ops/spgemm.py symbolic + numeric) -----------------
+// Bin b of the LDS kernels by a row's product count; -1: empty row; 11: long.
+int sym_bin(int64_t p) {
+  if (p == 0) return -1;
+  for (int b = 0; b <= 6; ++b)
+    if (p <= (int64_t)(kLoad * (128 << b))) return b;
+  for (int k = 0; k < 4; ++k)
+    if (p <= (int64_t)(kLoad * 16384) * (1 << k)) return 7 + k;
+  return 11;
+}
+int num_bin(int64_t p) {
+  if (p == 0) return -1;
+  for (int b = 0; b <= 6; ++b)
+    if (p <= std::min<int64_t>((int64_t)(kLoad * (128 << b)), kEscMin)) return b;
+  if (p <= kEscPcap) return 7;
+  for (int k = 1; k < 4; ++k)
+    if (p <= (int64_t)(kEscLoad * kEscPcap) * (1 << k)) return 7 + k;
+  return 11;
+}
+
+DCsr binned_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s, EngineStats* st) {
+  const std::vector<int64_t> nprod_h = down(pl.nprod.get(), A.m, s);
+  const std::vector<int64_t> Arp_h = down(A.rp.get(), A.m + 1, s);
+  const double seg = (double)pl.tot / (double)std::max<int64_t>(A.nnz, 1);
+  DevBuf<int64_t> bsplit;
+  auto splits = [&]() -> const int64_t* {
+    if (!bsplit.get()) {
+      bsplit = DevBuf<int64_t>((size_t)B.m * 7, s);
+      A4_HIP((hipError_t)spmm_spgemm_row_splits(B.rp.get(), B.ci.get(), B.m, (int)B.n, bsplit.get(), s));
+    }
+    return bsplit.get();
+  };
+  auto slices = [](int b) { return b == 8 ? 2 : (b == 9 ? 4 : (b == 10 ? 8 : 1)); };
+  DevBuf<int32_t> flags((size_t)std::max<int64_t>(A.m, 1), s);
+  DevBuf<int64_t> d64(1, s);
+  DevBuf<int32_t> d32(1, s);
+  DevBuf<float> df(1, s);
+  // run the LDS bins of one phase; returns the rows for the long-row path
+  auto run_bins = [&](int numeric, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv) {
+    std::vector<std::vector<int32_t>> by(12);
+    for (int64_t r = 0; r < A.m; ++r) {
+      const int b = numeric ? num_bin(nprod_h[r]) : sym_bin(nprod_h[r]);
+      if (b >= 0) by[b].push_back((int32_t)r);
+    }
+    A4_HIP(hipMemsetAsync(flags.get(), 0, std::max<int64_t>(A.m, 1) * sizeof(int32_t), s));
+    std::vector<DevBuf<int32_t>> keep;
+    for (int b = 0; b <= 10; ++b) {
+      if (by[b].empty()) continue;
+      keep.push_back(up(by[b], s));
+      const bool multi = b >= 8;
+      A4_HIP((hipError_t)spmm_spgemm_lds(b, numeric, A.rp.get(), A.ci.get(), A.v.get(), B.rp.get(), B.ci.get(),
+                                         B.v.get(), multi ? splits() : nullptr, keep.back().get(),
+                                         (int64_t)by[b].size(), (int)B.n, group_log2(seg / slices(b)), row_nnz,
+                                         nullptr, Crp ? Crp : d64.get(), Cci ? Cci : d32.get(), Cv ? Cv : df.get(),
+                                         flags.get(), s));
+    }
+    const std::vector<int32_t> fl = down(flags.get(), A.m, s);
+    std::vector<int32_t> lr = by[11];
+    for (int64_t r = 0; r < A.m; ++r) {
+      A4_CHECK((fl[r] & 4) == 0, "spgemm: output position out of range (kernel invariant violated)");
+      if (fl[r] & 2) lr.push_back((int32_t)r);   // a slice could overflow its LDS table
+    }
+    std::sort(lr.begin(), lr.end());
+    return std::make_pair(lr, fl);
+  };
+  // symbolic: exact nnz per row
+  DevBuf<int32_t> row_nnz((size_t)std::max<int64_t>(A.m, 1), s);
+  A4_HIP(hipMemsetAsync(row_nnz.get(), 0, std::max<int64_t>(A.m, 1) * sizeof(int32_t), s));
+  auto sym = run_bins(0, row_nnz.get(), nullptr, nullptr, nullptr);
+  std::vector<int32_t> nnz_h = down(row_nnz.get(), A.m, s);
+  std::vector<int64_t> lcnt(sym.first.size());
+  long_rows(0, A, B, sym.first, nprod_h, Arp_h, s, &lcnt, nullptr, nullptr, nullptr);
+  for (size_t i = 0; i < sym.first.size(); ++i) {
+    A4_CHECK(lcnt[i] < INT32_MAX, "a row of the product has 2^31 or more entries");
+    nnz_h[sym.first[i]] = (int32_t)lcnt[i];
+  }
+  std::vector<int64_t> Crp_h(A.m + 1, 0);
+  for (int64_t r = 0; r < A.m; ++r) Crp_h[r + 1] = Crp_h[r] + nnz_h[r];
+  DCsr C;
+  C.m = A.m;
+  C.n = B.n;
+  C.nnz = Crp_h[A.m];
+  C.rp = up(Crp_h, s);
+  C.ci = DevBuf<int32_t>((size_t)std::max<int64_t>(C.nnz, 1), s);
+  C.v = DevBuf<float>((size_t)std::max<int64_t>(C.nnz, 1), s);
+  row_nnz = up(nnz_h, s);   // the numeric kernels' per-row capacities (exact)
+  // numeric: values into the layout fixed by the symbolic phase
+  auto num = run_bins(1, row_nnz.get(), C.rp.get(), C.ci.get(), C.v.get());
+  long_rows(1, A, B, num.first, nprod_h, Arp_h, s, nullptr, &Crp_h, C.ci.get(), C.v.get());
+  st->long_rows += (int64_t)num.first.size();
+  // rows the ordered LDS tables could not keep sorted (flag 1): re-sorted here
+  std::vector<int32_t> bad;
+  for (int64_t r = 0; r < A.m; ++r)
+    if (num.second[r] & 1) bad.push_back((int32_t)r);
+  for (int32_t r : bad) {
+    const int64_t a = Crp_h[r], n = Crp_h[r + 1] - a;
+    std::vector<int32_t> c = down(C.ci.get() + a, n, s);
+    std::vector<float> v = down(C.v.get() + a, n, s);
+    std::vector<int64_t> idx(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return c[x] < c[y]; });
+    std::vector<int32_t> c2(n);
+    std::vector<float> v2(n);
+    for (int64_t i = 0; i < n; ++i) {
+      c2[i] = c[idx[i]];
+      v2[i] = v[idx[i]];
+    }
+    A4_HIP(hipMemcpyAsync(C.ci.get() + a, c2.data(), n * 4, hipMemcpyHostToDevice, s));
+    A4_HIP(hipMemcpyAsync(C.v.get() + a, v2.data(), n * 4, hipMemcpyHostToDevice, s));
+    A4_HIP(hipStreamSynchronize(s));
+  }
+  st->resorted_rows += (int64_t)bad.size();
+  return C;
+}
+
+}  // namespace
+
+DCsr dcsr_upload(const Csr& H, hipStream_t s) {
+  DCsr D;
+  D.m = H.m;
+  D.n = H.n;
+  D.nnz = H.nnz();
+  D.rp = up(H.rp, s);
+  D.ci = up(H.ci, s);
+  D.v = up(H.v, s);
+  return D;
+}
+
+Csr dcsr_download(const DCsr& D, hipStream_t s) {
+  Csr H;
+  H.m = D.m;
+  H.n = D.n;
+  H.rp = down(D.rp.get(), D.m + 1, s);
+  H.ci = down(D.ci.get(), D.nnz, s);
+  H.v = down(D.v.get(), D.nnz, s);
+  return H;
+}
+
+DCsr dev_spgemm(const DCsr& A, const DCsr& B, hipStream_t s, EngineStats* st, int64_t* products) {
+  A4_CHECK(A.n == B.m, "inner dimensions differ");
+  if (A.m == 0 || A.nnz == 0 || B.nnz == 0) {
+    *products = 0;
+    return empty_product(A, B, s);
+  }
+  const Plan pl = row_plan(A, B, s);
+  *products = pl.tot;
+  if (pl.tot == 0) return empty_product(A, B, s);
+  A4_CHECK(pl.mx < (int64_t(1) << 31), "a row of the product has 2^31 or more intermediate products");
+  DCsr C;
+  if (bitmap_product(A, B, pl, s, &C)) {
+    ++st->bitmap;
+    return C;
+  }
+  ++st->binned;
+  return binned_product(A, B, pl, s, st);
+}
+
+}  // namespace a4

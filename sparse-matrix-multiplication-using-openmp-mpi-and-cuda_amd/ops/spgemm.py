@@ -67,7 +67,7 @@ _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp,
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
-                     c_vp)
+                     C_I64, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp,
@@ -809,7 +809,8 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
             cbase -= plen_c
             colp = torch.empty(nnzb + 31 * ngc * B.m, dtype=torch.int32, device=dev)
             _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), None, B.m, nwin, None, P(ws8), None, P(cbase),
-                                                       plan.nsub_c, P(colp), st), "spgemm_bm_pad_pairs(columns)")
+                                                       plan.nsub_c, P(colp), 0, colp.numel(), P(err), st),
+                          "spgemm_bm_pad_pairs(columns)")
             del cbase, plen_c
         _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8),
                                                     P(colp) if colp is not None else P(B.col), m, nwin, plan.lg_c,
@@ -827,6 +828,8 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     out = dict(uoff=uoff, z=z, nunits=nunits, ws8=ws8 is not None)
     if not lazy:
         nnz, e0 = torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
+        if e0 & 32:
+            raise RuntimeError("spgemm bitmap: padded B layout overflow (kernel invariant violated)")
         out.update(nnz=nnz)
         if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
             out.update(truncated=True)
@@ -849,7 +852,8 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
             pbase -= plen
             Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
             _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, P(pbase), P(ws8),
-                                                       P(Bcv), None, 1, None, st), "spgemm_bm_pad_pairs")
+                                                       P(Bcv), None, 1, None, Bcv.shape[0], 0, P(err), st),
+                          "spgemm_bm_pad_pairs")
             del pbase
         else:
             Bcv = interleaved(B) if CONFIG.spgemm_bitmap_cv else None
@@ -887,6 +891,8 @@ def _bitmap_finish(A: CSR, B: CSR, plan: BitmapPlan, out: dict, info: SpgemmInfo
     info.rows_per_bin_num["bitmap_deferred"] = deferred
     if e & 2:
         raise RuntimeError("spgemm bitmap: numeric and count kernels disagree (kernel invariant violated)")
+    if e & 32:
+        raise RuntimeError("spgemm bitmap: padded B layout overflow (kernel invariant violated)")
     if plan.det and e & 21:
         # a unit beyond every deterministic kernel's budget (adversarial column
         # collisions): the CPU engine sums in the same (Gustavson) order

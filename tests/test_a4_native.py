@@ -334,3 +334,49 @@ def test_a4_mtx_gpu_bitmap_matches_cpu(tmp_path, a4_bin, p):
     G, C = mtx.read_mtx(g), mtx.read_mtx(c)
     assert G.nnz == C.nnz and bool((G.rowptr == C.rowptr).all()) and bool((G.col == C.col).all())
     np.testing.assert_allclose(G.val.numpy(), C.val.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _skewed(m, n, base, hubs, hub_len, seed):
+    """m x n CSR with ~base entries per row and a few hub rows of hub_len."""
+    import torch
+
+    from spmm_amd.ops import csr as CS
+
+    g = torch.Generator().manual_seed(seed)
+    rows, cols = [], []
+    for i in range(m):
+        k = hub_len if i in hubs else int(torch.randint(max(base // 2, 1), base * 2, (1,), generator=g))
+        c = torch.randperm(n, generator=g)[:k]
+        rows.append(torch.full((k,), i))
+        cols.append(c)
+    r, c = torch.cat(rows), torch.cat(cols)
+    return CS.from_coo(r, c, torch.rand(r.numel(), generator=g) - 0.5, m, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [1, 2])
+def test_a4_mtx_gpu_skewed_chain_has_no_cpu_fallback(tmp_path, a4_bin, p):
+    """A skewed (hub-row) chain stays on the GPU: the products that fail the
+    bitmap gate take the binned LDS path, and output rows of > 55296
+    intermediate products go through the long-row pipeline (long_route /
+    long_dense / long_place) -- recorded in --metrics-json, no CPU product.
+    Same structure as the CPU engine, values to fp32 summation order."""
+    import numpy as np
+
+    from spmm_amd.utils import mtx
+
+    d = tmp_path / "c"
+    d.mkdir()
+    mats = [_skewed(1200, 3000, 6, {0, 7}, 2500, 1), _skewed(3000, 2600, 30, set(range(0, 3000, 150)), 1800, 2),
+            _skewed(2600, 2200, 8, {3, 4}, 1500, 3)]
+    for i, M in enumerate(mats):
+        mtx.write_mtx(str(d / f"m{i + 1}.mtx"), M)
+    g, c, met = str(tmp_path / "g.mtx"), str(tmp_path / "c.mtx"), str(tmp_path / "met.json")
+    _run(a4_bin, p, str(d), "--format", "mtx", "--device", "hip", "--out", g, "--quiet", "--metrics-json", met)
+    _run(a4_bin, p, str(d), "--format", "mtx", "--device", "cpu", "--out", c, "--quiet")
+    m = json.load(open(met))
+    assert m["device_resident"] and m["cpu_products"] == 0 and m["gpu_products"] == 2, m
+    assert m["gpu_binned_products"] >= 1 and m["gpu_long_rows"] >= 1, m
+    G, C = mtx.read_mtx(g), mtx.read_mtx(c)
+    assert G.nnz == C.nnz and bool((G.rowptr == C.rowptr).all()) and bool((G.col == C.col).all())
+    np.testing.assert_allclose(G.val.numpy(), C.val.numpy(), rtol=1e-4, atol=1e-5)
