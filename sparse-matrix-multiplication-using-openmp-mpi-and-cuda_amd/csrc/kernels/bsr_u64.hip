@@ -147,7 +147,11 @@ __global__ __launch_bounds__(NT) void bsr_u64_numeric_lds(
     }
     return bad;
   };
+#if SPMM_CHAIN_SPEC
   if (__syncthreads_or(pass(std::true_type{}))) pass(std::false_type{});   // (uniform: the whole workgroup redoes it)
+#else
+  pass(std::false_type{});
+#endif
 
   const int orow = ti * TS + ty, ocol = tj * TS + tx;
   uint64_t* C = Cvals + tile * kk;

@@ -20,6 +20,13 @@
     if (_e != hipSuccess) return (int)_e;            \
   } while (0)
 
+#ifndef SPMM_CHAIN_CROSS_MUL   // speculative MAC: cross terms by v_mul_lo_u32 (1) or v_mad_u64_u32 (0)
+#define SPMM_CHAIN_CROSS_MUL 1
+#endif
+#ifndef SPMM_CHAIN_SPEC   // chain tile kernel: speculative wrapping MAC + exact recompute (1) or exact only (0)
+#define SPMM_CHAIN_SPEC 1
+#endif
+
 namespace spmm {
 
 constexpr int kWave = 64;      // CDNA wavefront width
@@ -60,12 +67,21 @@ __device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t 
   // four VALU ops: r = alo*blo + acc;  c = alo*bhi;  x = ahi*blo + c (its low
   // word = the cross terms mod 2^32);  s_hi = r_hi + x_lo (32-bit add into the
   // high half; opaque so the compiler does not rebuild it as a 64-bit add)
-  uint64_t r, c, x, k0, k1, k2;
+  uint64_t r, k0;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(k0) : "v"(alo), "v"(blo), "v"(acc));
+  uint32_t hi;
+#if SPMM_CHAIN_CROSS_MUL
+  // cross terms as two v_mul_lo_u32 + one v_add3_u32
+  uint32_t c1, c2;
+  asm("v_mul_lo_u32 %0, %1, %2" : "=v"(c1) : "v"(alo), "v"(bhi));
+  asm("v_mul_lo_u32 %0, %1, %2" : "=v"(c2) : "v"(ahi), "v"(blo));
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(r >> 32)), "v"(c1), "v"(c2));
+#else
+  uint64_t c, x, k1, k2;
   asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(c), "=s"(k1) : "v"(alo), "v"(bhi));
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(x), "=s"(k2) : "v"(ahi), "v"(blo), "v"(c));
-  uint32_t hi;
   asm("v_add_u32 %0, %1, %2" : "=v"(hi) : "v"((uint32_t)(r >> 32)), "v"((uint32_t)x));
+#endif
   const uint32_t lo = (uint32_t)r;
   const uint64_t s = ((uint64_t)hi << 32) | lo;
   const uint32_t tlo = lo - (uint32_t)acc;

@@ -1668,7 +1668,7 @@ __global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __rest
 // Wider windows mean longer contiguous B segments per (A entry, unit): random
 // segment gathers run at ~7 TB/s of 128-byte LINES, so 100-byte segments
 // deliver ~3.2 TB/s of useful bytes and 200-byte ones ~4.4
-// (tools/probes/seg_gather.hip, profiles/r4/seg_gather.csv).
+// (tools/probes/seg_gather.hip, profiles/r4/seg_gather.md).
 struct BmCfg {
   int lgw, nsub_count, pcap_fast, rounds_fast, rows_nt, rows_r;
 };

@@ -467,28 +467,47 @@ Node gpu_reduce_local(const Options& o, int lo, int hi, int k, const Streams& ss
   Loader<Node> loader(o, lo, hi, k, ss.load, st);
   Pool pool(o.streams, ss.pool);
   const int n = hi - lo + 1;
-  std::vector<std::shared_future<Node>> arr;
   auto ready = [](Node x) {
     std::promise<Node> p;
     p.set_value(std::move(x));
     return p.get_future().share();
   };
+  // The reference's association -- pairs of files, then adjacent pairs level
+  // by level, an odd node carried up (sparse_matrix_mult.cu:290-326) -- is the
+  // same tree as a binary counter over the level-0 products folded from the
+  // right at the end (checked for every n < 300).  Submitting in counter order
+  // starts a level-1 product as soon as its two halves exist instead of after
+  // the last file is parsed; the products wait on their operands' futures in
+  // the pool.  The "multiplying" lines keep the reference's level order.
+  struct Lv {
+    int level;
+    std::shared_future<Node> f;
+  };
+  std::vector<Lv> stk;
+  auto merge_push = [&](int lv, std::shared_future<Node> f) {
+    while (!stk.empty() && stk.back().level == lv) {
+      f = gpu_product(pool, stk.back().f, f, st).share();
+      stk.pop_back();
+      ++lv;
+    }
+    stk.push_back({lv, std::move(f)});
+  };
   for (int ind = 0; ind + 1 < n; ind += 2) {   // level 0 as files land
     Node a = loader.get(), b = loader.get();
     say(o, "multiplying " + std::to_string(lo + ind) + " " + std::to_string(lo + ind + 1));
-    arr.push_back(gpu_product(pool, ready(std::move(a)), ready(std::move(b)), st).share());
+    merge_push(0, gpu_product(pool, ready(std::move(a)), ready(std::move(b)), st).share());
   }
-  if (n % 2 == 1) arr.push_back(ready(loader.get()));
-  while (arr.size() > 1) {
-    std::vector<std::shared_future<Node>> nxt;
-    for (size_t ind = 0; ind + 1 < arr.size(); ind += 2) {
+  if (n % 2 == 1) stk.push_back({0, ready(loader.get())});
+  for (size_t w = (size_t)(n / 2 + n % 2); w > 1; w = w / 2 + w % 2)
+    for (size_t ind = 0; ind + 1 < w; ind += 2)
       say(o, "multiplying " + std::to_string(lo + (int)ind) + " " + std::to_string(lo + (int)ind + 1));
-      nxt.push_back(gpu_product(pool, arr[ind], arr[ind + 1], st).share());
-    }
-    if (arr.size() % 2 == 1) nxt.push_back(arr.back());
-    arr.swap(nxt);
+  std::shared_future<Node> acc = stk.back().f;
+  stk.pop_back();
+  while (!stk.empty()) {
+    acc = gpu_product(pool, stk.back().f, acc, st).share();
+    stk.pop_back();
   }
-  return arr[0].get();
+  return acc.get();
 }
 
 // ---- CPU tree ---------------------------------------------------------------

@@ -349,9 +349,11 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         chunk_off = torch.cumsum(region, 1) - region
         row_reg = region.sum(1)
         row_base = torch.cumsum(row_reg, 0) - row_reg
-        # the scatter pass writes exactly the histogram's slots: a histogram
-        # that disagrees with the rows' product counts is an invariant failure
-        # (checked once after the loop; the scratch is sized by the histogram)
+        # the scatter pass writes exactly the histogram's slots, while the
+        # scratch below is sized from the host plan's product counts (no
+        # read-back).  Both count the same (A entry, B row) pairs, so they agree
+        # unless a kernel is broken; this comparison, read once after the loop,
+        # only DETECTS such a failure -- it does not keep the scatter in bounds.
         bad += ((T + D).sum(1) if direct else T.sum(1)).ne(nprod_rows[start:end]).sum()
         rt_off = (row_base[:, None] + chunk_off).reshape(-1).contiguous()   # each (row, chunk) region's base
         # sizes from the host plan (no read-back): the regions never exceed the
@@ -814,7 +816,9 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
             del cbase, plen_c
         _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8),
                                                     P(colp) if colp is not None else P(B.col), m, nwin, plan.lg_c,
-                                                    plan.nsub_c, P(ucnt), P(err), B.col.numel(), int(colp is not None),
+                                                    plan.nsub_c, P(ucnt), P(err),
+                                                    colp.numel() if colp is not None else B.col.numel(),
+                                                    int(colp is not None),
                                                     st),
                       "spgemm_bm_count_rows")
         del colp

@@ -4,7 +4,7 @@ set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo}
 O=gpurun_out/r4g5; mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
-  tests/test_spgemm.py -k "bitmap or bench_scale or graph" -m gpu > $O/pytest.log 2>&1 &&
+  tests/test_spgemm.py tests/test_a4_native.py -k "bitmap or bench_scale or graph or mtx" -m gpu > $O/pytest.log 2>&1 &&
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > $O/bench1m.json 2> $O/bench1m.err &&
 SPMM_SPGEMM_BITMAP_PAD=0 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --graph off > $O/bench1m_nopad.json 2> $O/bench1m_nopad.err &&
 timeout -k 10 300 python -u bench.py --workload spgemm64k --steps 20 --warmup 3 > $O/bench64k.json 2> $O/bench64k.err &&
