@@ -41,24 +41,9 @@
 #define SPMM_BM_SWEEP_G 2
 #endif
 
-#ifndef SPMM_BM_DIAG_NOLOAD   // diagnostic builds only: count kernel without B loads / without ORs
-#define SPMM_BM_DIAG_NOLOAD 0
-#endif
-#ifndef SPMM_BM_DIAG_NOOR
-#define SPMM_BM_DIAG_NOOR 0
-#endif
-#ifndef SPMM_BM_DIAG_NOSWEEP
-#define SPMM_BM_DIAG_NOSWEEP 0
-#endif
 #ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
 #define SPMM_BM_P2_G 2   // 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586 (fewer empty rounds past the chunk count); 7 spills
 #endif
-
-
-
-
-
-
 
 #define BM_OUT(ptr, val) __builtin_nontemporal_store((val), (ptr))
 
@@ -1416,21 +1401,8 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
               ok2m |= (ok & (nv > 1) ? 1u : 0u) << d;
               x[d] = make_uint2(0u, 0u);
               if (i0 + d < nr)   // wave-uniform guard
-#if SPMM_BM_DIAG_NOLOAD   // timing decomposition only (wrong counts): no B loads
-                x[d] = make_uint2((uint32_t)clo + ((ds[d].x * 2654435761u + gl * 40503u) & ((2u << LGW) - 1u)),
-                                  (uint32_t)clo + ((ds[d].x * 2246822519u + gl * 9973u) & ((2u << LGW) - 1u)));
-#else
                 x[d] = *reinterpret_cast<const uint2*>(p.Bci + ds[d].x + (ok ? 2u * (uint32_t)gl : 0u));
-#endif
             }
-#if SPMM_BM_DIAG_NOOR   // timing decomposition only (wrong counts): loads consumed without LDS ORs
-            {
-              uint32_t acc = 0;
-#pragma unroll
-              for (int d = 0; d < RR; ++d) acc += ((okm >> d) & 1u) ? x[d].x ^ x[d].y : 0u;
-              if (acc == 0x9e3779b9u) bm32[0] = acc;
-            }
-#else
 #pragma unroll
             for (int d = 0; d < RR; ++d) {
               if ((okm >> d) & 1u) {
@@ -1442,7 +1414,6 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
                 atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
               }
             }
-#endif
           } else {
             int x[RR];
             uint32_t okm = 0;
@@ -1477,16 +1448,12 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
       }
       // popcount of this wave's bitmap rows, clearing them as they are read
       int cnt = 0;
-#if SPMM_BM_DIAG_NOSWEEP   // timing decomposition only (wrong counts)
-      cnt = (int)bm32[w * 64 + lane];
-#else
 #pragma unroll
       for (int kk = 0; kk < WPT; ++kk) {
         const int wd = w * WPW + kk * 64 + lane;
         cnt += __popcll(bm[wd]);
         bm[wd] = 0ull;
       }
-#endif
       cnt = bm_wave_sum(cnt);
       if (lane == 0) csum[w] = cnt;
       __syncthreads();
