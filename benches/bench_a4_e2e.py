@@ -69,6 +69,7 @@ def generate(folder: str, preset: str, seed: int, k: int = 32) -> dict:
         tiles += M.nb
         refio.write_matrix(refio.matrix_path(folder, i), M.to("cpu"))
         del M
+        print(f"[generate] matrix {i}/{cfg['n']} written", file=sys.stderr, flush=True)
     nbytes = sum(os.path.getsize(os.path.join(folder, f)) for f in os.listdir(folder))
     return dict(cfg, k=k, input_tiles=tiles, input_bytes=nbytes)
 
