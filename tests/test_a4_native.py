@@ -380,3 +380,38 @@ def test_a4_mtx_gpu_skewed_chain_has_no_cpu_fallback(tmp_path, a4_bin, p):
     G, C = mtx.read_mtx(g), mtx.read_mtx(c)
     assert G.nnz == C.nnz and bool((G.rowptr == C.rowptr).all()) and bool((G.col == C.col).all())
     np.testing.assert_allclose(G.val.numpy(), C.val.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_counter_order_tree_is_the_reference_tree():
+    """a4_main.cpp gpu_reduce_local submits the products in binary-counter order
+    (a level-k product as soon as its two halves exist, the stack folded from
+    the right at the end).  That is the same association as the reference's
+    level-by-level pairwise tree with the odd node carried up
+    (sparse_matrix_mult.cu:290-326) for every chain length -- the arithmetic is
+    not associative in its edge cases, so the tree must match exactly."""
+    def ref(n):
+        arr = [(i, i + 1) for i in range(0, n - 1, 2)] + ([n - 1] if n % 2 else [])
+        while len(arr) > 1:
+            nxt = [(arr[i], arr[i + 1]) for i in range(0, len(arr) - 1, 2)]
+            if len(arr) % 2:
+                nxt.append(arr[-1])
+            arr = nxt
+        return arr[0]
+
+    def counter(n):
+        st = []
+        for i in range(0, n - 1, 2):
+            lv, x = 0, (i, i + 1)
+            while st and st[-1][0] == lv:
+                x = (st.pop()[1], x)
+                lv += 1
+            st.append((lv, x))
+        if n % 2:
+            st.append((0, n - 1))
+        x = st.pop()[1]
+        while st:
+            x = (st.pop()[1], x)
+        return x
+
+    for n in range(1, 300):
+        assert ref(n) == counter(n), n
