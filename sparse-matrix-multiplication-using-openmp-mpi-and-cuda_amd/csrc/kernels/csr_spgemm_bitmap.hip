@@ -902,13 +902,14 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
     snl = 0;
   }
 
-  const int64_t NG = gridDim.x;
-  const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
-  const int64_t m = p.m;
+  // 32-bit row indices: the host takes this path only for m * nwin < 2^31
+  const int NG = (int)gridDim.x;
+  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+  const int m = (int)p.m;
 
   // row pipeline registers: rows me, me + NG, ...; row1 / row2 = the next two
   // rows of this workgroup
-  int64_t row = me, row1 = me + NG, row2 = me + 2 * NG;
+  int row = me, row1 = me + NG, row2 = me + 2 * NG;
   int ca0 = 0, cna = 0;           // its A row (scalars after the copy)
   float cav = 0.f;                // its A value (thread = entry)
   uint4 cwa = make_uint4(0, 0, 0, 0);   // its packed window bounds
@@ -922,13 +923,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   uint32_t nwb = 0;
   int64_t nuo = 0;
 
-  auto ld_arp = [&](int64_t r, int& a, int& b) {
+  auto ld_arp = [&](int r, int& a, int& b) {
     if (r < m) {
       a = (int)p.Arp[r + vz];
       b = (int)p.Arp[r + 1 + vz];
     }
   };
-  auto ld_entries = [&](int64_t r, int a, int b) {   // A entries of row r into njj / nav
+  auto ld_entries = [&](int r, int a, int b) {   // A entries of row r into njj / nav
     if (r < m) {
       const int a0 = __builtin_amdgcn_readfirstlane(a), na = __builtin_amdgcn_readfirstlane(b) - a0;
       if (tid < na) {
@@ -937,7 +938,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       }
     }
   };
-  auto ld_bounds = [&](int64_t r, int a, int b) {    // packed bounds + offsets of row r
+  auto ld_bounds = [&](int r, int a, int b) {    // packed bounds + offsets of row r
     if (r < m) {
       const int na = __builtin_amdgcn_readfirstlane(b) - __builtin_amdgcn_readfirstlane(a);
       if (tid < na) {
@@ -1287,29 +1288,30 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
 
   for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
 
-  const int64_t NG = gridDim.x;
-  const int64_t me = (NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
-  const int64_t m = p.m;
-  int64_t row = me;
+  // 32-bit row / unit indices: the host takes this path only for m * nwin < 2^31
+  const int NG = (int)gridDim.x;
+  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+  const int m = (int)p.m;
+  int row = me;
   int cna = 0;
   uint4 cwa = make_uint4(0, 0, 0, 0);
   uint32_t cwb = 0;
   int n1a = 0, n1b = 0, n2a = 0, n2b = 0, njj = 0;
   uint4 nwa = make_uint4(0, 0, 0, 0);
   uint32_t nwb = 0;
-  auto ld_arp = [&](int64_t r, int& a, int& b) {
+  auto ld_arp = [&](int r, int& a, int& b) {
     if (r < m) {
       a = (int)p.Arp[r + vz];
       b = (int)p.Arp[r + 1 + vz];
     }
   };
-  auto ld_entries = [&](int64_t r) {
+  auto ld_entries = [&](int r) {
     if (r < m) {
       const int a0 = __builtin_amdgcn_readfirstlane(n1a), na = __builtin_amdgcn_readfirstlane(n1b) - a0;
       if (tid < na) njj = p.Aci[a0 + tid];
     }
   };
-  auto ld_bounds = [&](int64_t r) {
+  auto ld_bounds = [&](int r) {
     if (r < m) {
       const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
       if (tid < na) {
@@ -1366,7 +1368,7 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
       const uint32_t b0 = bq;
       bq += PADC ? (uint32_t)(((len + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg) : (uint32_t)len;
       const int clo = q << LGW;
-      const int64_t u = row * nwin + q;
+      const int u = row * nwin + q;
       int pre, plen, TC, P;
       bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
       for (int cb = 0; cb < TC; cb += CCAP) {
