@@ -41,6 +41,13 @@
 #define SPMM_BM_SWEEP_G 2
 #endif
 
+#ifndef SPMM_BM_NUM_WIDE   // padded numeric rows: 2 pairs per lane and 16-byte loads (1) or 1 and 8-byte (0)
+#define SPMM_BM_NUM_WIDE 1    // (1M: numeric 52.8 -> 50.6 ms; the load-instruction count is what binds, PERF_LOG round 4)
+#endif
+#ifndef SPMM_BM_COUNT_WIDE   // padded row count: 4 columns per lane and 16-byte loads (1) or 2 and 8-byte (0)
+#define SPMM_BM_COUNT_WIDE 1    // (1M count 16.5 -> 15.3 ms, 64k step 1.485 -> 1.37 ms)
+#endif
+
 #ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
 #define SPMM_BM_P2_G 2   // 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586 (fewer empty rounds past the chunk count); 7 spills
 #endif
@@ -117,6 +124,19 @@ __device__ __forceinline__ int64_t bm_rfl64(int64_t x) {
   const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+
+// A unit's slots items[0, lim) to C[off, off + lim) (one store per entry and
+// array; 16-byte stores of four entries measured neutral, PERF_LOG round 4).
+template <int NT>
+__device__ __forceinline__ void bm_write_unit(const unsigned long long* items, int lim, int32_t* __restrict__ cci,
+                                              float* __restrict__ cv, int64_t off, uint32_t cmask) {
+  for (int i = threadIdx.x; i < lim; i += NT) {
+    const unsigned long long it = items[i];
+    BM_OUT(cci + (off + i), (int32_t)((uint32_t)it & cmask));
+    BM_OUT(cv + (off + i), __uint_as_float((uint32_t)(it >> 32)));
+  }
+}
+
 
 // Diagnostic phase stamps, compiled in only with -DSPMM_BM_STAMPS (the
 // accumulators cost registers): thread 0 of every workgroup adds the
@@ -807,11 +827,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         if (tid == 0) atomicOr(p.err, 2);
         lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : (int)want);
       }
-      for (int i = tid; i < lim; i += NT) {
-        const unsigned long long it = items[i];
-        BM_OUT(p.Cci + (off + i), (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu)));
-        BM_OUT(p.Cv + (off + i), __uint_as_float((uint32_t)(it >> 32)));
-      }
+      bm_write_unit<NT>(items, lim, p.Cci, p.Cv, off, DET ? kColMask : 0xFFFFFFFFu);
       clear_bm();
       __syncthreads();   // cleared (and items read) before the next unit's pass 1
       BM_STAMP(4);
@@ -859,12 +875,18 @@ __device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb
   return b;
 }
 
-template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET>
+// WIDE (padded pairs only): a lane loads TWO (column, value) pairs with one
+// 16-byte load -- half the lanes per chunk, half the load instructions; RR
+// product slots per lane filled by RR / 2 load rounds.
+template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET, bool WIDE = false>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
   constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
-  constexpr int RR = R;
+  constexpr int RR = R;                    // product slots per lane
+  constexpr int PPL = WIDE ? 2 : 1;        // pairs per lane and load
+  constexpr int RL = RR / PPL;             // load rounds
+  static_assert(!WIDE || (CV && !DET && RR % 2 == 0), "wide loads: interleaved pairs, unordered mode");
   constexpr int LCAP = DET ? 256 : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
   static_assert(WPW % 64 == 0 && PCAP < 65536, "geometry");
   static_assert(!DET || (CCAP << 6) <= (1 << kKeyBits), "DET keys fit 17 bits");
@@ -880,7 +902,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lg = p.lg;
+  const int lgc = p.lg;                    // log2 pairs per chunk
+  const int lg = lgc - (WIDE ? 1 : 0);     // log2 lanes per chunk
+  const int Gc = 1 << lgc;
   const int Gl = 1 << lg;
   const int ngrp = NW << (6 - lg);
   const int gid = (w << (6 - lg)) + (lane >> lg);
@@ -989,7 +1013,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       int len = 0, nch = 0;
       if (tid < na && tid < NT) {
         len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
-        nch = (len + Gl - 1) >> lg;
+        nch = (len + Gc - 1) >> lgc;
       }
       const uint32_t b0 = bq;
       bq += ra.pad ? (uint32_t)(((len + (1 << kPadLg) - 1) >> kPadLg) << kPadLg) : (uint32_t)len;
@@ -1002,7 +1026,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       const int want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
       int pre, plen, TC, P;
       bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-      const bool too_big = na > NT || P > PCAP || TC > CCAP || TC > R * ngrp;
+      const bool too_big = na > NT || P > PCAP || TC > CCAP || TC > RL * ngrp;
       if (P == 0 || too_big) {   // uniform
         if (too_big && P != 0 && tid == 0) {
           const uint32_t at = atomicAdd(p.novf, 1u);
@@ -1014,8 +1038,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
         continue;
       }
       for (int kk = 0; kk < nch; ++kk) {
-        const int rem = len - (kk << lg);
-        desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lg), (uint32_t)(rem < Gl ? rem : Gl));
+        const int rem = len - (kk << lgc);
+        desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lgc), (uint32_t)(rem < Gc ? rem : Gc));
         dval[pre + kk] = cav;
       }
       __syncthreads();
@@ -1023,29 +1047,40 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       // ---- pass 1 ----------------------------------------------------------
       const int nr = (TC + ngrp - 1) / ngrp;
       {
-        uint2 ds[RR];
+        uint2 ds[RL];
 #pragma unroll
-        for (int d = 0; d < RR; ++d) {
+        for (int d = 0; d < RL; ++d) {
           const int t = gid + d * ngrp;
           ds[d] = desc[t < TC ? t : TC - 1];
         }
-        uint32_t f[RR];
-        uint32_t okm = 0;
+        uint32_t f[RL];
+        uint32_t okm = 0;   // bit s: product slot s (round s / PPL, pair s % PPL) is in its segment
 #pragma unroll
-        for (int d = 0; d < RR; ++d) {
+        for (int d = 0; d < RL; ++d) {
           const int t = gid + d * ngrp;
-          const bool ok = (t < TC) & ((uint32_t)gl < ds[d].y);
-          okm |= (ok ? 1u : 0u) << d;
-          f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
+          const int nv = (int)ds[d].y - PPL * gl;
+          const bool ok = (t < TC) & (nv > 0);
+          okm |= (ok ? 1u : 0u) << (d * PPL);
+          if constexpr (WIDE) okm |= ((ok & (nv > 1)) ? 1u : 0u) << (d * PPL + 1);
+          f[d] = ds[d].x + (ok ? (uint32_t)(PPL * gl) : 0u);
         }
         int x[RR];
         float b[RR];
 #pragma unroll
-        for (int d = 0; d < RR; ++d) {
-          x[d] = 0;
-          b[d] = 0.f;
+        for (int d = 0; d < RL; ++d) {
+#pragma unroll
+          for (int h = 0; h < PPL; ++h) {
+            x[d * PPL + h] = 0;
+            b[d * PPL + h] = 0.f;
+          }
           if (d < nr) {   // wave-uniform
-            if constexpr (CV) {   // one 8-byte load: a chunk's products share cache lines
+            if constexpr (WIDE) {   // one 16-byte load: two pairs (chunks start on 128-byte lines)
+              const uint4 e = *reinterpret_cast<const uint4*>(p.Bcv + f[d]);
+              x[2 * d] = (int)e.x;
+              b[2 * d] = __uint_as_float(e.y);
+              x[2 * d + 1] = (int)e.z;
+              b[2 * d + 1] = __uint_as_float(e.w);
+            } else if constexpr (CV) {   // one 8-byte load: a chunk's products share cache lines
               const uint2 e = p.Bcv[f[d]];
               x[d] = (int)e.x;
               b[d] = __uint_as_float(e.y);
@@ -1057,9 +1092,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
         }
         // A values while the B loads are in flight
 #pragma unroll
-        for (int d = 0; d < RR; ++d) {
+        for (int d = 0; d < RL; ++d) {
           const int t = gid + d * ngrp;
-          v[d] = dval[t < TC ? t : TC - 1];
+          const float a = dval[t < TC ? t : TC - 1];
+#pragma unroll
+          for (int h = 0; h < PPL; ++h) v[d * PPL + h] = a;
         }
 #pragma unroll
         for (int d = 0; d < RR; ++d) {
@@ -1166,7 +1203,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       };
 #pragma unroll
       for (int d0 = 0; d0 < RR; d0 += 4) {
-        if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
+        if (d0 >= nr * PPL) break;   // uniform: slots past the unit's chunks hold no product
         int r[4];
 #pragma unroll
         for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
@@ -1234,11 +1271,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
         if (tid == 0) atomicOr(p.err, 2);
         lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : want);
       }
-      for (int i = tid; i < lim; i += NT) {
-        const unsigned long long it = items[i];
-        BM_OUT(p.Cci + (off + i), (int32_t)((uint32_t)it & (DET ? kColMask : 0xFFFFFFFFu)));
-        BM_OUT(p.Cv + (off + i), __uint_as_float((uint32_t)(it >> 32)));
-      }
+      bm_write_unit<NT>(items, lim, p.Cci, p.Cv, off, DET ? kColMask : 0xFFFFFFFFu);
       clear_bm();
       __syncthreads();
       BM_STAMP(4);
@@ -1266,7 +1299,12 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int WORDS_PER_WIN = NWORD / NSUB;
   static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
-  constexpr int SH = PADC ? 1 : 0;   // log2 columns per lane and load
+  // log2 columns per lane and load: padded columns are read 2 (8-byte loads)
+  // or, WIDE, 4 at a time (16-byte loads: half the load instructions, the
+  // host's lane groups halved to keep a chunk at one 128-byte line)
+  constexpr bool WIDE = PADC && SPMM_BM_COUNT_WIDE;
+  constexpr int SH = PADC ? (WIDE ? 2 : 1) : 0;
+  constexpr int CPL = 1 << SH;
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
@@ -1275,7 +1313,7 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lg = p.lg;
+  const int lg = p.lg - (WIDE ? 1 : 0);
   const int Gl = 1 << lg;
   const int ngrp = NW << (6 - lg);
   const int gid = (w << (6 - lg)) + (lane >> lg);
@@ -1392,28 +1430,36 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
             // two columns per lane: one 8-byte load (aligned: chunks start on
             // 32-column boundaries of the padded array); the second column
             // may be past the segment (padding)
-            uint2 x[RR];
-            uint32_t okm = 0, ok2m = 0;
+            static_assert(RR * CPL <= 32, "one bit per loaded column");
+            uint32_t x[RR][CPL];
+            uint32_t okb = 0;   // bit d * CPL + i: column i of round d is in its segment
 #pragma unroll
             for (int d = 0; d < RR; ++d) {
               const int t = gid + (i0 + d) * ngrp;
-              const int nv = (int)ds[d].y - 2 * gl;
+              const int nv = (int)ds[d].y - CPL * gl;
               const bool ok = (t < TCb) & (nv > 0);
-              okm |= (ok ? 1u : 0u) << d;
-              ok2m |= (ok & (nv > 1) ? 1u : 0u) << d;
-              x[d] = make_uint2(0u, 0u);
-              if (i0 + d < nr)   // wave-uniform guard
-                x[d] = *reinterpret_cast<const uint2*>(p.Bci + ds[d].x + (ok ? 2u * (uint32_t)gl : 0u));
+              okb |= (ok ? ((nv >= CPL) ? (1u << CPL) - 1u : (1u << nv) - 1u) : 0u) << (d * CPL);
+#pragma unroll
+              for (int i = 0; i < CPL; ++i) x[d][i] = 0u;
+              if (i0 + d < nr) {   // wave-uniform guard
+                const int32_t* src = p.Bci + ds[d].x + (ok ? (uint32_t)(CPL * gl) : 0u);
+                if constexpr (WIDE) {
+                  const uint4 v = *reinterpret_cast<const uint4*>(src);
+                  x[d][0] = v.x; x[d][1] = v.y; x[d][2] = v.z; x[d][3] = v.w;
+                } else {
+                  const uint2 v = *reinterpret_cast<const uint2*>(src);
+                  x[d][0] = v.x; x[d][1] = v.y;
+                }
+              }
             }
 #pragma unroll
             for (int d = 0; d < RR; ++d) {
-              if ((okm >> d) & 1u) {
-                const int cc = (int)x[d].x - clo;
-                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
-              }
-              if ((ok2m >> d) & 1u) {
-                const int cc = (int)x[d].y - clo;
-                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+#pragma unroll
+              for (int i = 0; i < CPL; ++i) {
+                if ((okb >> (d * CPL + i)) & 1u) {
+                  const int cc = (int)x[d][i] - clo;
+                  atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+                }
               }
             }
           } else {
@@ -1658,9 +1704,9 @@ __global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __rest
 //          count 2 windows (8 KB, 512 threads); fast <= 3840 products, SPMM_BM_CFG1_R (14) rounds
 //   cfg 2: W = 2^16: count 4 windows (32 KB, 1024 threads); fast <= 3072, 16 rounds
 // Reload (deferred units): min(1024, W / 64) threads, <= 12288 products, 2048 chunks.
-//   cfg 3: W = 2^18 (1M columns: 4 windows per row, ~2.7k products per window):
-//          row kernel 512 threads, <= 4096 products (2 workgroups per CU);
-//          row count 2 windows per unit (64 KB bitmap, 512 threads)
+// (A W = 2^18 configuration with a 512-thread row kernel -- longer, better
+// aligned segments -- measured 82 vs 76 ms on the 1M step and was removed:
+// its units are latency-bound at 2 workgroups per CU, PERF_LOG round 4.)
 // Wider windows mean longer contiguous B segments per (A entry, unit): random
 // segment gathers run at ~7 TB/s of 128-byte LINES, so 100-byte segments
 // deliver ~3.2 TB/s of useful bytes and 200-byte ones ~4.4
@@ -1671,20 +1717,13 @@ struct BmCfg {
 #ifndef SPMM_BM_CFG1_R   // register rounds of cfg 1's per-unit fast kernel (the 65536^2 config)
 #define SPMM_BM_CFG1_R 14   // 65536^2: 16 rounds spill 5 VGPRs; 14 = 1.64 -> 1.56 ms (384 of 131072 units deferred), 13: 1.61-1.67, 12: 1.82
 #endif
-#ifndef SPMM_BM_CFG3_R   // register rounds of cfg 3's 512-thread row kernel
-#define SPMM_BM_CFG3_R 9
-#endif
-#ifndef SPMM_BM_CFG3_PCAP
-#define SPMM_BM_CFG3_PCAP 4096
-#endif
 constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12, 256, SPMM_BM_ROWS_R},
                            {15, 2, 3840, SPMM_BM_CFG1_R, 256, SPMM_BM_ROWS_R},
-                           {16, 4, 3072, 16, 256, SPMM_BM_ROWS_R},
-                           {18, 2, SPMM_BM_CFG3_PCAP, SPMM_BM_CFG3_R, 512, SPMM_BM_CFG3_R}};
-constexpr int kNumCfgs = 4;
+                           {16, 4, 3072, 16, 256, SPMM_BM_ROWS_R}};
+constexpr int kNumCfgs = 3;
 constexpr int kFastNT = 256, kReloadCcap = 2048;
-// reload product slots: 96 KB of items (80 KB next to W = 2^18's 32 KB bitmap + 8 KB prefixes)
-constexpr int reload_pcap(int lgw) { return lgw >= 18 ? 10112 : 12288; }
+// reload product slots: 96 KB of items
+constexpr int reload_pcap(int) { return 12288; }
 // reload workgroup: up to 1024 threads (the longest A row it can stage), at
 // most one wave per 64 bitmap words
 constexpr int reload_nt(int lgw) { return ((1 << lgw) / 64) < 1024 ? ((1 << lgw) / 64) : 1024; }
@@ -1730,6 +1769,7 @@ struct BmRowKernel {
   static constexpr int R = K.rounds_fast > K.rows_r ? K.rows_r : K.rounds_fast;
   static constexpr auto k = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, false>;
   static constexpr auto kcv = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false>;
+  static constexpr auto kcvw = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false, R % 2 == 0>;
   static constexpr auto k_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, true>;
   static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, true>;
 };
@@ -1764,7 +1804,8 @@ template <int C, int NSUB>
 struct BmRowCountKernel {
   static constexpr int NT = count_nt(kCfgs[C].lgw, NSUB);
   static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, false>;
-  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, true>;
+  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT,
+                                                  SPMM_BM_COUNT_WIDE ? SPMM_BM_COUNT_RR / 2 : SPMM_BM_COUNT_RR, 256, true>;
 };
 
 template <int C>
@@ -1783,8 +1824,10 @@ int bm_count_rows(BmRowArgs ra, int nsub, hipStream_t s) {
 template <int C>
 int bm_numeric_rows(BmRowArgs ra, int det, hipStream_t s) {
   using K = BmRowKernel<C>;
+  const bool wide = SPMM_BM_NUM_WIDE && ra.a.Bcv && ra.pad && ra.a.lg >= 1;   // (16-byte loads need the padded pairs)
   const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
-                     : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT));
+                     : (wide ? launch_rows(K::kcvw, ra, s, K::NT)
+                             : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT)));
   if (rc) return rc;
   return det ? launch_bm(BmKernels<C>::reload_det, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s)
              : launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
@@ -1840,8 +1883,7 @@ SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t*
   switch (cfg) {
     case 0: return bm_count<0>(work, a, s);
     case 1: return bm_count<1>(work, a, s);
-    case 2: return bm_count<2>(work, a, s);
-    default: return bm_count<3>(work, a, s);
+    default: return bm_count<2>(work, a, s);
   }
 }
 
@@ -1862,8 +1904,7 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_
   switch (cfg) {
     case 0: return bm_numeric<0>(work, a, det, s);
     case 1: return bm_numeric<1>(work, a, det, s);
-    case 2: return bm_numeric<2>(work, a, det, s);
-    default: return bm_numeric<3>(work, a, det, s);
+    default: return bm_numeric<2>(work, a, det, s);
   }
 }
 
@@ -1935,8 +1976,7 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
   switch (cfg) {
     case 0: return bm_numeric_rows<0>(ra, det, s);
     case 1: return bm_numeric_rows<1>(ra, det, s);
-    case 2: return bm_numeric_rows<2>(ra, det, s);
-    default: return bm_numeric_rows<3>(ra, det, s);
+    default: return bm_numeric_rows<2>(ra, det, s);
   }
 }
 
@@ -1957,8 +1997,7 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
   switch (cfg) {
     case 0: return bm_count_rows<0>(ra, nsub, s);
     case 1: return bm_count_rows<1>(ra, nsub, s);
-    case 2: return bm_count_rows<2>(ra, nsub, s);
-    default: return bm_count_rows<3>(ra, nsub, s);
+    default: return bm_count_rows<2>(ra, nsub, s);
   }
 }
 

@@ -690,7 +690,7 @@ def _bm_pick(mean_row_products: float, ncols: int) -> Optional[int]:
     """The configuration with the widest window whose mean products per window
     fit BM_FILL of its fast capacity (widest = fewest units per row)."""
     best = None
-    for cfg in (0, 2, 1):   # widest window first (cfg 3 by request only: 82 vs 76 ms on the 1M step)
+    for cfg in (0, 2, 1):   # widest window first
         lgw, _, pcap, _, _ = _bm_config(cfg)
         W = 1 << lgw
         per_window = mean_row_products * min(W, ncols) / max(ncols, 1)
@@ -760,7 +760,7 @@ def _bitmap_plan(A: CSR, B: CSR, info: SpgemmInfo, pre: Optional[dict]) -> Optio
                       lg_c=4 if sl < 48 else (5 if sl < 96 else 6), nsub_c=nsub_c,
                       lg_num=4 if seg / nwin < 48 else (5 if seg / nwin < 96 else 6),
                       count_rows=ws8_ok and pre is not None and pre.get("amax", 1 << 30) <= 256,
-                      rows=ws8_ok and (rows_mode == "on" or cfg in (0, 3)),
+                      rows=ws8_ok and (rows_mode == "on" or cfg == 0),
                       det=CONFIG.spgemm_deterministic > 0, tot=tot)
 
 

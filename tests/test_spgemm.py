@@ -583,18 +583,19 @@ def test_spgemm_gpu_bitmap_matches_binned(monkeypatch, cfg, m, k, n, da, db):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("count_windows,n", [(2, 700000), (4, 700000), (2, 1 << 20), (4, 1 << 20)])
-def test_spgemm_gpu_bitmap_wide_windows(monkeypatch, count_windows, n):
-    """cfg 3 (2^18-column windows, 512-thread row kernel, the 1M config's
-    pick): ragged last window (n = 700000: 3 windows, the count unit's second
-    window past the end), count units of 2 and 4 windows, n below one window."""
+def test_spgemm_gpu_bitmap_count_units(monkeypatch, count_windows, n):
+    """Row count kernel with units of 2 and 4 windows over the padded column
+    groups (16-byte column loads), the 1M config's window (cfg 0: 2^17):
+    ragged last window (n = 700000: 6 windows, the last count unit partly
+    past the end) and exactly 8 windows."""
     from spmm_amd.utils.config import CONFIG
 
     dev = torch.device("cuda")
     A = gen_csr.uniform_csr(3000, 20000, 0.004, seed=61, device=dev)
     B = gen_csr.uniform_csr(20000, n, 100.0 / n, seed=62, device=dev)
     monkeypatch.setattr(CONFIG, "spgemm_bitmap_count_windows", count_windows)
-    info = _bitmap_vs_binned(monkeypatch, A, B, 3)
-    assert info.rows_per_bin_num.get("bitmap_cfg") == 3 and info.rows_per_bin_num.get("bitmap_rows") == 1, \
+    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    assert info.rows_per_bin_num.get("bitmap_cfg") == 0 and info.rows_per_bin_num.get("bitmap_rows") == 1, \
         info.rows_per_bin_num
 
 
