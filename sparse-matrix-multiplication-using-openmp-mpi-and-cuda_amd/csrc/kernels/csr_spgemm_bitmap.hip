@@ -258,20 +258,30 @@ struct BmArgs {
   int64_t ovf_cap;
   int64_t cap;             // numeric: entries allocated for C (a unit outside it is an error, never a write)
   const uint2* Bcv;        // row-major numeric: B as interleaved (column, value bits), or null
+                           // (per-unit WIDE numeric: the padded pair array)
   int32_t* err;            // bit 0: a deferred unit exceeds the reload budget (host falls back)
                            // bit 1: count / numeric disagree (kernel invariant)
                            // bit 2: deferred list full (host falls back)
+  const uint4* ws8 = nullptr;   // per-unit WIDE numeric: packed window bounds + padded pair bases
 };
+constexpr int kPadLg = 4;    // padded segments: multiples of 2^4 pairs (128 bytes)
+constexpr int kPadCLg = 5;   // padded count segments (column groups of a count unit): 2^5 columns (128 bytes)
 
 // CV: B read as interleaved (column, value bits) pairs (p.Bcv): one 8-byte load
 // per product instead of two 4-byte ones (numeric modes only)
-template <int LGW, int NSUB, int NT, int PCAP, int R, int CCAP, int MODE, bool DET = false, bool CV = false>
+// WIDE (fast numeric, padded pairs): two pairs per lane and 16-byte loads, as
+// in the row kernel; the window bounds come from ws8 (padded segment starts).
+template <int LGW, int NSUB, int NT, int PCAP, int R, int CCAP, int MODE, bool DET = false, bool CV = false,
+          bool WIDE = false>
 __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   using Gm = BmGeom<LGW, NSUB, NT, PCAP, R, CCAP, MODE>;
   constexpr int NW = NT / 64;
   constexpr bool VALUES = MODE != 0;
   constexpr int NWORD = Gm::NWORD, WPW = Gm::WPW, WPT = Gm::WPT;
-  constexpr int RR = MODE == 1 ? R : (MODE == 0 ? 16 : 8);   // rounds of loads in flight per block
+  constexpr int RR = MODE == 1 ? R : (MODE == 0 ? 16 : 8);   // product slots per lane
+  constexpr int PPL = WIDE ? 2 : 1;   // pairs per lane and load
+  constexpr int RL = RR / PPL;        // load rounds
+  static_assert(!WIDE || (MODE == 1 && CV && !DET && RR % 2 == 0), "wide loads: fast numeric, interleaved pairs");
   // deterministic fix-up list: the fast kernel defers a unit that overflows
   // it to the reload kernel, whose list is larger (it has one CU's LDS)
   constexpr int LCAP = !DET ? 1 : (MODE == 2 ? 1024 : 64);
@@ -293,7 +303,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lg = p.lg;
+  const int lgc = p.lg;                  // log2 pairs per chunk
+  const int lg = lgc - (WIDE ? 1 : 0);   // log2 lanes per chunk
+  const int Gc = 1 << lgc;
   const int Gl = 1 << lg;
   const int ngrp = NW << (6 - lg);
   const int gid = (w << (6 - lg)) + (lane >> lg);
@@ -410,9 +422,26 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
     if (live(h)) {
       const int na = __builtin_amdgcn_readfirstlane(rb) - __builtin_amdgcn_readfirstlane(ra);
       if (tid < na) {
-        const uint32_t* wr = p.ws + (int64_t)j * nw1;
-        b0 = wr[q0_of(h)];
-        b1 = wr[q1_of(h)];
+        if constexpr (WIDE) {   // the unit's segment in the padded pair array
+          const uint4 wa = p.ws8[2 * (int64_t)j];
+          const uint32_t wb = p.ws8[2 * (int64_t)j + 1].x;
+          uint32_t st = p.ws8[2 * (int64_t)j + 1].y;
+          const int q = q0_of(h);
+          uint32_t ln = 0;
+#pragma unroll
+          for (int qq = 0; qq < 8; ++qq) {
+            const uint32_t word = qq < 2 ? wa.y : qq < 4 ? wa.z : qq < 6 ? wa.w : wb;
+            const uint32_t l = (word >> (16 * (qq & 1))) & 0xffffu;
+            if (qq < q) st += ((l + (1u << kPadLg) - 1) >> kPadLg) << kPadLg;
+            if (qq == q) ln = l;
+          }
+          b0 = st;
+          b1 = st + ln;
+        } else {
+          const uint32_t* wr = p.ws + (int64_t)j * nw1;
+          b0 = wr[q0_of(h)];
+          b1 = wr[q1_of(h)];
+        }
       }
       if constexpr (VALUES) {
         oa = p.uoff[h.u + vz];
@@ -438,29 +467,40 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   int c[RR];
   float v[RR];
   auto fetch = [&](int i0, int nr, int TC, int clo) {
-    Desc ds[RR];
+    Desc ds[RL];
 #pragma unroll
-    for (int d = 0; d < RR; ++d) {
+    for (int d = 0; d < RL; ++d) {
       const int t = gid + (i0 + d) * ngrp;
       ds[d] = desc[t < TC ? t : TC - 1];
     }
-    uint32_t f[RR];
-    uint32_t okm = 0;
+    uint32_t f[RL];
+    uint32_t okm = 0;   // bit s: product slot s (round s / PPL, pair s % PPL) is in its segment
 #pragma unroll
-    for (int d = 0; d < RR; ++d) {
+    for (int d = 0; d < RL; ++d) {
       const int t = gid + (i0 + d) * ngrp;
-      const bool ok = (t < TC) & ((uint32_t)gl < ds[d].y);
-      okm |= (ok ? 1u : 0u) << d;
-      f[d] = ds[d].x + (ok ? (uint32_t)gl : 0u);
+      const int nv = (int)ds[d].y - PPL * gl;
+      const bool ok = (t < TC) & (nv > 0);
+      okm |= (ok ? 1u : 0u) << (d * PPL);
+      if constexpr (WIDE) okm |= ((ok & (nv > 1)) ? 1u : 0u) << (d * PPL + 1);
+      f[d] = ds[d].x + (ok ? (uint32_t)(PPL * gl) : 0u);
     }
     int x[RR];
     float b[RR];
 #pragma unroll
-    for (int d = 0; d < RR; ++d) {
-      x[d] = 0;
-      b[d] = 0.f;
+    for (int d = 0; d < RL; ++d) {
+#pragma unroll
+      for (int hh = 0; hh < PPL; ++hh) {
+        x[d * PPL + hh] = 0;
+        b[d * PPL + hh] = 0.f;
+      }
       if (i0 + d < nr) {   // wave-uniform
-        if constexpr (CV && VALUES) {
+        if constexpr (WIDE) {   // one 16-byte load: two pairs (segments start on 128-byte lines)
+          const uint4 e = *reinterpret_cast<const uint4*>(p.Bcv + f[d]);
+          x[2 * d] = (int)e.x;
+          b[2 * d] = __uint_as_float(e.y);
+          x[2 * d + 1] = (int)e.z;
+          b[2 * d + 1] = __uint_as_float(e.w);
+        } else if constexpr (CV && VALUES) {
           const uint2 e = p.Bcv[f[d]];
           x[d] = (int)e.x;
           b[d] = __uint_as_float(e.y);
@@ -473,7 +513,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 #pragma unroll
     for (int d = 0; d < RR; ++d) {
       c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
-      if constexpr (VALUES) v[d] = __uint_as_float(reinterpret_cast<const uint4&>(ds[d]).z) * b[d];
+      if constexpr (VALUES) v[d] = __uint_as_float(reinterpret_cast<const uint4&>(ds[d / PPL]).z) * b[d];
     }
   };
   // OR the columns into the bitmap.  Numeric mode keeps the old words: a
@@ -592,12 +632,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       int len = 0, nch = 0;
       if (tid < na && tid < NT) {
         len = (int)(bk1 - bk0);
-        nch = (len + Gl - 1) >> lg;
+        nch = (len + Gc - 1) >> lgc;
       }
       int pre, plen, TC, P;
       bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
       if (P == 0) continue;   // uniform; the count kernel wrote 0 for this unit
-      const bool too_big = na > NT || P > PCAP || TC > CCAP || (MODE == 1 && TC > R * ngrp);
+      const bool too_big = na > NT || P > PCAP || TC > CCAP || (MODE == 1 && TC > RL * ngrp);
       if (too_big) {   // uniform
         if (tid == 0) {
           if (MODE == 1) {
@@ -612,10 +652,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         continue;
       }
       for (int kk = 0; kk < nch; ++kk) {
-        const int rem = len - (kk << lg);
+        const int rem = len - (kk << lgc);
         Desc dd{};
-        dd.x = bk0 + ((uint32_t)kk << lg);
-        dd.y = (uint32_t)(rem < Gl ? rem : Gl);
+        dd.x = bk0 + ((uint32_t)kk << lgc);
+        dd.y = (uint32_t)(rem < Gc ? rem : Gc);
         reinterpret_cast<uint4&>(dd).z = __float_as_uint(avk);
         desc[pre + kk] = dd;
       }
@@ -722,7 +762,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         constexpr int P2G = SPMM_BM_P2_G;
 #pragma unroll
         for (int d0 = 0; d0 < RR; d0 += P2G) {
-          if (d0 >= nr) break;   // uniform: rounds past the unit's chunks hold no product
+          if (d0 >= nr * PPL) break;   // uniform: slots past the unit's chunks hold no product
           int r[P2G];
 #pragma unroll
           for (int dd = 0; dd < P2G && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
@@ -861,8 +901,6 @@ struct BmRowArgs {
   const uint4* ws8;
   int pad;   // numeric: Bcv is the padded pair array
 };
-constexpr int kPadLg = 4;    // padded segments: multiples of 2^4 pairs (128 bytes)
-constexpr int kPadCLg = 5;   // padded count segments (column groups of a count unit): 2^5 columns (128 bytes)
 
 // First B index of window q0 inside this entry's B row: the row start plus
 // the packed 16-bit lengths of windows 0 .. q0-1.
@@ -1735,6 +1773,8 @@ struct BmKernels {
   static constexpr auto count = spgemm_bm<K.lgw, K.nsub_count, kCountNT, 2, 1, 2048, 0>;
   static constexpr auto fast = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
                                          K.rounds_fast * (kFastNT / 16), 1>;
+  static constexpr auto fast_wide = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
+                                              K.rounds_fast * (kFastNT / 16), 1, false, true, K.rounds_fast % 2 == 0>;
   static constexpr int kReloadNT = reload_nt(K.lgw);
   static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2>;
   static constexpr auto fast_det = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
@@ -1836,7 +1876,9 @@ int bm_numeric_rows(BmRowArgs ra, int det, hipStream_t s) {
 template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, int det, hipStream_t s) {
   using K = BmKernels<C>;
-  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s);
+  const bool wide = a.ws8 != nullptr && a.Bcv != nullptr && a.lg >= 1;   // padded pairs given
+  const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s)
+                     : (wide ? launch_bm(K::fast_wide, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s));
   if (rc) return rc;
   return det ? launch_bm(K::reload_det, K::kReloadNT, int64_t(1) << 30, a, s)
              : launch_bm(K::reload, K::kReloadNT, int64_t(1) << 30, a, s);
@@ -1895,10 +1937,12 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_
                                        const uint32_t* ws, const int32_t* Bci, const float* Bv, int64_t m, int nwin,
                                        int lg, const int64_t* uoff, int64_t cap, int32_t* Cci, float* Cv,
                                        int32_t* ovf, uint32_t* novf, int64_t ovf_cap, int32_t* err, int det,
-                                       void* stream) {
+                                       const void* ws8, const void* bcv_padded, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1) return (int)hipErrorInvalidValue;
-  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap, nullptr, err};
+  if ((ws8 != nullptr) != (bcv_padded != nullptr) || (ws8 != nullptr && nwin > 8)) return (int)hipErrorInvalidValue;
+  BmArgs a{Arp, Aci, Av, ws, Bci, Bv, m, nwin, lg, nullptr, uoff, Cci, Cv, ovf, novf, ovf_cap, cap,
+           (const uint2*)bcv_padded, err, (const uint4*)ws8};
   hipStream_t s = (hipStream_t)stream;
   const int64_t work = m * nwin;
   switch (cfg) {

@@ -45,7 +45,7 @@ int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const 
 int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av, const uint32_t* ws,
                            const int32_t* Bci, const float* Bv, int64_t m, int nwin, int lg, const int64_t* uoff,
                            int64_t cap, int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                           int32_t* err, int det, void* stream);
+                           int32_t* err, int det, const void* ws8, const void* bcv_padded, void* stream);
 }
 
 namespace a4 {
@@ -152,7 +152,7 @@ bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
   DevBuf<int32_t> ovf((size_t)ovf_cap, s);
   A4_HIP((hipError_t)spmm_spgemm_bm_numeric(cfg, A.rp.get(), A.ci.get(), A.v.get(), ws.get(), B.ci.get(), B.v.get(),
                                             A.m, nwin, lg_num, uoff.get(), nnz, C.ci.get(), C.v.get(), ovf.get(),
-                                            (uint32_t*)(err.get() + 1), ovf_cap, err.get(), 0, s));
+                                            (uint32_t*)(err.get() + 1), ovf_cap, err.get(), 0, nullptr, nullptr, s));
   const int e = down(err.get(), 1, s)[0];
   A4_CHECK((e & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
   if (e & 5) return false;   // a unit beyond the reload kernel's budget: the binned path redoes the product

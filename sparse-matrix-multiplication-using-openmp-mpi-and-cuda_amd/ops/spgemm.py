@@ -74,7 +74,7 @@ _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64,
                      c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
-                     C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp)
+                     C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp, c_vp, c_vp)
 
 # LDS bins (csr_spgemm.hip: every table <= 80 KB so two workgroups share a CU).
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
@@ -794,11 +794,12 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     nnzb = _true_nnz(B)
     ngc = -(-nwin // plan.nsub_c)
     pad = CONFIG.spgemm_bitmap_pad > 0 and use_ws8
-    pad_num = pad and plan.rows and CONFIG.spgemm_bitmap_cv and nnzb + 15 * nwin * B.m < (1 << 32)
+    # (the per-unit fast kernel reads the padded pairs too, two per lane; not in deterministic mode)
+    pad_num = pad and (plan.rows or not plan.det) and CONFIG.spgemm_bitmap_cv and nnzb + 15 * nwin * B.m < (1 << 32)
     pad_cnt = pad and plan.count_rows and nnzb + 31 * ngc * B.m < (1 << 32)
     plen = torch.empty(B.m, dtype=torch.int64, device=dev) if pad_num else None
     plen_c = torch.empty(B.m, dtype=torch.int64, device=dev) if pad_cnt else None
-    if use_ws8 and (plan.count_rows or plan.rows):
+    if use_ws8 and (plan.count_rows or plan.rows or pad_num):
         ws8 = torch.empty(B.m * 8, dtype=torch.int32, device=dev)
         _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err),
                                                   P(plen) if plen is not None else None,
@@ -847,19 +848,22 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
     det = int(plan.det)
+    Bcv = None
+    if ws8 is not None and plen is not None:
+        # interleaved (column, value) pairs with every window segment starting
+        # on a 128-byte line: the numeric kernels take two pairs per 16-byte load
+        pbase = torch.cumsum(plen, 0)
+        pbase -= plen
+        Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
+        _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, P(pbase), P(ws8),
+                                                   P(Bcv), None, 1, None, Bcv.shape[0], 0, P(err), st),
+                      "spgemm_bm_pad_pairs")
+        del pbase
     if ws8 is not None and plan.rows:
         # the row-major kernel reads B as interleaved (column, value) pairs: one
-        # 8-byte stream per chunk instead of two 4-byte ones; padded, each
-        # window segment starts on a 128-byte line
-        if plen is not None:
-            pbase = torch.cumsum(plen, 0)
-            pbase -= plen
-            Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
-            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, P(pbase), P(ws8),
-                                                       P(Bcv), None, 1, None, Bcv.shape[0], 0, P(err), st),
-                          "spgemm_bm_pad_pairs")
-            del pbase
-        else:
+        # stream per chunk instead of two; padded, each window segment starts on
+        # a 128-byte line
+        if Bcv is None:
             Bcv = interleaved(B) if CONFIG.spgemm_bitmap_cv else None
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
@@ -869,9 +873,11 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
         if info is not None:
             info.rows_per_bin_num["bitmap_rows"] = 1
     else:
+        wide = Bcv is not None and not det
         _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
                                                  nwin, plan.lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf),
-                                                 ovf_cap, P(err), det, st),
+                                                 ovf_cap, P(err), det, P(ws8) if wide else None,
+                                                 P(Bcv) if wide else None, st),
                       "spgemm_bm_numeric")
     out.update(Cci=Cci, Cv=Cv, cap=cap, n=B.n)
     return out
