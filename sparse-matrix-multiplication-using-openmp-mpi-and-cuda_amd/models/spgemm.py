@@ -61,8 +61,9 @@ class OperandReady:
     splits and count kernel read only B's columns, so they run while the
     values are still crossing xGMI."""
 
-    def __init__(self, full: Callable[[], CSR], cols: Optional[Callable[[], CSR]] = None):
+    def __init__(self, full: Callable[[], CSR], cols: Optional[Callable[[], CSR]] = None, local: bool = False):
         self._full, self._cols = full, cols
+        self.local = local   # the operand never left this rank: its values are already readable
 
     def __call__(self) -> CSR:
         return self._full()
@@ -136,7 +137,7 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
     the columns-only operand (see :class:`OperandReady`).
     """
     if not comm.is_dist:
-        return panel, OperandReady(lambda: panel)
+        return panel, OperandReady(lambda: panel, local=True)
     dev = panel.device
     W = comm.world
     meta = comm.all_gather(torch.tensor([panel.m, panel.nnz], dtype=torch.int64, device=dev)).view(-1, 2)

@@ -486,6 +486,7 @@ def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, two_phase: bool = Fa
             return cached[0]
         # the columns-only stage of a two-stage gather (see models.spgemm.OperandReady)
         B_ready.cols = getattr(fetch, "cols", B_ready)
+        B_ready.local = getattr(fetch, "local", False)
     if not two_phase:
         if _bitmap_ok(A, B, info.flops // 2, pre):
             C_ = onepass_bitmap(A, B, info, B_ready, pre)
@@ -805,16 +806,27 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
                                                   P(plen) if plen is not None else None,
                                                   P(plen_c) if plen_c is not None else None, plan.nsub_c, st),
                       "spgemm_bm_pack_ws8")
+    Bcv = None
     if ws8 is not None and plan.count_rows:
         colp = None
-        if plen_c is not None:   # (columns only: B's values may still be in flight)
+        if plen_c is not None:
             cbase = torch.cumsum(plen_c, 0)
             cbase -= plen_c
             colp = torch.empty(nnzb + 31 * ngc * B.m, dtype=torch.int32, device=dev)
-            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), None, B.m, nwin, None, P(ws8), None, P(cbase),
-                                                       plan.nsub_c, P(colp), 0, colp.numel(), P(err), st),
+            # B's values are here (no all-gather in flight): both layouts in one pass
+            both = plen is not None and (B_ready is None or getattr(B_ready, "local", False))
+            pbase = None
+            if both:
+                pbase = torch.cumsum(plen, 0)
+                pbase -= plen
+                Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
+            # (otherwise columns only: B's values may still be in flight)
+            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val) if both else None, B.m, nwin,
+                                                       P(pbase) if both else None, P(ws8), P(Bcv) if both else None,
+                                                       P(cbase), plan.nsub_c, P(colp),
+                                                       Bcv.shape[0] if both else 0, colp.numel(), P(err), st),
                           "spgemm_bm_pad_pairs(columns)")
-            del cbase, plen_c
+            del cbase, plen_c, pbase
         _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8),
                                                     P(colp) if colp is not None else P(B.col), m, nwin, plan.lg_c,
                                                     plan.nsub_c, P(ucnt), P(err),
@@ -848,8 +860,7 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     ovf_cap = min(nunits, 1 << 20)
     ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
     det = int(plan.det)
-    Bcv = None
-    if ws8 is not None and plen is not None:
+    if ws8 is not None and plen is not None and Bcv is None:
         # interleaved (column, value) pairs with every window segment starting
         # on a 128-byte line: the numeric kernels take two pairs per 16-byte load
         pbase = torch.cumsum(plen, 0)
