@@ -41,13 +41,6 @@
 #define SPMM_BM_SWEEP_G 2
 #endif
 
-#ifndef SPMM_BM_NUM_WIDE   // padded numeric rows: 2 pairs per lane and 16-byte loads (1) or 1 and 8-byte (0)
-#define SPMM_BM_NUM_WIDE 1    // (1M: numeric 52.8 -> 50.6 ms; the load-instruction count is what binds, PERF_LOG round 4)
-#endif
-#ifndef SPMM_BM_COUNT_WIDE   // padded row count: 4 columns per lane and 16-byte loads (1) or 2 and 8-byte (0)
-#define SPMM_BM_COUNT_WIDE 1    // (1M count 16.5 -> 15.3 ms, 64k step 1.485 -> 1.37 ms)
-#endif
-
 #ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
 #define SPMM_BM_P2_G 2   // 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586 (fewer empty rounds past the chunk count); 7 spills
 #endif
@@ -1337,11 +1330,12 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
   constexpr int WORDS_PER_WIN = NWORD / NSUB;
   static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
-  // log2 columns per lane and load: padded columns are read 2 (8-byte loads)
-  // or, WIDE, 4 at a time (16-byte loads: half the load instructions, the
-  // host's lane groups halved to keep a chunk at one 128-byte line)
-  constexpr bool WIDE = PADC && SPMM_BM_COUNT_WIDE;
-  constexpr int SH = PADC ? (WIDE ? 2 : 1) : 0;
+  // log2 columns per lane and load: padded columns are read 4 at a time
+  // (16-byte loads: the gathers are bound by their load-instruction count,
+  // 1M count 16.5 -> 15.3 ms vs 8-byte loads, PERF_LOG round 4), the host's
+  // lane groups halved to keep a chunk at one 128-byte line
+  constexpr bool WIDE = PADC;
+  constexpr int SH = PADC ? 2 : 0;
   constexpr int CPL = 1 << SH;
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
@@ -1465,8 +1459,8 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
             ds[d] = desc[t < TCb ? t : TCb - 1];
           }
           if constexpr (PADC) {
-            // two columns per lane: one 8-byte load (aligned: chunks start on
-            // 32-column boundaries of the padded array); the second column
+            // four columns per lane: one 16-byte load (aligned: chunks start on
+            // 32-column boundaries of the padded array); the later columns
             // may be past the segment (padding)
             static_assert(RR * CPL <= 32, "one bit per loaded column");
             uint32_t x[RR][CPL];
@@ -1480,14 +1474,8 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
 #pragma unroll
               for (int i = 0; i < CPL; ++i) x[d][i] = 0u;
               if (i0 + d < nr) {   // wave-uniform guard
-                const int32_t* src = p.Bci + ds[d].x + (ok ? (uint32_t)(CPL * gl) : 0u);
-                if constexpr (WIDE) {
-                  const uint4 v = *reinterpret_cast<const uint4*>(src);
-                  x[d][0] = v.x; x[d][1] = v.y; x[d][2] = v.z; x[d][3] = v.w;
-                } else {
-                  const uint2 v = *reinterpret_cast<const uint2*>(src);
-                  x[d][0] = v.x; x[d][1] = v.y;
-                }
+                const uint4 v = *reinterpret_cast<const uint4*>(p.Bci + ds[d].x + (ok ? (uint32_t)(CPL * gl) : 0u));
+                x[d][0] = v.x; x[d][1] = v.y; x[d][2] = v.z; x[d][3] = v.w;
               }
             }
 #pragma unroll
@@ -1844,8 +1832,7 @@ template <int C, int NSUB>
 struct BmRowCountKernel {
   static constexpr int NT = count_nt(kCfgs[C].lgw, NSUB);
   static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, false>;
-  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT,
-                                                  SPMM_BM_COUNT_WIDE ? SPMM_BM_COUNT_RR / 2 : SPMM_BM_COUNT_RR, 256, true>;
+  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR / 2, 256, true>;
 };
 
 template <int C>
@@ -1864,7 +1851,9 @@ int bm_count_rows(BmRowArgs ra, int nsub, hipStream_t s) {
 template <int C>
 int bm_numeric_rows(BmRowArgs ra, int det, hipStream_t s) {
   using K = BmRowKernel<C>;
-  const bool wide = SPMM_BM_NUM_WIDE && ra.a.Bcv && ra.pad && ra.a.lg >= 1;   // (16-byte loads need the padded pairs)
+  // 2 pairs per lane and 16-byte loads on the padded pairs (1M numeric 52.8 ->
+  // 50.6 ms vs one 8-byte pair per lane, PERF_LOG round 4)
+  const bool wide = ra.a.Bcv && ra.pad && ra.a.lg >= 1;
   const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
                      : (wide ? launch_rows(K::kcvw, ra, s, K::NT)
                              : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT)));
