@@ -124,8 +124,7 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
        started asynchronously (they run in issue order): the row plan overlaps
        the columns, the window splits and count kernel (columns only) overlap
        the values; each lands in a padded [world, emax] buffer and one native
-       pass unpacks it (the values together with the interleaved (column,
-       value) pairs of the bitmap kernel).  Host panels (gloo on CPUs): one
+       pass unpacks it.  Host panels (gloo on CPUs): one
        packed [cols | values] collective and host-side concatenation.
 
     The collectives are ``comm`` methods, so the device branch is the one
@@ -200,12 +199,13 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
                 if g.numel() != W * emax:
                     raise RuntimeError(f"operand gather: {g.numel()} value words, expected {W * emax}")
                 val = torch.empty(nnz, dtype=torch.float32, device=dev)
-                cv = torch.empty((nnz, 2), dtype=torch.int32, device=dev)
                 if rec is not None:
                     rec[2] = GATHER_STATS.mark(dev)   # the compute stream may read the payload from here
-                unpack(None, g, col, val, cv)
+                # (no interleaved copy here: the bitmap kernels read B through its
+                # padded pair layout, built from col / val by the SpGEMM itself;
+                # ops.spgemm.interleaved makes the plain pairs on demand)
+                unpack(None, g, col, val, None)
                 B = CSR(m, panel.n, rowptr, col, val)
-                B._bcv = cv
                 got["B"] = B
                 got["gv"] = g
             return got["B"]

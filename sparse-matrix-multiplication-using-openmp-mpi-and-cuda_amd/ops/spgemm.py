@@ -665,8 +665,8 @@ BM_FILL = 0.7              # mean products per window <= BM_FILL * fast capacity
 
 def interleaved(B: CSR) -> torch.Tensor:
     """B as [nnz, 2] int32 (column, value bits) pairs: the operand of the
-    row-major bitmap numeric kernel.  A distributed gather produces it while
-    unpacking (``B._bcv``); otherwise one native 16-byte-vector copy."""
+    row-major bitmap numeric kernel when B's padded pair layout is not built
+    (one native 16-byte-vector copy; ``B._bcv`` if a caller attached one)."""
     cv = getattr(B, "_bcv", None)
     if cv is not None and cv.shape[0] == B.nnz:
         return cv

@@ -75,7 +75,7 @@ def _all_decompositions(world: int, device: str):
         lo, hi, klo, khi = rc[r], rc[r + 1], kc[r], kc[r + 1]
         Bp = B.row_slice(klo, khi).to(dev)
         out = {}
-        # operand gather stages (columns first, then values + interleaved pairs)
+        # operand gather stages (columns first, then values)
         meta, ready = MS.allgather_operand_async(Bp, comm)
         out["meta_rowptr"] = meta.rowptr.cpu()
         out["nnz_total"] = getattr(meta, "_nnz_total", meta.nnz)
