@@ -272,3 +272,47 @@ def test_bench_world_mismatch_fails():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "world size 3 != --gpus 2" in r.stderr
+
+
+
+def test_local_operand_is_marked_resident():
+    """N = 1: the right operand never leaves the rank, so ``OperandReady.local``
+    is set (the bitmap path then builds both padded layouts of B in one pass,
+    ops/spgemm.py _bitmap_launch); a gathered operand keeps the two-stage order."""
+    from spmm_amd.parallel import comm as CM
+
+    B = gen_csr.uniform_csr(64, 64, 0.1, seed=3)
+    _, ready = MS.allgather_operand_async(B, CM.Comm(0, 1, 0, torch.device("cpu"), None))
+    assert ready.local and ready() is B and ready.cols() is B
+    assert not MS.OperandReady(lambda: B).local
+
+
+@pytest.mark.gpu
+def test_local_flag_survives_the_spgemm_wrapper(monkeypatch):
+    """``spgemm``'s resolve-once wrapper around ``B_ready`` forwards ``local``
+    and ``cols`` to the bitmap path (a dropped flag silently costs a second
+    padding pass per step)."""
+    from spmm_amd.parallel import comm as CM
+    from spmm_amd.utils.config import CONFIG
+
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap", "on")
+    dev = torch.device("cuda", 0)
+    A = gen_csr.uniform_csr(4096, 4096, 0.01, seed=4).to(dev)
+    B = gen_csr.uniform_csr(4096, 4096, 0.01, seed=3).to(dev)
+    _, ready = MS.allgather_operand_async(B, CM.Comm(0, 1, 0, dev, None))
+    seen = {}
+    orig = SG.onepass_bitmap
+
+    def spy(A_, B_, info, B_ready, pre):
+        seen["local"] = getattr(B_ready, "local", None)
+        seen["cols"] = B_ready.cols() is B
+        return orig(A_, B_, info, B_ready, pre)
+
+    SG.onepass_bitmap = spy
+    try:
+        C = SG.spgemm(A, B, SG.SpgemmInfo(), B_ready=ready)
+    finally:
+        SG.onepass_bitmap = orig
+    assert seen == {"local": True, "cols": True}
+    Cd = C.to_dense().double().cpu()
+    assert torch.allclose(Cd, A.to_dense().double().cpu() @ B.to_dense().double().cpu(), atol=1e-4)
