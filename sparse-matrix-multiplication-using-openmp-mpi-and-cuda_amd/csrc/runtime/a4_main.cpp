@@ -36,6 +36,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -991,6 +992,10 @@ int main(int argc, char** argv) {
     const std::string msg = "a4 rank " + std::to_string(rank) + ": " + e.what() + "\n";
     std::fwrite(msg.data(), 1, msg.size(), stderr);
     std::fflush(stderr);
+    // the launcher forwards a rank's stderr through its proxy; an abort right
+    // after the write can tear the proxy down before the line is forwarded
+    // (seen ~1 in 10 runs of the fault-injection test), so give it a moment
+    std::this_thread::sleep_for(std::chrono::milliseconds(200));
     MPI_Abort(MPI_COMM_WORLD, 1);   // fail fast: peers blocked in a transfer are torn down
     return 1;
   }
