@@ -27,11 +27,16 @@
 // Output rows are column-sorted by construction (rank order = column order).
 // Per product: count 4 B of B + 1 LDS op; numeric 8 B of B + 5 LDS ops + 8 B
 // of C; per unit O(W / 64) LDS words of scan.  Window bounds inside every B
-// row come from one binary-search kernel (bm_window_splits), uint32 indices.
+// row come from one binary-search kernel (bm_window_splits), uint32 indices;
+// it and B's other layout kernels (packed bounds, padded arrays, the
+// gathered-operand unpack) are in csr_bitmap_layout.hip.
+#include "bitmap_common.hpp"
 #include "common.hpp"
 
 #include <cstdlib>
 #include <type_traits>
+
+using namespace spmm_bitmap;
 
 #ifndef SPMM_BM_ROWS_R   // register rounds of the row-major numeric kernel (chunk capacity 16 * R per unit)
 #define SPMM_BM_ROWS_R 10
@@ -48,18 +53,6 @@
 #define BM_OUT(ptr, val) __builtin_nontemporal_store((val), (ptr))
 
 namespace {
-
-// 64-lane inclusive prefix sum on the DPP network (VALU only; no LDS
-// traffic): row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31.
-__device__ __forceinline__ int bm_wave_incl(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
-  return x;
-}
 
 // Block-wide exclusive scan of a non-negative int (+ total); DPP inside the
 // wave, one LDS word per wave.  Ends synchronised; the caller must put a
@@ -257,8 +250,6 @@ struct BmArgs {
                            // bit 2: deferred list full (host falls back)
   const uint4* ws8 = nullptr;   // per-unit WIDE numeric: packed window bounds + padded pair bases
 };
-constexpr int kPadLg = 4;    // padded segments: multiples of 2^4 pairs (128 bytes)
-constexpr int kPadCLg = 5;   // padded count segments (column groups of a count unit): 2^5 columns (128 bytes)
 
 // CV: B read as interleaved (column, value bits) pairs (p.Bcv): one 8-byte load
 // per product instead of two 4-byte ones (numeric modes only)
@@ -1549,165 +1540,6 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   }
 }
 
-// ws8[j] from ws (nwin <= 8): first index + 16-bit window lengths; err bit 3
-// if a window segment of some B row is 65536 entries or longer.  plen (if
-// given): the row's length in the padded pair array (segments rounded up to
-// 2^kPadLg pairs).
-__global__ __launch_bounds__(256) void bm_pack_ws8(const uint32_t* __restrict__ ws, int64_t mb, int nwin,
-                                                   uint4* __restrict__ ws8, int32_t* __restrict__ err,
-                                                   int64_t* __restrict__ plen, int64_t* __restrict__ plen_c, int gc) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= mb) return;
-  const uint32_t* wr = ws + j * (nwin + 1);
-  uint32_t l[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  bool bad = false;
-  int64_t pl = 0, pc = 0;
-  for (int q = 0; q < nwin; ++q) {
-    const uint32_t d = wr[q + 1] - wr[q];
-    bad |= d > 0xffffu;
-    l[q] = d & 0xffffu;
-    pl += (((int64_t)d + (1 << kPadLg) - 1) >> kPadLg) << kPadLg;
-  }
-  for (int q = 0; q < nwin; q += gc) {   // count groups of gc windows
-    const int64_t d = (int64_t)wr[q + gc < nwin ? q + gc : nwin] - wr[q];
-    pc += ((d + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg;
-  }
-  if (bad) atomicOr(err, 8);
-  ws8[2 * j] = make_uint4(wr[0], l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16));
-  ws8[2 * j + 1] = make_uint4(l[6] | (l[7] << 16), 0u, 0u, 0u);
-  if (plen) plen[j] = pl;
-  if (plen_c) plen_c[j] = pc;
-}
-
-// Padded pair array: one wave per B row copies its (column, value) pairs to
-// row base pbase[j] + the padded start of each window (padding slots are left
-// as they are: the kernels never read a padded slot as a product), and stores
-// the base in ws8[2j + 1].y.
-__global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__ ws, const int32_t* __restrict__ col,
-                                                    const uint32_t* __restrict__ val, int64_t mb, int nwin,
-                                                    const int64_t* __restrict__ pbase, uint4* __restrict__ ws8,
-                                                    uint2* __restrict__ out, const int64_t* __restrict__ cbase,
-                                                    int gc, int32_t* __restrict__ outc, int64_t cap, int64_t cap_c,
-                                                    int32_t* __restrict__ err) {
-  const int lane = threadIdx.x & 63;
-  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  if (j >= mb) return;
-  const uint32_t* wr = ws + j * (nwin + 1);
-  const uint32_t w = lane <= nwin ? wr[lane] : 0u;   // lane q: first index of window q (q = nwin: row end)
-  const int64_t base = out ? pbase[j] : 0, cb = outc ? cbase[j] : 0;
-  if (lane == 0) {
-    uint32_t* x = reinterpret_cast<uint32_t*>(&ws8[2 * j + 1]);
-    if (out) x[1] = (uint32_t)base;
-    if (outc) x[2] = (uint32_t)cb;
-  }
-  // padded start of window q (lane q): exclusive scan of the rounded lengths
-  const uint32_t wn = __shfl_down(w, 1);
-  const uint32_t rl = lane < nwin ? ((wn - w + (1u << kPadLg) - 1) >> kPadLg) << kPadLg : 0u;
-  const uint32_t ps = (uint32_t)bm_wave_incl((int)rl) - rl;
-  // padded start of count group g (lane g): windows [g gc, (g + 1) gc)
-  const int ng = (nwin + gc - 1) / gc;
-  const uint32_t g0 = (uint32_t)__shfl(w, lane * gc < nwin ? lane * gc : nwin);
-  const uint32_t g1 = (uint32_t)__shfl(w, (lane + 1) * gc < nwin ? (lane + 1) * gc : nwin);
-  const uint32_t rc = lane < ng ? ((g1 - g0 + (1u << kPadCLg) - 1) >> kPadCLg) << kPadCLg : 0u;
-  const uint32_t pc = (uint32_t)bm_wave_incl((int)rc) - rc;
-  // entry loop with a wave-uniform trip count (every lane stays in it), so
-  // each entry fetches its window's bounds from the lanes holding them (lane
-  // shuffles) instead of selecting among eight uniform registers (1M: 0.937
-  // -> 0.871 ms per call, PERF_LOG round 4)
-  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
-  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)w, nwin);
-  for (uint32_t e0 = r0; e0 < r1; e0 += 64) {
-    const uint32_t e = e0 + lane;
-    const bool ok = e < r1;
-    int q = 0;
-#pragma unroll
-    for (int k = 1; k < 8; ++k) q += (k < nwin && e >= (uint32_t)__builtin_amdgcn_readlane((int)w, k)) ? 1 : 0;
-    const uint32_t c = ok ? (uint32_t)col[e] : 0u;
-    if (out) {
-      const uint32_t sw = (uint32_t)__shfl((int)w, q), sp = (uint32_t)__shfl((int)ps, q);
-      const int64_t d = base + sp + (e - sw);
-      if (ok) {
-        if (d < cap) out[d] = make_uint2(c, val[e]);
-        else atomicOr(err, 32);   // (a layout bug, never a write out of bounds)
-      }
-    }
-    if (outc) {
-      const int g = q / gc;
-      const uint32_t gw = (uint32_t)__shfl((int)w, g * gc), gp = (uint32_t)__shfl((int)pc, g);
-      const int64_t d = cb + gp + (e - gw);
-      if (ok) {
-        if (d < cap_c) outc[d] = (int32_t)c;
-        else atomicOr(err, 32);
-      }
-    }
-  }
-}
-
-// ws[j * (nwin + 1) + q] = first index of B row j whose column >= q * 2^lgw
-// (q = 0: row start, q = nwin: row end).  One thread per (row, q).
-__global__ __launch_bounds__(256) void bm_window_splits(const int64_t* __restrict__ Brp,
-                                                        const int32_t* __restrict__ Bci, int64_t mb, int lgw,
-                                                        int nwin, uint32_t* __restrict__ ws) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nw1 = nwin + 1;
-  if (t >= mb * nw1) return;
-  const int64_t j = t / nw1;
-  const int q = (int)(t - j * nw1);
-  int64_t lo = Brp[j], hi = Brp[j + 1];
-  if (q == 0) {
-    hi = lo;
-  } else if (q == nwin) {
-    lo = hi;
-  } else {
-    const int64_t bound = (int64_t)q << lgw;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)Bci[mid] < bound) lo = mid + 1; else hi = mid;
-    }
-  }
-  ws[t] = (uint32_t)lo;
-}
-
-// ---- operand layout kernels ------------------------------------------------
-// B as interleaved (column, value bits) pairs for the row-major numeric
-// kernel: 4 entries per thread, 16-byte loads and stores.
-__global__ __launch_bounds__(256) void bm_interleave(const int32_t* __restrict__ col, const uint32_t* __restrict__ val,
-                                                    int64_t n, uint2* __restrict__ cv) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i + 3 < n && ((reinterpret_cast<uintptr_t>(col + i) | reinterpret_cast<uintptr_t>(val + i)) & 15) == 0) {
-    const int4 c = *reinterpret_cast<const int4*>(col + i);
-    const uint4 v = *reinterpret_cast<const uint4*>(val + i);
-    reinterpret_cast<uint4*>(cv + i)[0] = make_uint4((uint32_t)c.x, v.x, (uint32_t)c.y, v.y);
-    reinterpret_cast<uint4*>(cv + i)[1] = make_uint4((uint32_t)c.z, v.z, (uint32_t)c.w, v.w);
-    return;
-  }
-  for (int64_t k = i; k < i + 4 && k < n; ++k) cv[k] = make_uint2((uint32_t)col[k], val[k]);
-}
-
-// The all-gathered right operand of a row-block SpGEMM -> contiguous arrays
-// in one pass (replaces concatenations and an interleave copy).  Rank r's
-// columns are gc[r * gstride + i] and its value bits gv[r * gstride + i],
-// i < base[r + 1] - base[r] (base[r] = first output index of rank r).  Any of
-// col / val / cv may be null; with gc null the columns are read back from
-// col (already unpacked: the two-stage gather, columns first).
-__global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __restrict__ gc, const uint32_t* __restrict__ gv,
-                                                         int64_t gstride, const int64_t* __restrict__ base,
-                                                         int32_t* __restrict__ col, uint32_t* __restrict__ val,
-                                                         uint2* __restrict__ cv) {
-  const int r = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t b0 = base[r], n = base[r + 1] - b0;
-  if (i >= n) return;
-  const int64_t src = (int64_t)r * gstride + i;
-  const uint32_t c = gc ? gc[src] : (uint32_t)col[b0 + i];
-  if (gc && col) col[b0 + i] = (int32_t)c;
-  if (gv) {
-    const uint32_t v = gv[src];
-    if (val) val[b0 + i] = v;
-    if (cv) cv[b0 + i] = make_uint2(c, v);
-  }
-}
-
 // ---- configurations -------------------------------------------------------
 // Every fast kernel: 256 threads and <= 40 KB of LDS, so four workgroups
 // (16 waves, 128 VGPRs each) share a CU; count and reload kernels take most
@@ -1879,17 +1711,6 @@ SPMM_EXPORT int spmm_spgemm_bm_config(int cfg, int* lgw, int* nsub_count, int* p
   return 0;
 }
 
-SPMM_EXPORT int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin,
-                                      uint32_t* ws, void* stream) {
-  if (mb <= 0) return 0;
-  const int64_t n = mb * (nwin + 1);
-  if (nwin < 1 || lgw < 6 || lgw > 30 || n > (int64_t)UINT32_MAX - 255) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_window_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Brp, Bci,
-                     mb, lgw, nwin, ws);
-  SPMM_LAUNCH_CHECK();
-  return 0;
-}
-
 // Count kernel: ucnt[m * nwin] = exact nnz of every (row, window) unit.
 SPMM_EXPORT int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const uint32_t* ws,
                                      const int32_t* Bci, int64_t m, int nwin, int lg, int32_t* ucnt, int32_t* err,
@@ -1946,39 +1767,6 @@ SPMM_EXPORT int spmm_spgemm_bm_stamps(int on, unsigned long long* out8) {
   return (int)e;
 }
 
-// ws8 for the row-major numeric kernel (nwin <= 8); err bit 3: a window
-// segment too long for 16 bits (use spmm_spgemm_bm_numeric instead).
-SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin, void* ws8, int32_t* err,
-                                        int64_t* plen, int64_t* plen_c, int gc, void* stream) {
-  if (mb <= 0) return 0;
-  if (nwin < 1 || nwin > 8 || gc < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_pack_ws8, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, mb, nwin,
-                     (uint4*)ws8, err, plen, plen_c, gc);
-  SPMM_LAUNCH_CHECK();
-  return 0;
-}
-
-// Padded arrays of B (either may be null): the (column, value) pair array of
-// the row-major numeric kernel (pass pad = 1 to it; pbase = exclusive scan of
-// the plen from spmm_spgemm_bm_pack_ws8) and the column array of the row
-// count kernel with count groups of gc windows padded to 32 columns (pad = 1
-// to it; cbase = exclusive scan of plen_c); totals < 2^32.  Also stores each
-// row's bases in ws8.
-// cap / cap_c: entries allocated for out / outc; err bit 5 if a row would
-// not fit (a layout invariant; nothing is written out of bounds).
-SPMM_EXPORT int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb,
-                                         int nwin, const int64_t* pbase, void* ws8, void* out, const int64_t* cbase,
-                                         int gc, int32_t* outc, int64_t cap, int64_t cap_c, int32_t* err,
-                                         void* stream) {
-  if (mb <= 0) return 0;
-  if (nwin < 1 || nwin > 8 || gc < 1 || gc > 8 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX)
-    return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_pad_pairs, dim3((unsigned)((mb * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, col,
-                     (const uint32_t*)val, mb, nwin, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc, cap, cap_c, err);
-  SPMM_LAUNCH_CHECK();
-  return 0;
-}
-
 // Row-major numeric (nwin <= 8, ws8 from spmm_spgemm_bm_pack_ws8), then the
 // reload kernel over the deferred units; same contract as spmm_spgemm_bm_numeric.
 // Bcv: optional [nnz(B)] (column, value bits) pairs read by the row-major kernel.
@@ -2021,30 +1809,4 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
     case 1: return bm_count_rows<1>(ra, nsub, s);
     default: return bm_count_rows<2>(ra, nsub, s);
   }
-}
-
-// Interleaved (column, value bits) copy of B for the row-major numeric kernel.
-SPMM_EXPORT int spmm_spgemm_bm_interleave(const int32_t* col, const float* val, int64_t n, void* cv, void* stream) {
-  if (n <= 0) return 0;
-  const int64_t th = (n + 3) / 4;
-  hipLaunchKernelGGL(bm_interleave, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, (hipStream_t)stream, col,
-                     (const uint32_t*)val, n, (uint2*)cv);
-  SPMM_LAUNCH_CHECK();
-  return 0;
-}
-
-// Unpack an all-gathered operand payload: rank r's columns at gc + r *
-// gstride, its value bits at gv + r * gstride (either may be null, see the
-// kernel); base: device int64[world + 1] output offsets.
-SPMM_EXPORT int spmm_spgemm_bm_unpack_gathered(const void* gc, const void* gv, int world, int64_t gstride,
-                                               const int64_t* base, int64_t max_n, int32_t* col, float* val, void* cv,
-                                               void* stream) {
-  if (world <= 0 || max_n <= 0) return 0;
-  if (world > 65535 || (max_n + 255) / 256 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
-  if (!gc && !col) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_unpack_gathered, dim3((unsigned)((max_n + 255) / 256), (unsigned)world), dim3(256), 0,
-                     (hipStream_t)stream, (const uint32_t*)gc, (const uint32_t*)gv, gstride, base, col,
-                     (uint32_t*)val, (uint2*)cv);
-  SPMM_LAUNCH_CHECK();
-  return 0;
 }
