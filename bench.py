@@ -70,6 +70,7 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
         C = MS.rowblock_spgemm(prob.A, prob.B, comm, info)   # first (untimed) run also counts FLOPs
         nnz_local = info.nnz
         step = lambda: MS.rowblock_spgemm(prob.A, prob.B, comm)  # noqa: E731
+    eager_step = step
     flops_local = info.flops
     del C
     graph = None
@@ -89,15 +90,44 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
             graph = None
             torch.cuda.empty_cache()
 
-        def verify():   # after the timed loop: the last replay's C is the eager product's
+        def verify():
+            """After the timed loop: (1) the last replay's C equals an eager
+            product's (row pointer and column sum exactly, value sum to fp32
+            accumulation-order tolerance); (2) the eager step -- row-plan
+            inspector, three host read-backs, exact C allocation: everything
+            the graph does once at capture -- timed on its own and reported
+            next to the replayed step as ``eager_ms_per_step``."""
             if graph is None:
                 return {}
             gi = SpgemmInfo()
             Cg = graph.result(gi)
             if Cg is None or gi.nnz != nnz_local:
                 raise SystemExit(f"[bench] graph replay disagrees with the eager product: nnz {gi.nnz} vs {nnz_local}")
+            dig = lambda C: (C.col.long().sum().item(), C.val.double().sum().item())  # noqa: E731
+            g_col, g_val = dig(Cg)
+            rp_g = Cg.rowptr.clone()
+            del Cg
+            ne = max(1, min(args.steps, 5))
+            Ce = eager_step()   # (warm: allocator)
+            del Ce
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(ne):
+                Ce = None
+                Ce = eager_step()
+            torch.cuda.synchronize()
+            eager_ms = (time.perf_counter() - t) / ne * 1e3
+            e_col, e_val = dig(Ce)
+            same_rp = bool(torch.equal(rp_g, Ce.rowptr))
+            del Ce, rp_g
+            ok = same_rp and g_col == e_col and abs(g_val - e_val) <= 1e-5 * max(1.0, abs(e_val))
+            if not ok:
+                raise SystemExit(f"[bench] graph replay C differs from the eager C: rowptr equal {same_rp}, "
+                                 f"col sums {g_col} / {e_col}, value sums {g_val} / {e_val}")
             return dict(graph_replay_nnz=gi.nnz, bitmap_cfg=gi.rows_per_bin_num.get("bitmap_cfg"),
-                        bitmap_deferred=gi.rows_per_bin_num.get("bitmap_deferred"))
+                        bitmap_deferred=gi.rows_per_bin_num.get("bitmap_deferred"),
+                        eager_ms_per_step=round(eager_ms, 3),
+                        graph_vs_eager_check=dict(rowptr_equal=same_rp, col_sum=e_col, val_sum=e_val))
         if graph is not None:
             step.verify = verify
     total_flops = int(_allreduce_sum(comm, flops_local))

@@ -52,13 +52,6 @@ __device__ __forceinline__ uint64_t ref_mac(uint64_t acc, uint64_t a, uint64_t b
 // s = acc + t == 2^64-1 needs s_lo == 0xffffffff.  When no lane of a tile
 // ever raises the flag the wrapped result IS the reference's (no collapse
 // fired); otherwise the caller recomputes the tile with ref_mac.
-// v_mad_u64_u32: x*y + z (64-bit addend, 64-bit result; the carry-out is dropped)
-__device__ __forceinline__ uint64_t mad_u64_u32(uint32_t x, uint32_t y, uint64_t z) {
-  uint64_t r, carry;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(x), "v"(y), "v"(z));
-  return r;
-}
-
 // Returns s = acc + a*b (wrapping); ``m`` accumulates max(s_lo, t_lo) so the
 // caller tests a whole group of MACs with one compare (max == 0xffffffff iff
 // some s_lo or t_lo was all-ones).
@@ -67,8 +60,10 @@ __device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t 
   // four VALU ops: r = alo*blo + acc;  c = alo*bhi;  x = ahi*blo + c (its low
   // word = the cross terms mod 2^32);  s_hi = r_hi + x_lo (32-bit add into the
   // high half; opaque so the compiler does not rebuild it as a 64-bit add)
+  // (64-bit v_mad_u64_u32 destinations are early-clobber: a destination pair
+  // overlapping a source is unsafe, so the register allocator must not reuse one)
   uint64_t r, k0;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(k0) : "v"(alo), "v"(blo), "v"(acc));
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=&s"(k0) : "v"(alo), "v"(blo), "v"(acc));
   uint32_t hi;
 #if SPMM_CHAIN_CROSS_MUL
   // cross terms as two v_mul_lo_u32 + one v_add3_u32
@@ -78,8 +73,8 @@ __device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t 
   asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(r >> 32)), "v"(c1), "v"(c2));
 #else
   uint64_t c, x, k1, k2;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(c), "=s"(k1) : "v"(alo), "v"(bhi));
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(x), "=s"(k2) : "v"(ahi), "v"(blo), "v"(c));
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=&v"(c), "=&s"(k1) : "v"(alo), "v"(bhi));
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(x), "=&s"(k2) : "v"(ahi), "v"(blo), "v"(c));
   asm("v_add_u32 %0, %1, %2" : "=v"(hi) : "v"((uint32_t)(r >> 32)), "v"((uint32_t)x));
 #endif
   const uint32_t lo = (uint32_t)r;

@@ -1305,6 +1305,415 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
   BM_STAMP_FLUSH();
 }
 
+// ---- pipelined row-major numeric kernel (padded pairs, unordered sum) -------
+// The same unit work as spgemm_bm_rows<..., WIDE> in a software pipeline that
+// hides the B gathers: unit k+1 is staged (scan, descriptors) and its B loads
+// are issued right after unit k's pass 2, BEFORE unit k's write-out, so the
+// gathers travel while unit k's slots are copied to C.  Unit k+1's pass 1
+// then finds its products landed (the flat kernel waited a full memory
+// latency at every pass 1: ~35 % of a unit's cycles, shader-clock stamps,
+// PERF_LOG round 5).  Memory is addressed through buffer descriptors with
+// 32-bit offsets: B gathers as buffer_load_dwordx4 (no 64-bit address
+// arithmetic per load), and the write-out as a FIXED count of 16-byte
+// buffer_store_dwordx4 per lane whose range check (num_records = the unit's
+// entries) drops the lanes past the unit -- a fixed store count lets the
+// compiler wait for the next unit's loads with vmcnt(#stores) and leave the
+// write-out stores in flight.  Four barriers per unit instead of six.
+typedef uint32_t bm_v4u __attribute__((ext_vector_type(4)));
+
+struct BmPipeArgs {
+  BmRowArgs r;
+  uint32_t bcv_bytes;   // bytes of the padded pair array (< 2^32: checked by the host)
+  int64_t annz;         // nnz(A) > 0
+};
+
+
+template <int LGW, int NT, int PCAP, int R, int CCAP>
+__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
+  const BmRowArgs& ra = pa.r;
+  const BmArgs& p = ra.a;
+  constexpr int NW = NT / 64;
+  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  constexpr int RR = R;          // product slots per lane
+  constexpr int RL = RR / 2;     // load rounds (two pairs per lane and load)
+  constexpr int NWR = (PCAP + 4 * NT - 1) / (4 * NT);   // write-out rounds: four entries per lane and round
+  static_assert(RR % 2 == 0 && WPW % 64 == 0 && PCAP < 65536, "geometry");
+  constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+  constexpr bool PAIRS = SG > 1;
+
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
+  __shared__ __attribute__((aligned(16))) unsigned long long items[NWR * 4 * NT];
+  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];   // chunk: {first B pair, valid pairs}
+  __shared__ float dval[CCAP];                                 //        a(i, j)
+  __shared__ int wsum[NW];        // rank sweep: word totals per wave
+  __shared__ int wscan[2 * NW];   // staging scan
+  __shared__ __attribute__((aligned(8))) int64_t suo[9];   // unit offsets of the staged row (uoff[row * nwin + q])
+  __shared__ int sdup;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lgc = p.lg;          // log2 pairs per chunk
+  const int lg = lgc - 1;        // log2 lanes per chunk
+  const int Gc = 1 << lgc;
+  const int Gl = 1 << lg;
+  const int ngrp = NW << (6 - lg);
+  const int gid = (w << (6 - lg)) + (lane >> lg);
+  const int gl = lane & (Gl - 1);
+  const int nwin = p.nwin;
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
+  const auto rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(p.Bcv), 0, (int)pa.bcv_bytes, 0x00020000);
+
+  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+  if (tid == 0) sdup = 0;
+
+  // 32-bit row indices: the host takes this path only for m * nwin < 2^31
+  const int NG = (int)gridDim.x;
+  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+  const int m = (int)p.m;
+  const int annz = (int)pa.annz;   // > 0 (checked by the host)
+
+  // ---- row pipeline --------------------------------------------------------
+  // The per-row inputs (A entries, packed window bounds, unit offsets) are
+  // loaded ONCE per row, unconditionally at the top of the row loop, each
+  // from values that landed during the previous row: row r + NG's bounds
+  // (from its A columns), row r + 2 NG's A entries (from its row pointers),
+  // row r + 3 NG's row pointers.  No load sits under a branch inside the
+  // loops and none is consumed in the row that issues it, so hipcc never
+  // merges or copies a register whose load is still in flight (a merge it
+  // materialises as copies that wait for the load: a full memory latency
+  // per row).  Indices are clamped into range (values past the matrix or the
+  // row are never used).
+  auto arp2 = [&](int r, int& a, int& b) {   // row pointers of row r (clamped)
+    const int rr = r < m ? r : m - 1;
+    a = (int)p.Arp[rr];
+    b = (int)p.Arp[rr + 1];
+  };
+  auto entry = [&](int a, int b) {   // this thread's A entry of the row [a, b) (clamped)
+    const int a0 = __builtin_amdgcn_readfirstlane(a), na = __builtin_amdgcn_readfirstlane(b) - a0;
+    const int e = a0 + (tid < na ? tid : 0);
+    return e < annz ? e : annz - 1;
+  };
+  auto uoff_of = [&](int r) {   // lane q <= nwin: uoff[r * nwin + q] (clamped)
+    const int rr = r < m ? r : m - 1;
+    return p.uoff[(int64_t)rr * nwin + (lane <= nwin ? lane : nwin)];
+  };
+  int a1 = 0, b1 = 0, a2 = 0, b2 = 0, a3 = 0, b3 = 0;
+  arp2(me, a1, b1);
+  arp2(me + NG, a2, b2);
+  int e2 = entry(a1, b1);
+  uint32_t jj1 = (uint32_t)p.Aci[e2];   // row me: A column / value of this thread's entry
+  float av1 = p.Av[e2];
+  uint4 wa1 = ra.ws8[2 * (int64_t)jj1];   // ... its packed bounds and the row's unit offsets
+  uint2 wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj1 + 1);
+  int64_t uo1 = uoff_of(me);
+  int na1 = b1 - a1;
+  e2 = entry(a2, b2);
+  uint32_t jj2 = (uint32_t)p.Aci[e2];   // row me + NG
+  float av2 = p.Av[e2];
+  int na2 = b2 - a2;
+  arp2(me + 2 * NG, a3, b3);            // row me + 2 NG
+  na1 = __builtin_amdgcn_readfirstlane(na1);
+
+  // staging registers of the row being staged
+  int cna = 0;
+  float cav = 0.f;
+  uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0;   // 16-bit window lengths, two per word; cl0 = the word
+                                                  // of the window being staged (shifted down every two
+                                                  // windows: no run-time indexing, which hipcc would
+                                                  // put in scratch)
+  uint32_t bq = 0;   // this thread's entry: first pair of the next window to stage
+  auto take_row = [&]() {   // the next row's inputs -> staging registers (their loads have landed)
+    cna = na1;
+    cav = av1;
+    bq = wb1.y;   // first pair of the entry's B row in the padded pair array
+    cl0 = wa1.y;
+    cl1 = wa1.z;
+    cl2 = wa1.w;
+    cl3 = wb1.x;
+    if (lane <= nwin) suo[lane] = uo1;   // read after the stage's scan barrier
+  };
+
+  // ---- the staged unit ------------------------------------------------------
+  int srow = me, sq = 0;
+  int sTC = 0, snr = 0, sclo = 0, swant = 0;
+  int64_t soff = 0;
+  bool sskip = false;
+  bm_v4u xb[RL];
+  uint32_t okm = 0;     // bit s: product slot s (round s / 2, pair s % 2) is in its segment
+  bool dirty = false;   // the bitmap holds a formed unit's columns
+
+  // Stage unit (srow, sq): scan, descriptors, offsets.  An empty or
+  // oversized unit is staged like any other with sskip set (no loop in
+  // here); the main loop runs no passes for it.  The scan's barrier also ends
+  // the previous unit's pass 2 (every rank lookup and slot write done).
+  auto stage = [&]() {
+    const int q = sq;
+    int len = 0, nch = 0;
+    if (tid < cna) {
+      len = (int)((cl0 >> (16 * (q & 1))) & 0xffffu);
+      nch = (len + Gc - 1) >> lgc;
+    }
+    if (q & 1) {   // uniform
+      cl0 = cl1;
+      cl1 = cl2;
+      cl2 = cl3;
+    }
+    const uint32_t b0 = bq;
+    bq += (uint32_t)(((len + (1 << kPadLg) - 1) >> kPadLg) << kPadLg);
+    int pre, plen, TCv, Pv;
+    bm_scan2<NT>(nch, len, wscan, pre, plen, TCv, Pv);
+    const int TC = __builtin_amdgcn_readfirstlane(TCv), P = __builtin_amdgcn_readfirstlane(Pv);
+    const int u = srow * nwin + q;
+    const bool too_big = cna > NT || P > PCAP || TC > CCAP || TC > RL * ngrp;
+    sskip = P == 0 || too_big;
+    if (too_big && P != 0 && tid == 0) {   // the reload kernel forms it
+      const uint32_t at = atomicAdd(p.novf, 1u);
+      if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
+      else atomicOr(p.err, 4);
+    }
+    if (dirty) {   // the previous unit's rank lookups are done (scan barrier)
+      for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+      dirty = false;
+    }
+    if (!sskip)
+      for (int kk = 0; kk < nch; ++kk) {
+        const int rem = len - (kk << lgc);
+        desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lgc), (uint32_t)(rem < Gc ? rem : Gc));
+        dval[pre + kk] = cav;
+      }
+    {   // this unit's offset in C and its count (the count kernel's)
+      const int64_t o0 = suo[q], o1 = suo[q + 1];
+      soff = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)o0 >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o0));
+      swant = __builtin_amdgcn_readfirstlane((int)(o1 - o0));
+    }
+    sTC = TC;
+    snr = sskip ? 0 : (TC + ngrp - 1) / ngrp;
+    sclo = q << LGW;
+    __syncthreads();   // descriptors written, bitmap clear, wscan / suo read
+  };
+  // descriptor reads and B gathers of the staged unit (rounds past its chunks load nothing)
+  auto issue_loads = [&]() {
+    const int TC = sTC;
+    uint2 ds[RL];
+#pragma unroll
+    for (int d = 0; d < RL; ++d) {
+      const int t = gid + d * ngrp;
+      ds[d] = desc[t < TC ? t : TC - 1];
+    }
+    okm = 0;
+    uint32_t f[RL];
+#pragma unroll
+    for (int d = 0; d < RL; ++d) {
+      const int t = gid + d * ngrp;
+      const int nv = (int)ds[d].y - 2 * gl;
+      const bool ok = (t < TC) & (nv > 0);
+      okm |= (ok ? 1u : 0u) << (2 * d);
+      okm |= ((ok & (nv > 1)) ? 1u : 0u) << (2 * d + 1);
+      f[d] = ds[d].x + (ok ? (uint32_t)(2 * gl) : 0u);
+    }
+#pragma unroll
+    for (int d = 0; d < RL; ++d) {
+      xb[d] = bm_v4u{0u, 0u, 0u, 0u};
+      if (d < snr) xb[d] = __builtin_amdgcn_raw_buffer_load_b128(rsb, (int)(f[d] * 8u), 0, 0);   // wave-uniform guard
+    }
+  };
+  // a unit's slots to C: NWR rounds of four entries per lane, 16-byte stores
+  // through descriptors of lim entries (lanes past the unit dropped)
+  auto write_out = [&](int64_t off, int lim) {
+    const int nb = __builtin_amdgcn_readfirstlane(lim * 4);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(p.Cci + off, 0, nb, 0x00020000);
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc(p.Cv + off, 0, nb, 0x00020000);
+#pragma unroll
+    for (int rd = 0; rd < NWR; ++rd) {
+      const int e = (rd * NT + tid) * 4;
+      const ulonglong2 i01 = *reinterpret_cast<const ulonglong2*>(&items[e]);
+      const ulonglong2 i23 = *reinterpret_cast<const ulonglong2*>(&items[e + 2]);
+      const bm_v4u cc{(uint32_t)i01.x, (uint32_t)i01.y, (uint32_t)i23.x, (uint32_t)i23.y};
+      const bm_v4u vv{(uint32_t)(i01.x >> 32), (uint32_t)(i01.y >> 32), (uint32_t)(i23.x >> 32),
+                      (uint32_t)(i23.y >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b128(cc, rc, e * 4, 0, 2);   // aux 2: nt
+      __builtin_amdgcn_raw_buffer_store_b128(vv, rv, e * 4, 0, 2);
+    }
+  };
+
+  take_row();
+  stage();
+  issue_loads();
+  // the loop is entered with the same stores behind the first unit's B
+  // loads as every later unit has (all dropped: zero records), so the
+  // compiler's wait at pass 1 is vmcnt(#stores) on every path, not vmcnt(0)
+  write_out(0, 0);
+  int c[RR];
+  float v[RR];
+  for (int row = me; row < m; row += NG) {
+    // ---- once per row: row + NG's bounds and offsets (its A columns jj2
+    // landed during the previous row), row + 2 NG's A entries, row + 3 NG's
+    // row pointers
+    wa1 = ra.ws8[2 * (int64_t)jj2];
+    wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj2 + 1);
+    uo1 = uoff_of(row + NG);
+    av1 = av2;
+    na1 = __builtin_amdgcn_readfirstlane(na2);
+    e2 = entry(a3, b3);
+    jj2 = (uint32_t)p.Aci[e2];
+    av2 = p.Av[e2];
+    na2 = b3 - a3;
+    arp2(row + 3 * NG, a3, b3);
+    for (int q = 0; q < nwin; ++q) {
+      const int TC = sTC, nr = snr, clo = sclo, want = swant;
+      const int64_t off = soff;
+      int lim = 0;
+      if (!sskip) {   // uniform
+        // ---- pass 1: the landed products, columns into the bitmap --------
+        // (a(i, j) from dval: rewritten only by the stage after this unit's pass 2)
+#pragma unroll
+        for (int d = 0; d < RL; ++d) {
+          const int t = gid + d * ngrp;
+          const float a = dval[t < TC ? t : TC - 1];
+          c[2 * d] = ((okm >> (2 * d)) & 1u) ? (int)xb[d].x - clo : -1;
+          c[2 * d + 1] = ((okm >> (2 * d + 1)) & 1u) ? (int)xb[d].z - clo : -1;
+          v[2 * d] = a * __uint_as_float(xb[d].y);
+          v[2 * d + 1] = a * __uint_as_float(xb[d].w);
+        }
+        uint32_t dupm = 0;
+        {
+          uint32_t old[RR];
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            old[d] = 0u;
+            if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
+          }
+#pragma unroll
+          for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
+        }
+        dirty = true;
+        if (dupm) sdup = 1;
+        __syncthreads();
+        // ---- rank prefix per 64-bit word (as spgemm_bm_rows) ------------
+        int run[WPT];
+        int wtot = 0;
+        if constexpr (PAIRS) {
+#pragma unroll
+          for (int kk = 0; kk < WPT / SG; ++kk) {
+            const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&bm[w * WPW + kk * 64 * SG + SG * lane]);
+            int cw[SG];
+#pragma unroll
+            for (int h = 0; h < SG / 2; ++h) {
+              const ulonglong2 x = src[h];
+              cw[2 * h] = __popcll(x.x);
+              cw[2 * h + 1] = __popcll(x.y);
+            }
+            int sum = 0;
+#pragma unroll
+            for (int i = 0; i < SG; ++i) {
+              if (i > 0) run[SG * kk + i] = sum;
+              sum += cw[i];
+            }
+            const int incl = bm_wave_incl(sum);
+            run[SG * kk] = wtot + incl - sum;
+            wtot += __builtin_amdgcn_readlane(incl, 63);
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < WPT; ++kk) {
+            const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
+            const int incl = bm_wave_incl(cnt);
+            run[kk] = wtot + incl - cnt;
+            wtot += __builtin_amdgcn_readlane(incl, 63);
+          }
+        }
+        const int any_dup = sdup;
+        if (lane == 0) wsum[w] = wtot;
+        __syncthreads();
+        int base = 0, total = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+          const int sw = wsum[i];
+          base += (i < w) ? sw : 0;
+          total += sw;
+        }
+        total = __builtin_amdgcn_readfirstlane(total);
+        if constexpr (PAIRS) {
+#pragma unroll
+          for (int kk = 0; kk < WPT / SG; ++kk) {
+            const uint32_t g0 = (uint32_t)(base + run[SG * kk]);
+            uint32_t pk[SG / 2];
+#pragma unroll
+            for (int h = 0; h < SG / 2; ++h) {
+              const uint32_t lo = g0 + (h > 0 ? (uint32_t)run[SG * kk + 2 * h] : 0u);
+              const uint32_t hi = g0 + (uint32_t)run[SG * kk + 2 * h + 1];
+              pk[h] = (lo & 0xffffu) | (hi << 16);
+            }
+            uint16_t* dst = &pre16[w * WPW + kk * 64 * SG + SG * lane];
+            if constexpr (SG == 2) {
+              *reinterpret_cast<uint32_t*>(dst) = pk[0];
+            } else if constexpr (SG == 4) {
+              *reinterpret_cast<uint2*>(dst) = make_uint2(pk[0], pk[1]);
+            } else {
+              static_assert(SG == 8, "sweep group of 2, 4 or 8 words");
+              *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
+        }
+        if (tid == 0) sdup = 0;
+        __syncthreads();
+        // ---- pass 2: rank -> slot; owners store, duplicates add after a barrier
+        auto rank = [&](int cc) {
+          const int wd = cc >> 6;
+          return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
+        };
+#pragma unroll
+        for (int d0 = 0; d0 < RR; d0 += 4) {
+          if (d0 >= nr * 2) break;   // uniform: slots past the unit's chunks hold no product
+          int r[4];
+#pragma unroll
+          for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
+#pragma unroll
+          for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) {
+            const int d = d0 + dd;
+            if (c[d] >= 0 && !((dupm >> d) & 1u))
+              items[r[dd]] = ((unsigned long long)__float_as_uint(v[d]) << 32) | (uint32_t)(c[d] + clo);
+          }
+        }
+        if (any_dup) {   // uniform
+          __syncthreads();
+#pragma unroll
+          for (int d = 0; d < RR; ++d)
+            if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+        }
+        lim = total;
+        if (want != total || off < 0 || off + total > p.cap) {   // never write outside the unit or C
+          if (tid == 0) atomicOr(p.err, 2);
+          lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : want);
+        }
+      }
+      // ---- stage the next unit and issue its B gathers; then this unit's write-out
+      bool more = true;
+      if (q + 1 < nwin) {   // uniform
+        sq = q + 1;
+      } else {
+        srow = row + NG;
+        sq = 0;
+        more = srow < m;
+        if (more) take_row();
+      }
+      if (more) {
+        stage();
+        issue_loads();
+      } else {
+        __syncthreads();   // this unit's pass 2 done before its slots are read
+      }
+      write_out(off, lim);
+    }
+  }
+}
+
 // ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
 // The count kernel of the same row pipeline: one window's bitmap (16 KB at
 // W = 2^17) per workgroup, so eight 256-thread workgroups share a CU and
@@ -1582,8 +1991,12 @@ struct BmKernels {
   static constexpr auto count = spgemm_bm<K.lgw, K.nsub_count, kCountNT, 2, 1, 2048, 0>;
   static constexpr auto fast = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
                                          K.rounds_fast * (kFastNT / 16), 1>;
+  // the wide kernel reads two padded pairs per lane: it exists only for an even
+  // round count; otherwise bm_numeric takes the plain kernel (B read through
+  // ws / Bci / Bv, never the padded pair array at unpadded offsets)
+  static constexpr bool kWide = K.rounds_fast % 2 == 0;
   static constexpr auto fast_wide = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
-                                              K.rounds_fast * (kFastNT / 16), 1, false, true, K.rounds_fast % 2 == 0>;
+                                              K.rounds_fast * (kFastNT / 16), 1, false, kWide, kWide>;
   static constexpr int kReloadNT = reload_nt(K.lgw);
   static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2>;
   static constexpr auto fast_det = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
@@ -1621,20 +2034,26 @@ struct BmRowKernel {
   static constexpr auto kcvw = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false, R % 2 == 0>;
   static constexpr auto k_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, true>;
   static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, true>;
+  static constexpr int RP = R & ~1;   // the pipelined kernel loads two pairs per lane and round
+  static constexpr auto kpipe = spgemm_bm_rows_pipe<K.lgw, NT, K.pcap_fast, RP, RP * (NT / 16)>;
 };
 
 
-template <typename Kern>
-int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastNT) {
+template <typename Kern, typename Args>
+int launch_rows(Kern kernel, const Args& args, int64_t m, hipStream_t s, int nt = kFastNT) {
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, nt, 0) != hipSuccess || per <= 0) per = 1;
   int64_t g = (int64_t)per * ncu;
-  if (ra.a.m < g) g = ra.a.m;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(nt), 0, s, ra);
+  if (m < g) g = m;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(nt), 0, s, args);
   SPMM_LAUNCH_CHECK();
   return 0;
+}
+template <typename Kern>
+int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastNT) {
+  return launch_rows(kernel, ra, ra.a.m, s, nt);
 }
 
 // count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
@@ -1670,12 +2089,15 @@ int bm_count_rows(BmRowArgs ra, int nsub, hipStream_t s) {
 
 // det: the deterministic kernels (fixed summation order)
 template <int C>
-int bm_numeric_rows(BmRowArgs ra, int det, hipStream_t s) {
+int bm_numeric_rows(BmRowArgs ra, int det, int64_t nbcv, int pipe, int64_t annz, hipStream_t s) {
   using K = BmRowKernel<C>;
   // 2 pairs per lane and 16-byte loads on the padded pairs (1M numeric 52.8 ->
-  // 50.6 ms vs one 8-byte pair per lane, PERF_LOG round 4)
+  // 50.6 ms vs one 8-byte pair per lane, PERF_LOG round 4); pipelined when
+  // the padded pairs fit 32-bit buffer offsets
   const bool wide = ra.a.Bcv && ra.pad && ra.a.lg >= 1;
-  const int rc = det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
+  const bool piped = wide && !det && pipe && annz > 0 && nbcv > 0 && nbcv * 8 < (int64_t(1) << 32);
+  const int rc = piped ? launch_rows(K::kpipe, BmPipeArgs{ra, (uint32_t)(nbcv * 8), annz}, ra.a.m, s, K::NT)
+               : det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
                      : (wide ? launch_rows(K::kcvw, ra, s, K::NT)
                              : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT)));
   if (rc) return rc;
@@ -1686,7 +2108,7 @@ int bm_numeric_rows(BmRowArgs ra, int det, hipStream_t s) {
 template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, int det, hipStream_t s) {
   using K = BmKernels<C>;
-  const bool wide = a.ws8 != nullptr && a.Bcv != nullptr && a.lg >= 1;   // padded pairs given
+  const bool wide = K::kWide && a.ws8 != nullptr && a.Bcv != nullptr && a.lg >= 1;   // padded pairs given
   const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s)
                      : (wide ? launch_bm(K::fast_wide, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s));
   if (rc) return rc;
@@ -1770,12 +2192,15 @@ SPMM_EXPORT int spmm_spgemm_bm_stamps(int on, unsigned long long* out8) {
 // Row-major numeric (nwin <= 8, ws8 from spmm_spgemm_bm_pack_ws8), then the
 // reload kernel over the deferred units; same contract as spmm_spgemm_bm_numeric.
 // Bcv: optional [nnz(B)] (column, value bits) pairs read by the row-major kernel.
+// nbcv: pairs in Bcv; pipe: the software-pipelined kernel (padded pairs, unordered
+// sum, nbcv * 8 < 2^32, annz = nnz(A) > 0), else the flat one.
 SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                             const void* ws8, const uint32_t* ws, const int32_t* Bci, const float* Bv,
                                             const void* Bcv,
                                             int64_t m, int nwin, int lg, const int64_t* uoff, int64_t cap,
                                             int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                                            int32_t* err, int det, int pad, void* stream) {
+                                            int32_t* err, int det, int pad, int64_t nbcv, int pipe, int64_t annz,
+                                            void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   if (pad && !Bcv) return (int)hipErrorInvalidValue;
@@ -1784,9 +2209,9 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
                (const uint4*)ws8, pad ? 1 : 0};
   hipStream_t s = (hipStream_t)stream;
   switch (cfg) {
-    case 0: return bm_numeric_rows<0>(ra, det, s);
-    case 1: return bm_numeric_rows<1>(ra, det, s);
-    default: return bm_numeric_rows<2>(ra, det, s);
+    case 0: return bm_numeric_rows<0>(ra, det, nbcv, pipe, annz, s);
+    case 1: return bm_numeric_rows<1>(ra, det, nbcv, pipe, annz, s);
+    default: return bm_numeric_rows<2>(ra, det, nbcv, pipe, annz, s);
   }
 }
 

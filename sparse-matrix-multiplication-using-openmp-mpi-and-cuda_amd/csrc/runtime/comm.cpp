@@ -141,6 +141,7 @@ class RcclComm : public Comm {
 
   void send_dev(const DevMat& M, int dst, hipStream_t s) override {
     maybe_inject_fault("send");
+    arrive({dst});
     hhdr_[0] = M.rows; hhdr_[1] = M.cols; hhdr_[2] = M.k; hhdr_[3] = M.nb;
     A4_HIP(hipMemcpyAsync(dhdr_, hhdr_, 4 * sizeof(int64_t), hipMemcpyHostToDevice, s));
     A4_NCCL(ncclSend(dhdr_, 4, ncclInt64, dst, comm_, s));
@@ -152,6 +153,7 @@ class RcclComm : public Comm {
     bytes_sent += M.bytes() + 32;
   }
   DevMat recv_dev(int src, hipStream_t s) override {
+    arrive({src});
     A4_NCCL(ncclRecv(dhdr_, 4, ncclInt64, src, comm_, s));
     A4_HIP(hipMemcpyAsync(hhdr_, dhdr_, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     wait(s);
@@ -174,6 +176,7 @@ class RcclComm : public Comm {
     if (ms.empty()) return;
     maybe_inject_fault("send");
     const size_t n = ms.size();
+    arrive(dsts);
     ensure_hdrs(n);
     for (size_t i = 0; i < n; ++i) {
       const DevMat& M = *ms[i];
@@ -197,6 +200,7 @@ class RcclComm : public Comm {
     const size_t n = srcs.size();
     std::vector<DevMat> out(n);
     if (!n) return out;
+    arrive(srcs);
     ensure_hdrs(n);
     A4_NCCL(ncclGroupStart());
     for (size_t i = 0; i < n; ++i) A4_NCCL(ncclRecv(dh_ + 4 * i, 4, ncclInt64, srcs[i], comm_, s));
@@ -231,6 +235,7 @@ class RcclComm : public Comm {
   }
   void allgatherv_dev(const void* send, void* recv, const std::vector<size_t>& bytes, hipStream_t s) override {
     maybe_inject_fault("send");
+    A4_MPI(MPI_Barrier(MPI_COMM_WORLD));   // every rank has arrived: the timeout bounds the transfer only
     size_t at = 0;
     A4_NCCL(ncclGroupStart());
     for (int r = 0; r < world_; ++r) {
@@ -254,6 +259,23 @@ class RcclComm : public Comm {
   }
 
  private:
+  // Arrival handshake: a zero-byte MPI token exchanged with every peer of the
+  // transfer before its RCCL calls are posted.  A slow peer (skewed work,
+  // rank 0 writing the output) is waited for here, without a bound, as the
+  // reference's blocking MPI calls wait; a dead peer ends the job through the
+  // MPI launcher.  The RCCL wait below then times only the transfer itself,
+  // so a healthy but skewed job never trips the timeout.
+  void arrive(const std::vector<int>& peers) {
+    std::vector<MPI_Request> rq(2 * peers.size());
+    char tok_out = 1;
+    std::vector<char> tok_in(peers.size());
+    for (size_t i = 0; i < peers.size(); ++i) {
+      A4_MPI(MPI_Isend(&tok_out, 0, MPI_BYTE, peers[i], kArriveTag, MPI_COMM_WORLD, &rq[2 * i]));
+      A4_MPI(MPI_Irecv(&tok_in[i], 0, MPI_BYTE, peers[i], kArriveTag, MPI_COMM_WORLD, &rq[2 * i + 1]));
+    }
+    if (!rq.empty()) A4_MPI(MPI_Waitall((int)rq.size(), rq.data(), MPI_STATUSES_IGNORE));
+  }
+  static constexpr int kArriveTag = 0x5a4;
   // Bounded wait: a peer that died leaves the stream pending forever; poll the
   // communicator's async error and give up after the timeout (fail fast).
   void wait(hipStream_t s) {

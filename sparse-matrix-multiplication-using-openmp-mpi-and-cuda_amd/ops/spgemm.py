@@ -65,7 +65,7 @@ _native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, 
 _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, C_INT, c_vp, c_vp,
                      C_I64, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
-                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, c_vp)
+                     C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, C_I64, C_INT, C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
                      C_I64, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
@@ -879,7 +879,9 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
         _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
                                                       P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
                                                       plan.lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf),
-                                                      P(novf), ovf_cap, P(err), det, int(plen is not None), st),
+                                                      P(novf), ovf_cap, P(err), det, int(plen is not None),
+                                                      Bcv.shape[0] if Bcv is not None else 0,
+                                                      int(CONFIG.spgemm_bitmap_pipe > 0), _true_nnz(A), st),
                       "spgemm_bm_numeric_rows")
         if info is not None:
             info.rows_per_bin_num["bitmap_rows"] = 1

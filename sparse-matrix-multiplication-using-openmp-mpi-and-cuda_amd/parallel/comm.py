@@ -230,7 +230,7 @@ def init(backend: str = "auto", device: str = "auto", timeout_s: Optional[float]
     ``cuda`` or ``cpu``.
 
     timeout_s (default ``CONFIG.comm_timeout_s``, env ``SPMM_COMM_TIMEOUT``,
-    120 s): a collective that has not completed by then raises (gloo) or
+    600 s; the test suite sets 120 s): a collective that has not completed by then raises (gloo) or
     aborts the communicator and the process (RCCL watchdog), so a stuck rank
     names itself instead of hanging the job past a launcher's silence window.
     The reference's blocking MPI calls have no timeout at all

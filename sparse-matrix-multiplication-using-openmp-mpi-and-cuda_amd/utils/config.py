@@ -60,6 +60,9 @@ class Config:
     # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU
     # engine) on the bitmap-rank path: 0 = off, 1 = on (other GPU paths stay unordered), 2 = strict
     # (a product no deterministic GPU kernel covers runs on the CPU engine)
+    # row-major bitmap numeric kernel: software-pipelined (next unit's B gathers issued before this
+    # unit's write-out, buffer-descriptor addressing) = 1, flat kernel = 0 (PERF_LOG round 5)
+    spgemm_bitmap_pipe: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_PIPE", 1, int))
     spgemm_deterministic: int = field(default_factory=lambda: _env("SPMM_SPGEMM_DETERMINISTIC", 0, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))
     # long-row routing histogram reads a chunk-offset table for the long rows of B (1) or their columns (0)
@@ -72,8 +75,13 @@ class Config:
     # (65536^2 @ 0.1 % x 128 cols, BASELINE config 3, which names the MFMA path)
     # the two kernels are within 5 %: MFMA 149 us, row kernel 142 us (PERF_LOG)
     spmm_mfma_min_reuse: float = field(default_factory=lambda: _env("SPMM_MFMA_MIN_REUSE", 1.0, float))
-    # seconds before a pending collective raises / aborts (below the launchers' ~180 s silence window)
-    comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 120.0, float))
+    # seconds before a pending collective raises / aborts.  torch.distributed's
+    # watchdog also counts the wait for a slower peer to arrive (skewed R-MAT
+    # panels, rank 0 writing output), so the default leaves room for that; the
+    # test suite sets 120 s (tests/conftest.py).  The native a4 separates the
+    # two: an MPI arrival handshake first, then a 120 s bound on the RCCL
+    # transfer alone (csrc/runtime/comm.cpp RcclComm::arrive)
+    comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))
 
     def as_dict(self) -> dict:
         return {f.name: getattr(self, f.name) for f in fields(self)}

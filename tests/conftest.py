@@ -8,6 +8,11 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# collectives inside the test runs fail within 120 s (under the GPU launcher's
+# silence window); the library default is longer (utils/config.py)
+os.environ.setdefault("SPMM_COMM_TIMEOUT", "120")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")

@@ -1164,3 +1164,92 @@ def test_spgemm_graph_replay_matches_eager(n, d):
         assert info.nnz == C1.nnz
         assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
         assert torch.allclose(C1.val, C2.val, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_spgemm_graph_replay_after_value_change():
+    """Values of B changed IN PLACE between replays: the next replay of the
+    captured graph computes the product of the new values (the graph holds
+    pointers, not a cached C), matching a fresh eager product."""
+    dev = torch.device("cuda")
+    n, d = 65536, 1e-3
+    A = gen_csr.uniform_csr(n, n, d, seed=13, device=dev)
+    B = gen_csr.uniform_csr(n, n, d, seed=14, device=dev)
+    g = SG.SpgemmGraph(A, B)
+    g.run()
+    v0 = g.result().val.clone()   # (result() views the graph's own C buffers)
+    gen = torch.Generator(device=dev).manual_seed(5)
+    B.val.copy_(torch.rand(B.val.shape, generator=gen, device=dev) * 2 - 1)   # new values, same structure
+    A.val.mul_(-0.5)
+    g.run()
+    C1 = g.result()
+    ref = SG.spgemm(A, B)
+    assert torch.equal(ref.rowptr, C1.rowptr) and torch.equal(ref.col, C1.col)
+    assert torch.allclose(ref.val, C1.val, atol=1e-6, rtol=1e-5)
+    assert not torch.allclose(v0, C1.val)   # the replay did recompute
+
+
+@pytest.mark.gpu
+def test_spgemm_graph_replay_structure_change():
+    """B's column structure changed in place (same row lengths): every
+    kernel of the product is in the graph, so the replay gives the new
+    product.  A's rows changed so that the product exceeds the plan's C
+    capacity: result() reports it (no C is returned) and nothing outside C
+    is written -- a canary allocated next to the operands is intact and a
+    later eager product is still exact."""
+    dev = torch.device("cuda")
+    n, d = 65536, 1e-3
+    A = gen_csr.uniform_csr(n, n, d, seed=23, device=dev)
+    B = gen_csr.uniform_csr(n, n, d, seed=24, device=dev)
+    g = SG.SpgemmGraph(A, B)
+    # (1) new B columns: shift every column by a row-dependent offset, re-sorted per row
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), B.rowptr[1:] - B.rowptr[:-1])
+    newc = (B.col.long() + 7 * rows + 1) % n
+    key = rows * n + newc
+    order = torch.argsort(key)
+    B.col.copy_(newc[order].to(B.col.dtype))
+    B.val.copy_(B.val[order])
+    g.run()
+    C1 = g.result()
+    ref = SG.spgemm(A, B)
+    assert torch.equal(ref.rowptr, C1.rowptr) and torch.equal(ref.col, C1.col)
+    assert torch.allclose(ref.val, C1.val, atol=1e-6, rtol=1e-5)
+    # (2) B's entries moved into the first half of its rows (each about twice
+    # as long) and A's columns folded onto those rows: about twice the
+    # products the graph's C capacity was planned for
+    canary = torch.full((1 << 20,), 7, dtype=torch.int32, device=dev)
+    nnz_b, half = B.nnz, n // 2
+    lens = torch.full((half,), nnz_b // half, dtype=torch.int64, device=dev)
+    lens[: nnz_b - int(lens.sum())] += 1
+    rp = torch.zeros(n + 1, dtype=B.rowptr.dtype, device=dev)
+    rp[1:half + 1] = torch.cumsum(lens, 0).to(rp.dtype)
+    rp[half + 1:] = nnz_b
+    B.rowptr.copy_(rp)
+    brow = torch.repeat_interleave(torch.arange(half, device=dev), lens)
+    k = torch.arange(nnz_b, device=dev) - (rp[:-1].long())[brow]
+    bcol = (k * 499 + brow * 7) % n   # distinct within a row (499 * k < n)
+    order = torch.argsort(brow * n + bcol)
+    B.col.copy_(bcol[order].to(B.col.dtype))
+    A.col.copy_((A.col.long() % half).to(A.col.dtype))
+    arows = torch.repeat_interleave(torch.arange(n, device=dev), A.rowptr[1:] - A.rowptr[:-1])
+    order = torch.argsort(arows * n + A.col.long())
+    A.col.copy_(A.col[order])
+    A.val.copy_(A.val[order])
+    assert int(SG.row_nprod(A, B).sum()) > g.plan.tot
+    g.run()
+    with pytest.raises(RuntimeError):
+        g.result()
+    torch.cuda.synchronize()
+    assert int((canary != 7).sum()) == 0
+    C3 = SG.spgemm(A, B)   # the device is still sound: a fresh eager product is exact
+    assert C3.is_sorted()
+    for r in torch.randint(0, n, (8,)).tolist():
+        want = torch.zeros(n, dtype=torch.float64, device=dev)
+        for e in range(int(A.rowptr[r]), int(A.rowptr[r + 1])):
+            j, a = int(A.col[e]), float(A.val[e])
+            lo, hi = int(B.rowptr[j]), int(B.rowptr[j + 1])
+            want.index_add_(0, B.col[lo:hi].long(), a * B.val[lo:hi].double())
+        got = torch.zeros(n, dtype=torch.float64, device=dev)
+        lo, hi = int(C3.rowptr[r]), int(C3.rowptr[r + 1])
+        got[C3.col[lo:hi].long()] = C3.val[lo:hi].double()
+        assert torch.allclose(got, want, atol=1e-4, rtol=1e-4), r
