@@ -1362,6 +1362,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   const int gl = lane & (Gl - 1);
   const int nwin = p.nwin;
   uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  BM_STAMP_DECL
   if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
   const auto rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(p.Bcv), 0, (int)pa.bcv_bytes, 0x00020000);
 
@@ -1385,10 +1386,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   // materialises as copies that wait for the load: a full memory latency
   // per row).  Indices are clamped into range (values past the matrix or the
   // row are never used).
-  auto arp2 = [&](int r, int& a, int& b) {   // row pointers of row r (clamped)
+  auto arp2 = [&](int r, int& a, int& b) {   // row pointers of row r (clamped; low words: nnz(A) < 2^31)
     const int rr = r < m ? r : m - 1;
-    a = (int)p.Arp[rr];
-    b = (int)p.Arp[rr + 1];
+    const int* lo = reinterpret_cast<const int*>(p.Arp);
+    a = lo[2 * rr];
+    b = lo[2 * rr + 2];
   };
   auto entry = [&](int a, int b) {   // this thread's A entry of the row [a, b) (clamped)
     const int a0 = __builtin_amdgcn_readfirstlane(a), na = __builtin_amdgcn_readfirstlane(b) - a0;
@@ -1401,20 +1403,38 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   };
   int a1 = 0, b1 = 0, a2 = 0, b2 = 0, a3 = 0, b3 = 0;
   arp2(me, a1, b1);
-  arp2(me + NG, a2, b2);
   int e2 = entry(a1, b1);
   uint32_t jj1 = (uint32_t)p.Aci[e2];   // row me: A column / value of this thread's entry
   float av1 = p.Av[e2];
   uint4 wa1 = ra.ws8[2 * (int64_t)jj1];   // ... its packed bounds and the row's unit offsets
   uint2 wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj1 + 1);
   int64_t uo1 = uoff_of(me);
-  int na1 = b1 - a1;
+  int na1 = __builtin_amdgcn_readfirstlane(b1 - a1);
+  arp2(me + NG, a2, b2);
   e2 = entry(a2, b2);
-  uint32_t jj2 = (uint32_t)p.Aci[e2];   // row me + NG
+  uint32_t jj2 = (uint32_t)p.Aci[e2];   // row me + NG: its A entries
   float av2 = p.Av[e2];
   int na2 = b2 - a2;
-  arp2(me + 2 * NG, a3, b3);            // row me + 2 NG
-  na1 = __builtin_amdgcn_readfirstlane(na1);
+  arp2(me + 2 * NG, a3, b3);            // row me + 2 NG: its row pointers
+  // Once per row, in the LAST unit of row r (after its pass 1, with loads
+  // that land while the unit finishes): row r + NG's inputs are taken into
+  // the staging registers, then row r + 2 NG's bounds and offsets are loaded
+  // from its A columns (landed one row ago), row r + 3 NG's A entries from its
+  // row pointers (idem) and row r + 4 NG's row pointers.  No load sits under
+  // a branch and none is consumed in the unit that issues it.
+  auto row_block = [&](int r) {
+    jj1 = jj2;
+    wa1 = ra.ws8[2 * (int64_t)jj1];
+    wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj1 + 1);
+    uo1 = uoff_of(r + 2 * NG);
+    av1 = av2;
+    na1 = __builtin_amdgcn_readfirstlane(na2);
+    e2 = entry(a3, b3);
+    jj2 = (uint32_t)p.Aci[e2];
+    av2 = p.Av[e2];
+    na2 = b3 - a3;
+    arp2(r + 4 * NG, a3, b3);
+  };
 
   // staging registers of the row being staged
   int cna = 0;
@@ -1539,7 +1559,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
     }
   };
 
-  take_row();
+  take_row();           // staging registers: row me
+  row_block(me - NG);   // next-row registers: row me + NG's bounds; A entries of me + 2 NG; Arp of me + 3 NG
   stage();
   issue_loads();
   // the loop is entered with the same stores behind the first unit's B
@@ -1548,25 +1569,20 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   write_out(0, 0);
   int c[RR];
   float v[RR];
-  for (int row = me; row < m; row += NG) {
-    // ---- once per row: row + NG's bounds and offsets (its A columns jj2
-    // landed during the previous row), row + 2 NG's A entries, row + 3 NG's
-    // row pointers
-    wa1 = ra.ws8[2 * (int64_t)jj2];
-    wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj2 + 1);
-    uo1 = uoff_of(row + NG);
-    av1 = av2;
-    na1 = __builtin_amdgcn_readfirstlane(na2);
-    e2 = entry(a3, b3);
-    jj2 = (uint32_t)p.Aci[e2];
-    av2 = p.Av[e2];
-    na2 = b3 - a3;
-    arp2(row + 3 * NG, a3, b3);
-    for (int q = 0; q < nwin; ++q) {
+  // one unit of row `row`, window q; LAST: the row's last window (the row
+  // inputs move one row along, and the next unit staged is the next row's first)
+  auto unit = [&](auto last_tag, int row, int q) {
+    constexpr bool LAST = decltype(last_tag)::value;
       const int TC = sTC, nr = snr, clo = sclo, want = swant;
       const int64_t off = soff;
       int lim = 0;
-      if (!sskip) {   // uniform
+      BM_STAMP(4);   // (the previous unit's write-out)
+      if (sskip) {   // uniform
+        if constexpr (LAST) {
+          take_row();
+          row_block(row);
+        }
+      } else {
         // ---- pass 1: the landed products, columns into the bitmap --------
         // (a(i, j) from dval: rewritten only by the stage after this unit's pass 2)
 #pragma unroll
@@ -1592,6 +1608,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
         dirty = true;
         if (dupm) sdup = 1;
         __syncthreads();
+        if constexpr (LAST) {   // the next row into the staging registers; the row inputs move along
+          take_row();
+          row_block(row);
+        }
+        BM_STAMP(1);
         // ---- rank prefix per 64-bit word (as spgemm_bm_rows) ------------
         int run[WPT];
         int wtot = 0;
@@ -1663,6 +1684,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
         }
         if (tid == 0) sdup = 0;
         __syncthreads();
+        BM_STAMP(2);
         // ---- pass 2: rank -> slot; owners store, duplicates add after a barrier
         auto rank = [&](int cc) {
           const int wd = cc >> 6;
@@ -1693,15 +1715,15 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
           lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : want);
         }
       }
+      BM_STAMP(3);
       // ---- stage the next unit and issue its B gathers; then this unit's write-out
       bool more = true;
-      if (q + 1 < nwin) {   // uniform
-        sq = q + 1;
-      } else {
+      if constexpr (LAST) {
         srow = row + NG;
         sq = 0;
         more = srow < m;
-        if (more) take_row();
+      } else {
+        sq = q + 1;
       }
       if (more) {
         stage();
@@ -1709,9 +1731,15 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
       } else {
         __syncthreads();   // this unit's pass 2 done before its slots are read
       }
+      BM_STAMP(0);
+      BM_STAMP_UNIT();
       write_out(off, lim);
-    }
+      };
+  for (int row = me; row < m; row += NG) {
+    for (int q = 0; q + 1 < nwin; ++q) unit(std::false_type{}, row, q);
+    unit(std::true_type{}, row, nwin - 1);
   }
+  BM_STAMP_FLUSH();
 }
 
 // ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
@@ -1949,6 +1977,258 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   }
 }
 
+// ---- pipelined row-major count kernel (two-window units, padded columns) ---
+// spgemm_bm_rows_count<..., NSUB = 2, PADC> in the pipelined form of
+// spgemm_bm_rows_pipe: unit k+1's scan rides unit k's OR phase (its
+// per-wave sums are written before that phase's barrier), its descriptors
+// are written after it and its B loads issued BEFORE unit k's popcount and
+// clear, so the gathers travel while unit k's bitmap is counted and
+// cleared.  Three barriers per unit instead of four; column loads through a
+// buffer descriptor (32-bit offsets); the row inputs are loaded once per row
+// at the top of the row loop from values that landed during the previous
+// row (as in spgemm_bm_rows_pipe).  Chunks past the RR load rounds (rare:
+// units of > RR * ngrp chunks) are loaded and ORed in the same phase,
+// synchronously.
+struct BmCountPipeArgs {
+  BmRowArgs r;
+  uint32_t colp_bytes;   // bytes of the padded column array (< 2^32: checked by the host)
+  int64_t annz;          // nnz(A) > 0
+};
+
+template <int LGW, int NT, int RR, int CCAP>
+__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeArgs pa) {
+  const BmRowArgs& ra = pa.r;
+  const BmArgs& p = ra.a;
+  constexpr int NSUB = 2;
+  constexpr int NW = NT / 64;
+  constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  constexpr int WORDS_PER_WIN = NWORD / NSUB;
+  constexpr int WAVES_PER_WIN = WORDS_PER_WIN / WPW;
+  static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
+  static_assert(RR * 4 <= 32, "one bit per loaded column");
+
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
+  __shared__ int wscan[2 * NW];
+  __shared__ int csum[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = p.lg - 1;       // log2 lanes per chunk (four columns per lane)
+  const int Gl = 1 << lg;
+  const int Gc = Gl << 2;        // columns per chunk
+  const int ngrp = NW << (6 - lg);
+  const int gid = (w << (6 - lg)) + (lane >> lg);
+  const int gl = lane & (Gl - 1);
+  const int nwin = p.nwin;
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  if (*p.err & 8) return;   // ws8 lengths truncated: the host re-counts with spgemm_bm (uniform exit)
+  const auto rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(p.Bci), 0, (int)pa.colp_bytes, 0x00020000);
+  const auto rsu = __builtin_amdgcn_make_buffer_rsrc(p.ucnt, 0, (int)((uint32_t)p.m * (uint32_t)nwin * 4u), 0x00020000);
+
+  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+
+  const int NG = (int)gridDim.x;
+  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+  const int m = (int)p.m;
+  const int annz = (int)pa.annz;
+  const int ngc = (nwin + 1) / 2;   // units per row
+
+  // ---- row pipeline (as spgemm_bm_rows_pipe) --------------------------------
+  auto arp2 = [&](int r, int& a, int& b) {   // (low words: nnz(A) < 2^31)
+    const int rr = r < m ? r : m - 1;
+    const int* lo = reinterpret_cast<const int*>(p.Arp);
+    a = lo[2 * rr];
+    b = lo[2 * rr + 2];
+  };
+  auto entry = [&](int a, int b) {
+    const int a0 = __builtin_amdgcn_readfirstlane(a), na = __builtin_amdgcn_readfirstlane(b) - a0;
+    const int e = a0 + (tid < na ? tid : 0);
+    return e < annz ? e : annz - 1;
+  };
+  int a1 = 0, b1 = 0, a2 = 0, b2 = 0, a3 = 0, b3 = 0;
+  arp2(me, a1, b1);
+  uint32_t jj1 = (uint32_t)p.Aci[entry(a1, b1)];
+  uint4 wa1 = ra.ws8[2 * (int64_t)jj1];       // {., lengths of windows 0-1, 2-3, 4-5}
+  uint4 wb1 = ra.ws8[2 * (int64_t)jj1 + 1];   // {lengths 6-7, ., first padded column, .}
+  int na1 = __builtin_amdgcn_readfirstlane(b1 - a1);
+  arp2(me + NG, a2, b2);
+  uint32_t jj2 = (uint32_t)p.Aci[entry(a2, b2)];
+  int na2 = b2 - a2;
+  arp2(me + 2 * NG, a3, b3);
+  // once per row, at the top of row r's last unit (after take_row took row
+  // r + NG): row r + 2 NG's bounds, row r + 3 NG's A columns, row r + 4 NG's
+  // row pointers (as spgemm_bm_rows_pipe's row_block)
+  auto row_block = [&](int r) {
+    wa1 = ra.ws8[2 * (int64_t)jj2];
+    wb1 = ra.ws8[2 * (int64_t)jj2 + 1];
+    na1 = __builtin_amdgcn_readfirstlane(na2);
+    jj2 = (uint32_t)p.Aci[entry(a3, b3)];
+    na2 = b3 - a3;
+    arp2(r + 4 * NG, a3, b3);
+  };
+
+  int cna = 0;
+  uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0;   // a unit's two 16-bit lengths: cl0 (shifted down per unit)
+  uint32_t bq = 0;
+  auto take_row = [&]() {
+    cna = na1;
+    bq = wb1.z;
+    cl0 = wa1.y;
+    cl1 = wa1.z;
+    cl2 = wa1.w;
+    cl3 = wb1.x;
+  };
+
+  // ---- the staged unit ------------------------------------------------------
+  int su = 0, sq = 0, sTC = 0, snr = 0, sclo = 0, sP = 0;
+  uint2 xb[RR][2];     // four columns per round (two 8-byte halves)
+  uint32_t okb = 0;    // bit 4 d + i: column i of round d is in its segment
+  // per-thread scan inputs of the next unit (computed in the OR phase)
+  int nlen = 0, nch = 0;
+  uint32_t nb0 = 0;
+  auto next_inputs = [&]() {   // lengths of the next unit of the staged row (cl0), advance
+    nlen = 0;
+    nch = 0;
+    if (tid < cna) {
+      nlen = (int)(cl0 & 0xffffu) + (int)(cl0 >> 16);   // (lengths past nwin are packed as 0)
+      nch = (nlen + Gc - 1) / Gc;
+    }
+    nb0 = bq;
+    bq += (uint32_t)(((nlen + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg);
+    cl0 = cl1;
+    cl1 = cl2;
+    cl2 = cl3;
+  };
+  int pre = 0;
+  // the scan's per-wave sums (before a barrier) ...
+  auto scan_begin = [&]() {
+    const int xa = bm_wave_incl(nch), xc = bm_wave_incl(nlen);
+    if (lane == 63) {
+      wscan[w] = xa;
+      wscan[NW + w] = xc;
+    }
+    pre = xa - nch;
+  };
+  // ... and after it: totals, descriptors of the staged unit
+  auto scan_end = [&](int u, int q0) {
+    int qa = 0, ta = 0, tc = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int sa = wscan[i], sc = wscan[NW + i];
+      qa += (i < w) ? sa : 0;
+      ta += sa;
+      tc += sc;
+    }
+    pre += qa;
+    sTC = __builtin_amdgcn_readfirstlane(ta);
+    sP = __builtin_amdgcn_readfirstlane(tc);
+    su = u;
+    sq = q0;
+    sclo = q0 << LGW;
+    snr = (sTC + ngrp - 1) / ngrp;
+    for (int kk = 0; kk < nch; ++kk) {
+      const int rem = nlen - kk * Gc;
+      if (pre + kk < CCAP) desc[pre + kk] = make_uint2(nb0 + (uint32_t)(kk * Gc), (uint32_t)(rem < Gc ? rem : Gc));
+    }
+  };
+  auto ld_round = [&](int d, int i0, int TC, uint2 (&x)[2], uint32_t& ok4) {   // chunk round i0 + d of this lane group
+    const int t = gid + (i0 + d) * ngrp;
+    const uint2 ds = desc[t < TC ? t : TC - 1];
+    const int nv = (int)ds.y - 4 * gl;
+    const bool ok = (t < TC) & (nv > 0);
+    ok4 = ok ? ((nv >= 4) ? 15u : (1u << nv) - 1u) : 0u;
+    const bm_v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsb, (int)((ds.x + (ok ? (uint32_t)(4 * gl) : 0u)) * 4u), 0, 0);
+    x[0] = make_uint2(v.x, v.y);
+    x[1] = make_uint2(v.z, v.w);
+  };
+  auto issue_loads = [&]() {
+    okb = 0;
+    const int TC = sTC < CCAP ? sTC : CCAP;
+#pragma unroll
+    for (int d = 0; d < RR; ++d) {
+      xb[d][0] = make_uint2(0u, 0u);
+      xb[d][1] = make_uint2(0u, 0u);
+      if (d < snr) {   // wave-uniform guard
+        uint32_t ok4;
+        ld_round(d, 0, TC, xb[d], ok4);
+        okb |= ok4 << (4 * d);
+      }
+    }
+  };
+  auto or_cols = [&](const uint2 (&x)[2], uint32_t ok4, int clo) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if ((ok4 >> i) & 1u) {
+        const int cc = (int)(i < 2 ? (i == 0 ? x[0].x : x[0].y) : (i == 2 ? x[1].x : x[1].y)) - clo;
+        atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+      }
+    }
+  };
+
+  // prologue: the first unit staged and its loads issued
+  take_row();
+  row_block(me - NG);
+  next_inputs();
+  scan_begin();
+  __syncthreads();
+  scan_end(me * nwin, 0);
+  __syncthreads();
+  issue_loads();
+  // (one store per wave behind every unit's loads: the ucnt store; dropped here)
+  __builtin_amdgcn_raw_buffer_store_b32(0u, rsu, -1, 0, 0);
+
+  auto unit = [&](auto last_tag, int row, int g) {
+    constexpr bool LAST = decltype(last_tag)::value;
+    const int u = su, q0 = sq, TC = sTC, nr = snr, clo = sclo, P = sP;
+    if constexpr (LAST) {   // the next row into the staging registers; the row inputs move along
+      take_row();
+      row_block(row);
+    }
+    // ---- ORs of unit k (its loads landed) --------------------------------
+#pragma unroll
+    for (int d = 0; d < RR; ++d) or_cols(xb[d], (okb >> (4 * d)) & 15u, clo);
+    for (int i0 = RR; i0 < nr; ++i0) {   // rare: chunks past the register rounds, synchronously
+      uint2 x[2];
+      uint32_t ok4;
+      ld_round(0, i0, TC < CCAP ? TC : CCAP, x, ok4);
+      or_cols(x, ok4, clo);
+    }
+    // the next unit's scan inputs
+    const bool more = !LAST || row + NG < m;
+    next_inputs();
+    scan_begin();
+    __syncthreads();   // A: every OR of unit k done; the next scan's wave sums written
+    if (more) scan_end(LAST ? (row + NG) * nwin : row * nwin + 2 * (g + 1), LAST ? 0 : 2 * (g + 1));
+    __syncthreads();   // E: the next unit's descriptors written
+    if (more) issue_loads();
+    // ---- popcount of this wave's bitmap rows (unit k), clearing them ------
+    int cnt = 0;
+    if (P != 0) {   // uniform (an empty unit left the bitmap clean)
+#pragma unroll
+      for (int kk = 0; kk < WPT; ++kk) {
+        const int wd = w * WPW + kk * 64 + lane;
+        cnt += __popcll(bm[wd]);
+        bm[wd] = 0ull;
+      }
+      cnt = __builtin_amdgcn_readlane(bm_wave_incl(cnt), 63);
+    }
+    if (lane == 0) csum[w] = cnt;
+    if (TC > CCAP && tid == 0) atomicOr(p.err, 2);   // (never: A rows <= NT entries, checked by the host)
+    __syncthreads();   // F: bitmap clear for the next ORs, csum written
+    // ucnt of unit k's windows: one buffer store per wave (lanes past NSUB, other waves: dropped)
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[(lane & 1) * WAVES_PER_WIN + i];
+    const bool wr = w == 0 && lane < NSUB && q0 + lane < nwin;
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, rsu, wr ? (u + lane) * 4 : -1, 0, 0);
+  };
+  for (int row = me; row < m; row += NG) {
+    for (int g = 0; g + 1 < ngc; ++g) unit(std::false_type{}, row, g);
+    unit(std::true_type{}, row, ngc - 1);
+  }
+}
+
 // ---- configurations -------------------------------------------------------
 // Every fast kernel: 256 threads and <= 40 KB of LDS, so four workgroups
 // (16 waves, 128 VGPRs each) share a CU; count and reload kernels take most
@@ -2074,12 +2354,25 @@ struct BmRowCountKernel {
   static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, false>;
   static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR / 2, 256, true>;
 };
+// pipelined (two-window units, padded columns; 32 KB bitmap + 6 KB descriptors: 4 workgroups per CU)
+template <int C>
+struct BmRowCountPipe {
+  static constexpr int NT = 256;
+  static constexpr auto k = spgemm_bm_rows_count_pipe<kCfgs[C].lgw, NT, SPMM_BM_COUNT_RR / 2, 768>;
+};
 
 template <int C>
-int bm_count_rows(BmRowArgs ra, int nsub, hipStream_t s) {
+int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s) {
   using K1 = BmRowCountKernel<C, 1>;
   using K2 = BmRowCountKernel<C, 2>;
   using K4 = BmRowCountKernel<C, 4>;
+  const int64_t colp_bytes = ra.a.cap * 4;
+  // (pipelined from two units per row up: with one, every unit is a row's last and the
+  // pipeline only adds work -- 65536^2 count 1.32 -> 1.36 ms step, PERF_LOG round 5)
+  if (ra.pad && pipe && nsub == 2 && ra.a.nwin >= 3 && K2::NT == BmRowCountPipe<C>::NT && annz > 0 &&
+      colp_bytes < (int64_t(1) << 32) && ra.a.m * ra.a.nwin < (int64_t(1) << 30))
+    return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz}, ra.a.m, s,
+                       BmRowCountPipe<C>::NT);
   if (ra.pad)
     return nsub == 4 ? launch_rows(K4::kp, ra, s, K4::NT)
                      : (nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT));
@@ -2219,9 +2512,10 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
 // output as spmm_spgemm_bm_count.  Returns without counting when err bit 3
 // is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
 // pad: Bci is the padded column array of spmm_spgemm_bm_pad_pairs (gc = nsub).
+// pipe: the pipelined kernel (pad, nsub 2, nnzb * 4 < 2^32, annz = nnz(A) > 0).
 SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
                                           const int32_t* Bci, int64_t m, int nwin, int lg, int nsub, int32_t* ucnt,
-                                          int32_t* err, int64_t nnzb, int pad, void* stream) {
+                                          int32_t* err, int64_t nnzb, int pad, int pipe, int64_t annz, void* stream) {
   if (m <= 0) return 0;
   if (lg < 4 || lg > 6 || cfg < 0 || cfg >= kNumCfgs || nwin < 1 || nwin > 8) return (int)hipErrorInvalidValue;
   BmRowArgs ra{BmArgs{Arp, Aci, nullptr, nullptr, Bci, nullptr, m, nwin, lg, ucnt, nullptr, nullptr, nullptr, nullptr,
@@ -2230,8 +2524,8 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
   hipStream_t s = (hipStream_t)stream;
   if (nsub != 1 && nsub != 2 && nsub != 4) return (int)hipErrorInvalidValue;
   switch (cfg) {
-    case 0: return bm_count_rows<0>(ra, nsub, s);
-    case 1: return bm_count_rows<1>(ra, nsub, s);
-    default: return bm_count_rows<2>(ra, nsub, s);
+    case 0: return bm_count_rows<0>(ra, nsub, pipe, annz, s);
+    case 1: return bm_count_rows<1>(ra, nsub, pipe, annz, s);
+    default: return bm_count_rows<2>(ra, nsub, pipe, annz, s);
   }
 }

@@ -63,7 +63,7 @@ _native.register_hip("spmm_spgemm_bm_config", C_INT, c_vp, c_vp, c_vp, c_vp, c_v
 _native.register_hip("spmm_spgemm_bm_stamps", C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_pack_ws8", c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, C_INT, c_vp, c_vp,
-                     C_I64, C_INT, c_vp)
+                     C_I64, C_INT, C_INT, C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, C_I64, C_INT, C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
@@ -831,8 +831,8 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
                                                     P(colp) if colp is not None else P(B.col), m, nwin, plan.lg_c,
                                                     plan.nsub_c, P(ucnt), P(err),
                                                     colp.numel() if colp is not None else B.col.numel(),
-                                                    int(colp is not None),
-                                                    st),
+                                                    int(colp is not None), int(CONFIG.spgemm_bitmap_pipe > 0),
+                                                    _true_nnz(A), st),
                       "spgemm_bm_count_rows")
         del colp
     else:

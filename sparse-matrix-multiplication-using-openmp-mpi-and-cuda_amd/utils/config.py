@@ -60,8 +60,9 @@ class Config:
     # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU
     # engine) on the bitmap-rank path: 0 = off, 1 = on (other GPU paths stay unordered), 2 = strict
     # (a product no deterministic GPU kernel covers runs on the CPU engine)
-    # row-major bitmap numeric kernel: software-pipelined (next unit's B gathers issued before this
-    # unit's write-out, buffer-descriptor addressing) = 1, flat kernel = 0 (PERF_LOG round 5)
+    # row-major bitmap numeric and count kernels: software-pipelined (the next unit's B gathers
+    # issued before this unit's write-out / popcount, buffer-descriptor addressing) = 1, flat
+    # kernels = 0 (PERF_LOG round 5)
     spgemm_bitmap_pipe: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_PIPE", 1, int))
     spgemm_deterministic: int = field(default_factory=lambda: _env("SPMM_SPGEMM_DETERMINISTIC", 0, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))

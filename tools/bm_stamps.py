@@ -46,6 +46,8 @@ lib.spmm_spgemm_bm_stamps(0, None)
 st = list(out)
 units = max(st[7], 1)
 names = ["num staging", "num pass1", "num scan", "num pass2", "num writeout", "count stage+OR", "count pop+clear"]
+if os.environ.get("SPMM_SPGEMM_BITMAP_PIPE", "1") != "0":   # pipelined kernel: [0] = the NEXT unit staged + its loads issued
+    names[0] = "num stage next+ld"
 if info.rows_per_bin_num.get("bitmap_fused"):
     names[5:7] = ["fused count phase", "fused look-back"]
 tot = sum(st[:5])
