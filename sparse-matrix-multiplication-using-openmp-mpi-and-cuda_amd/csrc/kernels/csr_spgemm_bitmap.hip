@@ -2022,6 +2022,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   const int gl = lane & (Gl - 1);
   const int nwin = p.nwin;
   uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  BM_STAMP_DECL
   if (*p.err & 8) return;   // ws8 lengths truncated: the host re-counts with spgemm_bm (uniform exit)
   const auto rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(p.Bci), 0, (int)pa.colp_bytes, 0x00020000);
   const auto rsu = __builtin_amdgcn_make_buffer_rsrc(p.ucnt, 0, (int)((uint32_t)p.m * (uint32_t)nwin * 4u), 0x00020000);
@@ -2199,6 +2200,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     next_inputs();
     scan_begin();
     __syncthreads();   // A: every OR of unit k done; the next scan's wave sums written
+    BM_STAMP(5);
     if (more) scan_end(LAST ? (row + NG) * nwin : row * nwin + 2 * (g + 1), LAST ? 0 : 2 * (g + 1));
     __syncthreads();   // E: the next unit's descriptors written
     if (more) issue_loads();
@@ -2222,11 +2224,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[(lane & 1) * WAVES_PER_WIN + i];
     const bool wr = w == 0 && lane < NSUB && q0 + lane < nwin;
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, rsu, wr ? (u + lane) * 4 : -1, 0, 0);
+    BM_STAMP(6);
   };
   for (int row = me; row < m; row += NG) {
     for (int g = 0; g + 1 < ngc; ++g) unit(std::false_type{}, row, g);
     unit(std::true_type{}, row, ngc - 1);
   }
+  BM_STAMP_FLUSH();
 }
 
 // ---- configurations -------------------------------------------------------

@@ -454,6 +454,29 @@ def _true_nnz(B: CSR) -> int:
     return max(B.nnz, getattr(B, "_nnz_total", 0))
 
 
+_native.register_hip("spmm_prim_scan_ws", C_I64, restype=C.c_size_t)
+_native.register_hip("spmm_prim_scan", c_vp, C_INT, C_I64, c_vp, C_INT, c_vp, c_vp)
+
+
+def device_scan(x: torch.Tensor, out: torch.Tensor, inclusive: bool) -> torch.Tensor:
+    """out[i] = sum x[0..i] (inclusive) or x[0..i-1] (exclusive), int64, with
+    the in-tree scan kernels (csrc/kernels/prim.hip: tile reduce, recursive
+    scan of the tile sums, tile scan + carry).  Launches only -- capturable
+    into a HIP graph; replaces the host prefix of the reference
+    (sparse_matrix_mult.cu:214-216) and keeps rocPRIM out of the bitmap
+    product's kernel set."""
+    n = x.numel()
+    assert out.dtype == torch.int64 and out.numel() >= n and x.dtype in (torch.int32, torch.int64)
+    if n == 0:
+        return out
+    lib = _native.hip()
+    ws = torch.empty(int(lib.spmm_prim_scan_ws(n)), dtype=torch.uint8, device=x.device)
+    x = x.contiguous()
+    _native.check(lib.spmm_prim_scan(_native.ptr(x), x.element_size(), n, _native.ptr(out), int(inclusive),
+                                     _native.ptr(ws), _native.stream_ptr(x.device)), "prim_scan")
+    return out
+
+
 def _spgemm(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, two_phase: bool = False) -> CSR:
     """``two_phase``: symbolic + numeric only (no one-pass / bitmap modes),
     the exact-memory path the OOM fallback uses."""
@@ -810,15 +833,13 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     if ws8 is not None and plan.count_rows:
         colp = None
         if plen_c is not None:
-            cbase = torch.cumsum(plen_c, 0)
-            cbase -= plen_c
+            cbase = device_scan(plen_c, torch.empty_like(plen_c), inclusive=False)
             colp = torch.empty(nnzb + 31 * ngc * B.m, dtype=torch.int32, device=dev)
             # B's values are here (no all-gather in flight): both layouts in one pass
             both = plen is not None and (B_ready is None or getattr(B_ready, "local", False))
             pbase = None
             if both:
-                pbase = torch.cumsum(plen, 0)
-                pbase -= plen
+                pbase = device_scan(plen, torch.empty_like(plen), inclusive=False)
                 Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
             # (otherwise columns only: B's values may still be in flight)
             _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val) if both else None, B.m, nwin,
@@ -840,7 +861,7 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
                                                P(ucnt), P(err), st), "spgemm_bm_count")
     uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
     uoff[:1].zero_()   # (a fill kernel: capturable, unlike a host scalar copy)
-    torch.cumsum(ucnt, 0, out=uoff[1:])
+    device_scan(ucnt, uoff[1:], inclusive=True)
     del ucnt
     out = dict(uoff=uoff, z=z, nunits=nunits, ws8=ws8 is not None)
     if not lazy:
@@ -863,8 +884,7 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     if ws8 is not None and plen is not None and Bcv is None:
         # interleaved (column, value) pairs with every window segment starting
         # on a 128-byte line: the numeric kernels take two pairs per 16-byte load
-        pbase = torch.cumsum(plen, 0)
-        pbase -= plen
+        pbase = device_scan(plen, torch.empty_like(plen), inclusive=False)
         Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
         _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, P(pbase), P(ws8),
                                                    P(Bcv), None, 1, None, Bcv.shape[0], 0, P(err), st),

@@ -52,6 +52,9 @@ if info.rows_per_bin_num.get("bitmap_fused"):
     names[5:7] = ["fused count phase", "fused look-back"]
 tot = sum(st[:5])
 print(f"n={n} d={d} plain step {plain * 1e3:.2f} ms  info={info.rows_per_bin_num}")
+if os.environ.get("SPMM_SPGEMM_BITMAP_PIPE", "1") != "0":   # pipelined count kernel: [5] ORs (+ next scan), [6] the rest
+    names[5:7] = ["count ORs", "count stage+pop"]
 for i, nm in enumerate(names):
     share = f"{100 * st[i] / tot:5.1f} %" if i < 5 and tot else ""
-    print(f"{nm:18s} {st[i] / units:10.0f} cycles/unit {share}")
+    per = units if i < 5 else max(units // 2, 1)   # (count units: two windows)
+    print(f"{nm:18s} {st[i] / per:10.0f} cycles/unit {share}")
