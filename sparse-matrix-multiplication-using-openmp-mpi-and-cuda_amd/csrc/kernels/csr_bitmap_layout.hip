@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void bm_pack_ws8(const uint32_t* __restrict__ 
 // as they are: the kernels never read a padded slot as a product), and stores
 // the base in ws8[2j + 1].y.
 __global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__ ws, const int32_t* __restrict__ col,
-                                                    const uint32_t* __restrict__ val, int64_t mb, int nwin,
+                                                    const uint32_t* __restrict__ val, int64_t mb, int nwin, int lgw,
                                                     const int64_t* __restrict__ pbase, uint4* __restrict__ ws8,
                                                     uint2* __restrict__ out, const int64_t* __restrict__ cbase,
                                                     int gc, int32_t* __restrict__ outc, int64_t cap, int64_t cap_c,
@@ -63,41 +63,39 @@ __global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__
     if (out) x[1] = (uint32_t)base;
     if (outc) x[2] = (uint32_t)cb;
   }
-  // padded start of window q (lane q): exclusive scan of the rounded lengths
+  // padded start of window q (lane q): exclusive scan of the rounded lengths;
+  // an entry of window q goes to e + dp[q] (dp = padded start - first index)
   const uint32_t wn = __shfl_down(w, 1);
   const uint32_t rl = lane < nwin ? ((wn - w + (1u << kPadLg) - 1) >> kPadLg) << kPadLg : 0u;
   const uint32_t ps = (uint32_t)bm_wave_incl((int)rl) - rl;
+  const uint32_t dp = ps - w;
   // padded start of count group g (lane g): windows [g gc, (g + 1) gc)
   const int ng = (nwin + gc - 1) / gc;
   const uint32_t g0 = (uint32_t)__shfl(w, lane * gc < nwin ? lane * gc : nwin);
   const uint32_t g1 = (uint32_t)__shfl(w, (lane + 1) * gc < nwin ? (lane + 1) * gc : nwin);
   const uint32_t rc = lane < ng ? ((g1 - g0 + (1u << kPadCLg) - 1) >> kPadCLg) << kPadCLg : 0u;
   const uint32_t pc = (uint32_t)bm_wave_incl((int)rc) - rc;
-  // entry loop with a wave-uniform trip count (every lane stays in it), so
-  // each entry fetches its window's bounds from the lanes holding them (lane
-  // shuffles) instead of selecting among eight uniform registers (1M: 0.937
-  // -> 0.871 ms per call, PERF_LOG round 4)
+  const uint32_t dc = pc - g0;
+  // entry loop with a wave-uniform trip count; an entry's window is its
+  // column >> lgw (B's rows are column-sorted), so its destination needs ONE
+  // lane shuffle per layout (round 4: seven window-bound compares and two
+  // shuffles per layout)
   const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
   const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)w, nwin);
   for (uint32_t e0 = r0; e0 < r1; e0 += 64) {
     const uint32_t e = e0 + lane;
     const bool ok = e < r1;
-    int q = 0;
-#pragma unroll
-    for (int k = 1; k < 8; ++k) q += (k < nwin && e >= (uint32_t)__builtin_amdgcn_readlane((int)w, k)) ? 1 : 0;
     const uint32_t c = ok ? (uint32_t)col[e] : 0u;
+    const int q = (int)(c >> lgw);
     if (out) {
-      const uint32_t sw = (uint32_t)__shfl((int)w, q), sp = (uint32_t)__shfl((int)ps, q);
-      const int64_t d = base + sp + (e - sw);
+      const int64_t d = base + (uint32_t)(e + (uint32_t)__shfl((int)dp, q));
       if (ok) {
         if (d < cap) out[d] = make_uint2(c, val[e]);
         else atomicOr(err, 32);   // (a layout bug, never a write out of bounds)
       }
     }
     if (outc) {
-      const int g = q / gc;
-      const uint32_t gw = (uint32_t)__shfl((int)w, g * gc), gp = (uint32_t)__shfl((int)pc, g);
-      const int64_t d = cb + gp + (e - gw);
+      const int64_t d = cb + (uint32_t)(e + (uint32_t)__shfl((int)dc, q / gc));
       if (ok) {
         if (d < cap_c) outc[d] = (int32_t)c;
         else atomicOr(err, 32);
@@ -205,14 +203,15 @@ SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin
 // cap / cap_c: entries allocated for out / outc; err bit 5 if a row would
 // not fit (a layout invariant; nothing is written out of bounds).
 SPMM_EXPORT int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb,
-                                         int nwin, const int64_t* pbase, void* ws8, void* out, const int64_t* cbase,
+                                         int nwin, int lgw, const int64_t* pbase, void* ws8, void* out, const int64_t* cbase,
                                          int gc, int32_t* outc, int64_t cap, int64_t cap_c, int32_t* err,
                                          void* stream) {
   if (mb <= 0) return 0;
-  if (nwin < 1 || nwin > 8 || gc < 1 || gc > 8 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX)
+  if (nwin < 1 || nwin > 8 || gc < 1 || gc > 8 || lgw < 1 || lgw > 30 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX)
     return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bm_pad_pairs, dim3((unsigned)((mb * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, col,
-                     (const uint32_t*)val, mb, nwin, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc, cap, cap_c, err);
+                     (const uint32_t*)val, mb, nwin, lgw, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc, cap, cap_c,
+                     err);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

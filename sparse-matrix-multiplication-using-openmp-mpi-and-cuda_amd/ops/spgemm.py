@@ -66,7 +66,7 @@ _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp,
                      C_I64, C_INT, C_INT, C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, C_I64, C_INT, C_I64, c_vp)
-_native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
+_native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
                      C_I64, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
@@ -842,7 +842,7 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
                 pbase = device_scan(plen, torch.empty_like(plen), inclusive=False)
                 Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
             # (otherwise columns only: B's values may still be in flight)
-            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val) if both else None, B.m, nwin,
+            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val) if both else None, B.m, nwin, lgw,
                                                        P(pbase) if both else None, P(ws8), P(Bcv) if both else None,
                                                        P(cbase), plan.nsub_c, P(colp),
                                                        Bcv.shape[0] if both else 0, colp.numel(), P(err), st),
@@ -886,7 +886,7 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
         # on a 128-byte line: the numeric kernels take two pairs per 16-byte load
         pbase = device_scan(plen, torch.empty_like(plen), inclusive=False)
         Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
-        _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, P(pbase), P(ws8),
+        _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, lgw, P(pbase), P(ws8),
                                                    P(Bcv), None, 1, None, Bcv.shape[0], 0, P(err), st),
                       "spgemm_bm_pad_pairs")
         del pbase
