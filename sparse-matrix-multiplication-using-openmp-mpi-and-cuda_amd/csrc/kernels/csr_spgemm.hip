@@ -1362,13 +1362,15 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
     const int64_t rt2 = it2 < nl ? list[it2] : -1;   // in flight during the atomics
     const int c0 = (int)(rt % nch) << LONG_LGW;
     for (int64_t i0 = tid;;) {
+      int ci[LONG_DL];
+      float cv[LONG_DL];
 #pragma unroll
       for (int u = 0; u < LONG_DL; ++u) {
-        if (x[u] == ~0ull) continue;
-        const int c = (int)(uint32_t)x[u] - c0;
-        atomicOr(&bits[c >> 5], 1u << (c & 31));
-        if constexpr (VALUES) atomicAdd(&vals[c], __uint_as_float((uint32_t)(x[u] >> 32)));
+        ci[u] = x[u] == ~0ull ? -1 : (int)(uint32_t)x[u] - c0;
+        cv[u] = __uint_as_float((uint32_t)(x[u] >> 32));
+        if (ci[u] >= 0) atomicOr(&bits[ci[u] >> 5], 1u << (ci[u] & 31));
       }
+      if constexpr (VALUES) spmm::lds_fadd_n(vals, ci, cv);
       i0 += LONG_DL * LONG_DNT;
       if (i0 >= n) break;
       // LONG_DL scratch loads in flight per lane before the LDS updates
@@ -1443,13 +1445,15 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
             vv[u] = 0.f;
             if constexpr (VALUES) vv[u] = ok[u] ? Bv[f[u]] : 0.f;
           }
+          int ci[LONG_DU];
+          float cv[LONG_DU];
 #pragma unroll
           for (int u = 0; u < LONG_DU; ++u) {
-            if (cc[u] < 0) continue;
-            const int c = cc[u] - c0;
-            atomicOr(&bits[c >> 5], 1u << (c & 31));
-            if constexpr (VALUES) atomicAdd(&vals[c], av[u] * vv[u]);
+            ci[u] = cc[u] < 0 ? -1 : cc[u] - c0;
+            cv[u] = av[u] * vv[u];
+            if (ci[u] >= 0) atomicOr(&bits[ci[u] >> 5], 1u << (ci[u] & 31));
           }
+          if constexpr (VALUES) spmm::lds_fadd_n(vals, ci, cv);
         }
         lr_wave_fence();   // seg / sa reads done before the next block's writes
       }
@@ -1579,7 +1583,7 @@ __global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int32_t* __rest
 #pragma unroll
         for (int u = 0; u < LR_R; ++u)
           if ((dupm >> u) & 1u)
-            atomicAdd(reinterpret_cast<float*>(&it[rank((uint32_t)x[u] - c0)]) + 1, __uint_as_float((uint32_t)(x[u] >> 32)));
+            spmm::lds_fadd(reinterpret_cast<float*>(&it[rank((uint32_t)x[u] - c0)]) + 1, __uint_as_float((uint32_t)(x[u] >> 32)));
       }
       lr_wave_fence();
       for (int i = lane; i < total; i += 64) scratch[base + i] = it[i];
