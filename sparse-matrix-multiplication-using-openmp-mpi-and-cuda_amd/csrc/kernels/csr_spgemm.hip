@@ -1235,6 +1235,135 @@ __global__ __launch_bounds__(LONG_NT) void long_route(
   }
 }
 
+// Product-parallel scatter (default; SPMM_LONG_ROUTE_PP=0 selects long_route<true, false>).
+// The workgroup's <= LONG_EPW A entries (one row) are expanded jointly: lane e of every wave
+// holds entry e's B-row length, a DPP prefix gives each entry's first product slot, and the
+// waves take 64-product windows of the concatenation round-robin, LONG_PPU windows per step
+// with all their B loads in flight.  long_route<true, false> walks one A entry per wave, so a
+// wave holding a hub entry (~14k products at R-MAT 24) runs on while its workgroup's other
+// waves sit idle, and every entry pays four dependent load latencies (A, B row pointer, B)
+// before its first product: PMC at R-MAT 24 averaged ~9 resident waves per CU and ~2000
+// cycles per 256-product step.  Same slots (per-chunk LDS cursors from long_wg_scan, one
+// cursor atomic per run of a chunk), same scratch records; only the order inside a
+// (workgroup, chunk) run changes, which long_dense and long_rank do not depend on.
+#ifndef SPMM_LONG_PPU
+#define SPMM_LONG_PPU 4
+#endif
+constexpr int LONG_PPU = SPMM_LONG_PPU;
+#ifndef SPMM_LONG_PPG
+#define SPMM_LONG_PPG 64
+#endif
+constexpr int LONG_PPG = SPMM_LONG_PPG;   // chunks per phase of a long B row
+static_assert(LONG_EPW <= 64, "one A entry per lane");
+
+__global__ __launch_bounds__(LONG_NT) void long_route_pp(
+    const int32_t* __restrict__ Aci, const float* __restrict__ Av, const int64_t* __restrict__ Brp,
+    const int32_t* __restrict__ Bci, const float* __restrict__ Bv, const int64_t* __restrict__ wg_e0,
+    const int64_t* __restrict__ wg_e1, int nch, int32_t* __restrict__ wg_hist,
+    const int32_t* __restrict__ wg_row, const int64_t* __restrict__ row_off,
+    unsigned long long* __restrict__ scratch, const int32_t* __restrict__ lidx, const uint32_t* __restrict__ btab,
+    int ph_lo, int ph_hi) {
+  constexpr int NWV = LONG_NT / 64;
+  __shared__ unsigned long long cur[LONG_MAXCH];
+  __shared__ int own_all[NWV][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#if SPMM_LONG_XCD
+  const int64_t wg = spmm::xcd_remap(blockIdx.x, gridDim.x);
+#else
+  const int64_t wg = blockIdx.x;
+#endif
+  const int64_t ro = (int64_t)wg_row[wg] * nch;
+  // [ph_lo, ph_hi): the phases of this launch.  One launch per phase puts every workgroup
+  // on the same column group, so the B rows' segments of that group (1/8 of B at R-MAT 24,
+  // ~64 MB of hub rows) stay in the MALL across rows instead of streaming from HBM per row.
+  // A launch touches the cursors of its phases' chunks only and hands them to the next
+  // launch through wg_hist (offsets inside the (row, chunk) regions).
+  const int ngrp = lidx != nullptr ? (nch + LONG_PPG - 1) / LONG_PPG : 0;
+  const int ph_end = min(ph_hi, ngrp + 1);
+  const int tlo = ph_lo == 0 ? 0 : (ph_lo - 1) * LONG_PPG;
+  const int thi = ph_lo == 0 ? nch : min(nch, (ph_end - 1) * LONG_PPG);
+  const bool handoff = !(ph_lo == 0 && ph_end == ngrp + 1);
+  for (int t = tlo + tid; t < thi; t += LONG_NT) cur[t] = (unsigned long long)(row_off[ro + t] + wg_hist[wg * nch + t]);
+  const int64_t e0 = wg_e0[wg];
+  const int ne = (int)(wg_e1[wg] - e0);
+  int blen = 0, k = -1;
+  int64_t b0 = 0;
+  float a = 0.f;
+  if (lane < ne) {
+    const int j = Aci[e0 + lane];
+    a = Av[e0 + lane];
+    b0 = Brp[j];
+    blen = (int)(Brp[j + 1] - b0);
+    if (lidx != nullptr) k = lidx[j];
+  }
+  __syncthreads();
+  int* own = own_all[w];
+  // phase 0: entries on short B rows, whole rows; phases 1..: entries on long B rows (chunk
+  // offset table), LONG_PPG chunks at a time, so a workgroup keeps ~LONG_PPG scratch runs
+  // open instead of nch and their partly written lines complete in L2 (entry-major order
+  // left ~nch partial lines per workgroup, 8 MB per XCD: 1.3x the bytes written at R-MAT 24)
+  for (int ph = ph_lo; ph < ph_end; ++ph) {
+    int64_t st = b0;
+    int len = 0;
+    if (ph == 0) {
+      len = k < 0 ? blen : 0;
+    } else if (k >= 0) {
+      const uint32_t* tk = btab + (int64_t)k * (nch + 1);
+      const int t0 = (ph - 1) * LONG_PPG;
+      const uint32_t s0 = tk[t0];
+      len = (int)(tk[min(t0 + LONG_PPG, nch)] - s0);
+      st = b0 + s0;
+    }
+    const int incl = wave_incl_scan_dpp(len);
+    const int tot = __builtin_amdgcn_readlane(incl, 63);
+    if (tot == 0) continue;   // uniform
+    const int pre = incl - len;
+    const int nwin = (tot + 63) >> 6;
+    for (int j0 = w; j0 < nwin; j0 += NWV * LONG_PPU) {
+      int c[LONG_PPU];
+      float v[LONG_PPU];
+#pragma unroll
+      for (int u = 0; u < LONG_PPU; ++u) {
+        const int qw = (j0 + u * NWV) << 6;
+        c[u] = -1;
+        v[u] = 0.f;
+        if (qw < tot) {   // uniform
+          const int o = wave_slot_owner(pre, len, qw, lane, own);
+          const int q = qw + lane;
+          const int64_t so = ((int64_t)__shfl((int)(st >> 32), o) << 32) | (uint32_t)__shfl((int)st, o);
+          const int po = __shfl(pre, o);
+          const float ao = __shfl(a, o);
+          if (q < tot) {
+            const int64_t f = so + (q - po);
+            c[u] = Bci[f];
+            v[u] = ao * Bv[f];
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LONG_PPU; ++u) {
+        // lanes of one chunk form runs (consecutive products of a sorted B row): one cursor
+        // atomic per run
+        const int t = c[u] < 0 ? -1 : c[u] >> LONG_LGW;
+        const int tp = __shfl_up(t, 1);
+        const unsigned long long heads = __ballot(lane == 0 || t != tp);
+        const unsigned long long below = heads & (~0ull >> (63 - lane));
+        const int head = 63 - __clzll((long long)below);
+        const unsigned long long after = heads & ~(~0ull >> (63 - lane));
+        const int next = after ? __ffsll((long long)after) - 1 : 64;
+        unsigned long long base = 0;
+        if (head == lane && t >= 0) base = atomicAdd(&cur[t], (unsigned long long)(next - lane));
+        base = __shfl(base, head);
+        if (t >= 0) scratch[base + (lane - head)] = ((unsigned long long)__float_as_uint(v[u]) << 32) | (uint32_t)c[u];
+      }
+    }
+  }
+  if (handoff) {
+    __syncthreads();
+    for (int t = tlo + tid; t < thi; t += LONG_NT) wg_hist[wg * nch + t] = (int32_t)(cur[t] - (unsigned long long)row_off[ro + t]);
+  }
+}
+
 // Routing plan on the device (replaces a chain of torch ops over the
 // [workgroups x chunks] histogram: widening copies, a transpose, cumsums,
 // gathers; ~10 passes over arrays of ~2e9 entries per R-MAT 24 batch).  Per
@@ -1934,6 +2063,14 @@ static size_t route_lds_pad() {
   return pad;
 }
 
+static int route_pp() {   // 0: long_route<true, false>; 1: long_route_pp, a launch per phase; 2: one launch
+  static const int on = [] {
+    const char* e = getenv("SPMM_LONG_ROUTE_PP");
+    return e ? atoi(e) : 1;
+  }();
+  return on;
+}
+
 SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const float* Av, const int64_t* Brp,
                                        const int32_t* Bci, const float* Bv, const int64_t* wg_e0,
                                        const int64_t* wg_e1, int64_t nwg, int nch, int32_t* wg_hist,
@@ -1959,6 +2096,14 @@ SPMM_EXPORT int spmm_spgemm_long_route(int scatter, const int32_t* Aci, const fl
     hipLaunchKernelGGL((long_route<true, true>), dim3((unsigned)nwg), dim3(LONG_NT), 0, s, Aci, Av, Brp, Bci, Bv, wg_e0,
                        wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, lidx, btab, nullptr, nullptr,
                        rt_mode, (uint4*)dl, dl_off);
+  else if (scatter && route_pp()) {
+    const int nph = lidx != nullptr ? (nch + LONG_PPG - 1) / LONG_PPG + 1 : 1;
+    const int per = route_pp() == 1 ? 1 : nph;   // SPMM_LONG_ROUTE_PP=2: every phase in one launch
+    for (int p0 = 0; p0 < nph; p0 += per)
+      hipLaunchKernelGGL(long_route_pp, dim3((unsigned)nwg), dim3(LONG_NT), route_lds_pad(), s, Aci, Av, Brp, Bci, Bv,
+                         wg_e0, wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, lidx, btab, p0,
+                         p0 + per);
+  }
   else if (scatter)
     hipLaunchKernelGGL((long_route<true, false>), dim3((unsigned)nwg), dim3(LONG_NT), route_lds_pad(), s, Aci, Av, Brp, Bci, Bv,
                        wg_e0, wg_e1, nch, wg_hist, wg_row, row_off, (unsigned long long*)scratch, nullptr, nullptr,

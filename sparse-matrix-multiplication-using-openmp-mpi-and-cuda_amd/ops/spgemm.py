@@ -368,7 +368,8 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         wg_row = row_of_wg.to(torch.int32)
         _native.check(lib.spmm_spgemm_long_route(1, P(A.col), P(A.val), P(B.rowptr), P(B.col), P(B.val), P(wg_e0),
                                                  P(wg_e1), nwg, nch, P(wg_hist), P(wg_row), P(rt_off), P(scratch),
-                                                 P(lidx) if direct else nil, P(btab) if direct else nil, nil, nil,
+                                                 P(lidx) if lidx is not None else nil,
+                                                 P(btab) if btab is not None else nil, nil, nil,
                                                  P(mode) if direct else nil, P(dl) if direct else nil,
                                                  P(dl_off) if direct else nil, stream), "long_route")
         del wg_hist, wg_row
