@@ -85,20 +85,15 @@ __device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t 
   return s;
 }
 
-// LDS float add: one read + compare-swap try, ds_add_f32 only for the lanes that lost it.
+// LDS float adds: one read + compare-swap try, ds_add_f32 only for the lanes that lost it.
 // gfx950 executes ds_add_f32 at ~3 LDS cycles per active lane (~193 CU-cycles per full
 // wave-instruction, any address pattern) while a ds_read_b32 + ds_cmpst_rtn_b32 pair takes ~23
 // on distinct addresses (tools/probes/lds_atomic.hip, PERF_LOG round 5).  A compare-swap LOOP
 // collapses on hot addresses (one winner per LDS round trip: R-MAT 15 -> 34 s per step), so
 // losers take the hardware-serialised add instead: never much worse than ds_add_f32 alone
-// (~210 cycles with 48 of 64 lanes losing), ~8x better when few lanes collide.
-// ``p`` must point into LDS.
-__device__ __forceinline__ void lds_fadd(float* p, float v) {
-  uint32_t* q = reinterpret_cast<uint32_t*>(p);
-  const uint32_t old = *q;
-  if (atomicCAS(q, old, __float_as_uint(__uint_as_float(old) + v)) != old) atomicAdd(p, v);
-}
-
+// (~210 cycles with 48 of 64 lanes losing), ~8x better when few lanes collide.  Used where
+// every product is an add (long_dense); the bitmap kernels' duplicate adds and long_rank's
+// keep ds_add_f32: their adding lanes mostly collide (1M step 61.4 vs 62.6 ms with the try).
 // N independent adds base[idx[u]] += v[u] (idx < 0: none): all reads, then all compare-swap
 // tries in flight together, then ds_add_f32 for the lanes that lost.
 template <int N>

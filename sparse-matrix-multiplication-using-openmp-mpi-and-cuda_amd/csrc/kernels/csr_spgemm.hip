@@ -1712,7 +1712,7 @@ __global__ __launch_bounds__(LR_WAVES * 64) void long_rank(const int32_t* __rest
 #pragma unroll
         for (int u = 0; u < LR_R; ++u)
           if ((dupm >> u) & 1u)
-            spmm::lds_fadd(reinterpret_cast<float*>(&it[rank((uint32_t)x[u] - c0)]) + 1, __uint_as_float((uint32_t)(x[u] >> 32)));
+            atomicAdd(reinterpret_cast<float*>(&it[rank((uint32_t)x[u] - c0)]) + 1, __uint_as_float((uint32_t)(x[u] >> 32)));
       }
       lr_wave_fence();
       for (int i = lane; i < total; i += 64) scratch[base + i] = it[i];

@@ -766,13 +766,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
               if ((dupm >> d) & 1u) {
                 unsigned long long* it = &items[rank(c[d])];
                 tri |= (atomicOr(reinterpret_cast<uint32_t*>(it), kDupBit) & kDupBit) != 0u;
-                spmm::lds_fadd(reinterpret_cast<float*>(it) + 1, v[d]);
+                atomicAdd(reinterpret_cast<float*>(it) + 1, v[d]);
               }
             if (tri) sfix = 1;
           } else {
 #pragma unroll
             for (int d = 0; d < RR; ++d)
-              if ((dupm >> d) & 1u) spmm::lds_fadd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+              if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
           }
         }
       } else {
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
               } else {
                 cw[0] = (uint32_t)(c[d] + clo);
               }
-              spmm::lds_fadd(reinterpret_cast<float*>(&items[rr]) + 1, v[d]);
+              atomicAdd(reinterpret_cast<float*>(&items[rr]) + 1, v[d]);
             }
           }
         }
@@ -1245,13 +1245,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
             if ((dupm >> d) & 1u) {
               unsigned long long* it = &items[rank(c[d])];
               tri |= (atomicOr(reinterpret_cast<uint32_t*>(it), kDupBit) & kDupBit) != 0u;
-              spmm::lds_fadd(reinterpret_cast<float*>(it) + 1, v[d]);
+              atomicAdd(reinterpret_cast<float*>(it) + 1, v[d]);
             }
           if (tri) sfix = 1;
         } else {
 #pragma unroll
           for (int d = 0; d < RR; ++d)
-            if ((dupm >> d) & 1u) spmm::lds_fadd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+            if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
         }
       }
       __syncthreads();
@@ -1707,7 +1707,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
           __syncthreads();
 #pragma unroll
           for (int d = 0; d < RR; ++d)
-            if ((dupm >> d) & 1u) spmm::lds_fadd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
+            if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
         }
         lim = total;
         if (want != total || off < 0 || off + total > p.cap) {   // never write outside the unit or C
