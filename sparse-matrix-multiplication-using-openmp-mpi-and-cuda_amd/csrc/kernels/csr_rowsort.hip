@@ -1,0 +1,191 @@
+// Device re-sort of listed CSR rows (the SpGEMM rows whose LDS table could not keep
+// its output column-sorted, flag 1): one engine for the Python front end
+// (ops/csr.py sort_rows) and the native chain (csrc/runtime/csr_engine.cpp), which
+// re-sorted them on the host one row at a time (round 4).  The reference keeps its
+// output ordered through std::map on the host (sparse_matrix_mult.cu:287-327).
+//
+// Entries are packed as int64 keys (column << 32 | value bits): a row's columns are
+// distinct, so sorting the keys sorts by column and carries the value along.
+//   rs_pack      one wave per listed row: keys into a compact buffer at toff[i]
+//   rs_sort_wave rows of <= 64 entries: bitonic across the lanes of one wave
+//   rs_sort_lds  rows of 65..kRsLds entries: one 1024-thread workgroup, bitonic in LDS
+//   (longer)     every listed row at once through the in-tree radix sort (prim.hip)
+//                on (row index << 31 | column) keys
+//   rs_unpack    keys back into the row
+#include "common.hpp"
+
+extern "C" {
+int spmm_prim_scan(const void* in, int in_bytes, int64_t n, int64_t* out, int inclusive, void* ws, void* stream);
+size_t spmm_prim_scan_ws(int64_t n);
+size_t spmm_prim_sort_ws(int64_t n);
+int spmm_prim_sort_pairs_u64(uint64_t* keys, uint64_t* vals, int64_t n, int bits, void* ws, void* stream);
+}
+
+namespace {
+
+constexpr int kRsLds = 16384;   // 128 KB of LDS
+constexpr int kRsNt = 1024;
+
+__global__ __launch_bounds__(256) void rs_lens(const int64_t* __restrict__ rp, const int64_t* __restrict__ rows,
+                                               int64_t nrows, int64_t* __restrict__ len) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < nrows) len[i] = rp[rows[i] + 1] - rp[rows[i]];
+}
+
+// radix: key = (i << 31) | column, value = value bits; otherwise key = column << 32 | bits
+template <bool RADIX>
+__global__ __launch_bounds__(256) void rs_pack(const int64_t* __restrict__ rp, const int64_t* __restrict__ rows,
+                                               int64_t nrows, const int64_t* __restrict__ toff,
+                                               const int32_t* __restrict__ ci, const uint32_t* __restrict__ v,
+                                               uint64_t* __restrict__ key, uint64_t* __restrict__ val) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nrows) return;
+  const int64_t s = rp[rows[i]], n = rp[rows[i] + 1] - s, d = toff[i];
+  for (int64_t e = lane; e < n; e += 64) {
+    const uint64_t c = (uint32_t)ci[s + e];
+    if (RADIX) {
+      key[d + e] = ((uint64_t)i << 31) | c;
+      val[d + e] = v[s + e];
+    } else {
+      key[d + e] = (c << 32) | v[s + e];
+    }
+  }
+}
+
+template <bool RADIX>
+__global__ __launch_bounds__(256) void rs_unpack(const int64_t* __restrict__ rp, const int64_t* __restrict__ rows,
+                                                 int64_t nrows, const int64_t* __restrict__ toff,
+                                                 const uint64_t* __restrict__ key, const uint64_t* __restrict__ val,
+                                                 int32_t* __restrict__ ci, uint32_t* __restrict__ v) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nrows) return;
+  const int64_t s = rp[rows[i]], n = rp[rows[i] + 1] - s, d = toff[i];
+  for (int64_t e = lane; e < n; e += 64) {
+    const uint64_t k = key[d + e];
+    if (RADIX) {
+      ci[s + e] = (int32_t)(k & 0x7fffffffu);
+      v[s + e] = (uint32_t)val[d + e];
+    } else {
+      ci[s + e] = (int32_t)(k >> 32);
+      v[s + e] = (uint32_t)k;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int mask) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, mask), hi = (uint32_t)__shfl_xor((int)(x >> 32), mask);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void rs_sort_wave(const int64_t* __restrict__ toff, int64_t nrows,
+                                                    uint64_t* __restrict__ key) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nrows) return;   // wave-uniform
+  const int64_t s = toff[i];
+  const int64_t len = toff[i + 1] - s;
+  if (len < 2 || len > 64) return;
+  uint64_t x = lane < len ? key[s + lane] : ~0ull;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint64_t o = shfl_xor_u64(x, j);
+      const bool lower = (lane & j) == 0, up = (lane & k) == 0;
+      x = (lower == up) ? (o < x ? o : x) : (o > x ? o : x);
+    }
+  }
+  if (lane < len) key[s + lane] = x;
+}
+
+__global__ __launch_bounds__(kRsNt) void rs_sort_lds(const int64_t* __restrict__ toff, uint64_t* __restrict__ key) {
+  __shared__ uint64_t sh[kRsLds];
+  const int tid = threadIdx.x;
+  const int64_t s = toff[blockIdx.x];
+  const int len = (int)(toff[blockIdx.x + 1] - s);
+  if (len <= 64 || len > kRsLds) return;   // (workgroup-uniform)
+  int n = 128;
+  while (n < len) n <<= 1;
+  for (int i = tid; i < n; i += kRsNt) sh[i] = i < len ? key[s + i] : ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < n; i += kRsNt) {
+        const int p = i ^ j;
+        if (p > i) {
+          const uint64_t a = sh[i], b = sh[p];
+          if ((a > b) == ((i & k) == 0)) {
+            sh[i] = b;
+            sh[p] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < len; i += kRsNt) key[s + i] = sh[i];
+}
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace
+
+// Workspace bytes of spmm_csr_sort_rows for nrows listed rows holding total entries.
+SPMM_EXPORT size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen) {
+  size_t b = align256((size_t)(nrows + 1) * 8) * 2 + align256(spmm_prim_scan_ws(nrows + 1)) +
+             align256((size_t)total * 8);
+  if (maxlen > kRsLds) b += align256((size_t)total * 8) + align256(spmm_prim_sort_ws(total));
+  return b;
+}
+
+// Sort the entries of rows[0..nrows) (int64 row ids, device) of the CSR (rp, ci, v) by column,
+// in place.  total = sum of their lengths, maxlen = the longest (host values: the caller
+// sizes the workspace with spmm_csr_sort_rows_ws from them).  Launches only.
+SPMM_EXPORT int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64_t nrows, int64_t total, int64_t maxlen,
+                                   int32_t* ci, float* v, void* ws, void* stream) {
+  if (nrows <= 0 || total <= 0 || maxlen < 2) return 0;
+  if (nrows >= ((int64_t)1 << 32) || (nrows + 3) / 4 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  char* p = (char*)ws;
+  int64_t* len = (int64_t*)p;
+  p += align256((size_t)(nrows + 1) * 8);
+  int64_t* toff = (int64_t*)p;
+  p += align256((size_t)(nrows + 1) * 8);
+  char* scan_ws = p;
+  p += align256(spmm_prim_scan_ws(nrows + 1));
+  uint64_t* key = (uint64_t*)p;
+  p += align256((size_t)total * 8);
+  const bool radix = maxlen > kRsLds;
+  hipLaunchKernelGGL(rs_lens, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, rp, rows, nrows, len);
+  SPMM_LAUNCH_CHECK();
+  (void)hipMemsetAsync(len + nrows, 0, 8, s);
+  int rc = spmm_prim_scan(len, 8, nrows + 1, toff, 0, scan_ws, s);   // exclusive: toff[nrows] = total
+  if (rc) return rc;
+  const dim3 gw((unsigned)((nrows + 3) / 4));
+  if (radix) {
+    uint64_t* val = (uint64_t*)p;
+    p += align256((size_t)total * 8);
+    hipLaunchKernelGGL(rs_pack<true>, gw, dim3(256), 0, s, rp, rows, nrows, toff, ci, (const uint32_t*)v, key, val);
+    SPMM_LAUNCH_CHECK();
+    int bits = 31;
+    while (bits < 63 && ((int64_t)1 << (bits - 31)) < nrows) ++bits;
+    rc = spmm_prim_sort_pairs_u64(key, val, total, bits, p, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(rs_unpack<true>, gw, dim3(256), 0, s, rp, rows, nrows, toff, key, val, ci, (uint32_t*)v);
+  } else {
+    hipLaunchKernelGGL(rs_pack<false>, gw, dim3(256), 0, s, rp, rows, nrows, toff, ci, (const uint32_t*)v, key,
+                       nullptr);
+    SPMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rs_sort_wave, gw, dim3(256), 0, s, toff, nrows, key);
+    SPMM_LAUNCH_CHECK();
+    if (maxlen > 64) {
+      hipLaunchKernelGGL(rs_sort_lds, dim3((unsigned)nrows), dim3(kRsNt), 0, s, toff, key);
+      SPMM_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(rs_unpack<false>, gw, dim3(256), 0, s, rp, rows, nrows, toff, key, nullptr, ci, (uint32_t*)v);
+  }
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}

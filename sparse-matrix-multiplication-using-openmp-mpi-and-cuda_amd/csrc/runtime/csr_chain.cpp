@@ -421,6 +421,7 @@ int run_mtx(const MtxOptions& o, int rank, int world) {
       << "\", \"ranks\": " << world << ", \"n_files\": " << paths.size() << ", \"flops\": " << fl_all
       << ", \"gpu_products\": " << (es.bitmap + es.binned) << ", \"gpu_bitmap_products\": " << es.bitmap
       << ", \"gpu_binned_products\": " << es.binned << ", \"gpu_long_rows\": " << es.long_rows
+      << ", \"host_resorted_rows\": " << es.resorted_rows << ", \"device_sorted_rows\": " << es.device_sorted_rows
       << ", \"cpu_products\": " << cpu_products << ", \"t_chain_s\": " << (t1 - t0)
       << ", \"t_write_s\": " << (t2 - t1) << "}\n";
   }

@@ -36,6 +36,10 @@ int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_
 int spmm_spgemm_long_place(const int64_t* src, const int64_t* dst, const int64_t* cnt, int64_t nrt,
                            const void* scratch, int32_t* Cci, float* Cv, void* stream);
 int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch);
+// csr_rowsort.hip
+size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen);
+int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64_t nrows, int64_t total, int64_t maxlen,
+                       int32_t* ci, float* v, void* ws, void* stream);
 // csr_spgemm_bitmap.hip
 int spmm_spgemm_bm_config(int cfg, int* lgw, int* nsub_count, int* pcap_fast, int* rounds_fast, int* reload_rows);
 int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin, uint32_t* ws,
@@ -348,24 +352,22 @@ DCsr binned_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
   std::vector<int32_t> bad;
   for (int64_t r = 0; r < A.m; ++r)
     if (num.second[r] & 1) bad.push_back((int32_t)r);
-  for (int32_t r : bad) {
-    const int64_t a = Crp_h[r], n = Crp_h[r + 1] - a;
-    std::vector<int32_t> c = down(C.ci.get() + a, n, s);
-    std::vector<float> v = down(C.v.get() + a, n, s);
-    std::vector<int64_t> idx(n);
-    std::iota(idx.begin(), idx.end(), 0);
-    std::sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return c[x] < c[y]; });
-    std::vector<int32_t> c2(n);
-    std::vector<float> v2(n);
-    for (int64_t i = 0; i < n; ++i) {
-      c2[i] = c[idx[i]];
-      v2[i] = v[idx[i]];
+  // ... on the device (csr_rowsort.hip, the kernels ops/csr.py sort_rows uses): the row
+  // lengths are host values here, so no read-back at all
+  if (!bad.empty()) {
+    std::vector<int64_t> rows_h(bad.begin(), bad.end());
+    int64_t total = 0, maxlen = 0;
+    for (int32_t r : bad) {
+      const int64_t n = Crp_h[r + 1] - Crp_h[r];
+      total += n;
+      maxlen = std::max(maxlen, n);
     }
-    A4_HIP(hipMemcpyAsync(C.ci.get() + a, c2.data(), n * 4, hipMemcpyHostToDevice, s));
-    A4_HIP(hipMemcpyAsync(C.v.get() + a, v2.data(), n * 4, hipMemcpyHostToDevice, s));
-    A4_HIP(hipStreamSynchronize(s));
+    DevBuf<int64_t> rows_d = up(rows_h, s);
+    DevBuf<uint8_t> ws(std::max<size_t>(spmm_csr_sort_rows_ws((int64_t)rows_h.size(), total, maxlen), 1), s);
+    A4_HIP((hipError_t)spmm_csr_sort_rows(C.rp.get(), rows_d.get(), (int64_t)rows_h.size(), total, maxlen, C.ci.get(),
+                                          C.v.get(), ws.get(), s));
+    st->device_sorted_rows += (int64_t)bad.size();
   }
-  st->resorted_rows += (int64_t)bad.size();
   return C;
 }
 

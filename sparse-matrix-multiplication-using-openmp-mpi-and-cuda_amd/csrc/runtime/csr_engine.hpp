@@ -37,7 +37,8 @@ struct DCsr {
 };
 
 struct EngineStats {
-  int64_t bitmap = 0, binned = 0, long_rows = 0, resorted_rows = 0;
+  int64_t bitmap = 0, binned = 0, long_rows = 0, resorted_rows = 0;   // resorted_rows: on the host (none since round 5)
+  int64_t device_sorted_rows = 0;   // flagged rows re-sorted by csr_rowsort.hip
 };
 
 DCsr dcsr_upload(const Csr& H, hipStream_t s);

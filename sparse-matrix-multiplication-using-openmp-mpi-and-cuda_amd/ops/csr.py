@@ -168,8 +168,29 @@ def from_torch(t: torch.Tensor) -> CSR:
                t.values())
 
 
-def sort_rows(C: CSR, rows: Optional[torch.Tensor] = None) -> CSR:
-    """Re-sort columns inside rows (all rows, or only ``rows``)."""
+_native.register_hip("spmm_csr_sort_rows_ws", C.c_int64, C.c_int64, C.c_int64, restype=C.c_size_t)
+_native.register_hip("spmm_csr_sort_rows", c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp, c_vp, c_vp, c_vp)
+
+
+def sort_rows(C: CSR, rows: Optional[torch.Tensor] = None, inplace: bool = False) -> CSR:
+    """Re-sort columns inside rows (all rows, or only ``rows``).  On the GPU
+    the listed rows are sorted by csr_rowsort.hip (bitonic per wave / LDS
+    workgroup, the in-tree radix sort for rows beyond 16384 entries): one
+    read-back of their total and longest length, no per-row host work.
+    ``inplace``: sort C's own arrays (the SpGEMM's fresh output)."""
+    if (rows is not None and rows.numel() and C.col.is_cuda and C.col.dtype == torch.int32
+            and C.val.dtype == torch.float32 and rows.numel() < C.m):
+        r = rows.long().contiguous()
+        lens = C.rowptr[r + 1] - C.rowptr[r]
+        total, maxlen = torch.stack([lens.sum(), lens.max()]).tolist()
+        col, val = (C.col, C.val) if inplace else (C.col.clone(), C.val.clone())
+        lib = _native.hip()
+        ws = torch.empty(max(int(lib.spmm_csr_sort_rows_ws(r.numel(), total, maxlen)), 1), dtype=torch.uint8,
+                         device=C.col.device)
+        _native.check(lib.spmm_csr_sort_rows(_native.ptr(C.rowptr), _native.ptr(r), r.numel(), total, maxlen,
+                                             _native.ptr(col), _native.ptr(val), _native.ptr(ws),
+                                             _native.stream_ptr(C.col.device)), "csr_sort_rows")
+        return CSR(C.m, C.n, C.rowptr, col, val)
     if rows is None or rows.numel() == C.m:
         r = C.row_ids()
         code = r * C.n + C.col.long()

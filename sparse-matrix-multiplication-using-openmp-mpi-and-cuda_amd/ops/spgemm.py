@@ -1174,7 +1174,7 @@ def _finish(C_: CSR, flags: torch.Tensor, info: SpgemmInfo, counts=None) -> CSR:
     bad = ((flags & 1) != 0).nonzero().flatten()
     if bad.numel():
         info.resorted_rows = int(bad.numel())
-        C_ = sort_rows(C_, bad)
+        C_ = sort_rows(C_, bad, inplace=True)
     return C_
 
 

@@ -377,6 +377,7 @@ def test_a4_mtx_gpu_skewed_chain_has_no_cpu_fallback(tmp_path, a4_bin, p):
     m = json.load(open(met))
     assert m["device_resident"] and m["cpu_products"] == 0 and m["gpu_products"] == 2, m
     assert m["gpu_binned_products"] >= 1 and m["gpu_long_rows"] >= 1, m
+    assert m["host_resorted_rows"] == 0, m   # flagged rows are re-sorted on the device (csr_rowsort.hip)
     G, C = mtx.read_mtx(g), mtx.read_mtx(c)
     assert G.nnz == C.nnz and bool((G.rowptr == C.rowptr).all()) and bool((G.col == C.col).all())
     np.testing.assert_allclose(G.val.numpy(), C.val.numpy(), rtol=1e-4, atol=1e-5)

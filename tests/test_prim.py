@@ -79,3 +79,35 @@ def test_bsr_symbolic_native_matches_torch(shape):
     assert torch.equal(got.keys.cpu(), ref.keys)
     assert torch.equal(got.tile_ptr.cpu(), ref.tile_ptr)
     assert torch.equal(got.pa.cpu(), ref.pa) and torch.equal(got.pb.cpu(), ref.pb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("long_rows", [False, True])
+def test_csr_sort_rows_device(long_rows):
+    """ops.csr.sort_rows on listed rows (csr_rowsort.hip: wave / LDS bitonic, radix beyond
+    16384 entries) equals a per-row torch sort; unlisted rows stay as they were."""
+    from spmm_amd.ops.csr import CSR, sort_rows
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(5 + long_rows)
+    lens = [0, 1, 2, 63, 64, 65, 100, 2047, 2048, 2049, 16384, 5, 700]
+    if long_rows:
+        lens += [16385, 40000]
+    m, n = len(lens), 1 << 20
+    cols, vals = [], []
+    for ln in lens:
+        cols.append(torch.randperm(n, generator=g)[:ln].to(torch.int32))   # distinct, unsorted
+        vals.append(torch.randn(ln, generator=g))
+    rowptr = torch.zeros(m + 1, dtype=torch.int64)
+    rowptr[1:] = torch.cumsum(torch.tensor(lens), 0)
+    Cm = CSR(m, n, rowptr.to(dev), torch.cat(cols).to(dev), torch.cat(vals).to(dev))
+    rows = torch.tensor([i for i in range(m) if i % 4 != 3], dtype=torch.int64, device=dev)
+    out = sort_rows(Cm, rows)
+    for i in range(m):
+        s, e = int(rowptr[i]), int(rowptr[i + 1])
+        if i % 4 == 3:
+            assert torch.equal(out.col[s:e], Cm.col[s:e])
+            continue
+        c, p = torch.sort(Cm.col[s:e])
+        assert torch.equal(out.col[s:e], c), i
+        assert torch.equal(out.val[s:e], Cm.val[s:e][p]), i
