@@ -382,6 +382,7 @@ int run_mtx(const MtxOptions& o, int rank, int world) {
   int64_t row0 = 0, cpu_products = 0;
   int64_t flops = 0;
   EngineStats es;
+  std::vector<double> t_products;   // device products: wall seconds each (upload / gather excluded)
   const double t0 = now_s();
   Csr P = read_rowblock(paths[0], rank, world, o.threads, &row0);
   DCsr Pd;
@@ -396,7 +397,11 @@ int run_mtx(const MtxOptions& o, int rank, int world) {
       A4_CHECK(B.m == Pd.n, paths[i] + ": " + std::to_string(B.m) + " rows, the product so far has " +
                                std::to_string(Pd.n) + " columns");
       int64_t products = 0;
+      A4_HIP(hipStreamSynchronize(s));   // per-product wall time: operands resident, C complete
+      const double tp = now_s();
       DCsr C = dev_spgemm(Pd, B, s, &es, &products);
+      A4_HIP(hipStreamSynchronize(s));
+      t_products.push_back(now_s() - tp);
       flops += 2 * products;
       Pd = std::move(C);
     } else {
@@ -422,7 +427,9 @@ int run_mtx(const MtxOptions& o, int rank, int world) {
       << ", \"gpu_products\": " << (es.bitmap + es.binned) << ", \"gpu_bitmap_products\": " << es.bitmap
       << ", \"gpu_binned_products\": " << es.binned << ", \"gpu_long_rows\": " << es.long_rows
       << ", \"host_resorted_rows\": " << es.resorted_rows << ", \"device_sorted_rows\": " << es.device_sorted_rows
-      << ", \"cpu_products\": " << cpu_products << ", \"t_chain_s\": " << (t1 - t0)
+      << ", \"cpu_products\": " << cpu_products << ", \"t_products_s\": [";
+    for (size_t i = 0; i < t_products.size(); ++i) m << (i ? ", " : "") << t_products[i];
+    m << "], \"t_chain_s\": " << (t1 - t0)
       << ", \"t_write_s\": " << (t2 - t1) << "}\n";
   }
   Pd = DCsr();

@@ -6,6 +6,7 @@
 // no product falls back to the CPU.  Per-row host arrays (product counts,
 // flags, the long rows' chunk counts) are the only device->host traffic.
 #include "csr_engine.hpp"
+#include "../kernels/bitmap_plan.hpp"
 
 #include <algorithm>
 #include <cstring>
@@ -40,16 +41,18 @@ int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch);
 size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen);
 int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64_t nrows, int64_t total, int64_t maxlen,
                        int32_t* ci, float* v, void* ws, void* stream);
-// csr_spgemm_bitmap.hip
-int spmm_spgemm_bm_config(int cfg, int* lgw, int* nsub_count, int* pcap_fast, int* rounds_fast, int* reload_rows);
-int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin, uint32_t* ws,
-                          void* stream);
-int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const uint32_t* ws, const int32_t* Bci,
-                         int64_t m, int nwin, int lg, int32_t* ucnt, int32_t* err, void* stream);
-int spmm_spgemm_bm_numeric(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av, const uint32_t* ws,
-                           const int32_t* Bci, const float* Bv, int64_t m, int nwin, int lg, const int64_t* uoff,
-                           int64_t cap, int32_t* Cci, float* Cv, int32_t* ovf, uint32_t* novf, int64_t ovf_cap,
-                           int32_t* err, int det, const void* ws8, const void* bcv_padded, void* stream);
+// csr_bitmap_plan.hip (SpmmBmOpts / SpmmBmPlan: bitmap_plan.hpp)
+int spmm_spgemm_bm_env_opts(SpmmBmOpts* o);
+int spmm_spgemm_bm_choose(const SpmmBmOpts* o, int64_t m, int64_t annz, int64_t bn, int64_t bnnz, int64_t tot,
+                          int64_t nonempty, int64_t pmax, int64_t amax);
+int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t annz, int64_t mb, int64_t bn, int64_t bnnz,
+                             int64_t tot, int64_t nonempty, int64_t amax, double mean_seg, SpmmBmPlan* p);
+int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const int64_t* Brp,
+                         const int32_t* Bci, const float* Bv, void* ws, int64_t* uoff, int32_t* z, int* pairs_built,
+                         void* stream);
+int spmm_spgemm_bm_back(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const float* Av,
+                        const int32_t* Bci, const float* Bv, int pairs_built, void* ws, const int64_t* uoff,
+                        int32_t* z, int64_t cap, int32_t* Cci, float* Cv, void* stream);
 }
 
 namespace a4 {
@@ -110,63 +113,48 @@ DCsr empty_product(const DCsr& A, const DCsr& B, hipStream_t s) {
   return C;
 }
 
-// ---- bitmap-rank path (ops/spgemm.py onepass_bitmap, per-unit kernels) ------
+// ---- bitmap-rank path: the shared native planner (csr_bitmap_plan.hip), the same
+// decisions, layouts and kernels as ops/spgemm.py onepass_bitmap (eager flow) ------------
 bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s, DCsr* out) {
-  if (B.nnz >= (int64_t(1) << 31) || B.n >= (int64_t(1) << 30) || A.nnz >= (int64_t(1) << 31)) return false;
-  const double mean = (double)pl.tot / (double)std::max<int64_t>(pl.nz, 1);
-  if (pl.mx > 4 * mean || pl.nz < A.m / 2) return false;   // skewed rows: the binned path's job
-  int cfg = -1, lgw = 0, nsub = 0, pcap = 0, rounds = 0, reload_rows = 0;
-  for (int c : {0, 2, 1}) {   // widest window whose mean products per window fit 70 % of the fast capacity
-    A4_HIP((hipError_t)spmm_spgemm_bm_config(c, &lgw, &nsub, &pcap, &rounds, &reload_rows));
-    const double W = (double)(int64_t(1) << lgw);
-    if (mean * std::min(W, (double)B.n) / std::max<double>((double)B.n, 1) <= 0.7 * pcap) {
-      cfg = c;
-      break;
-    }
-  }
-  if (cfg < 0) return false;
-  A4_HIP((hipError_t)spmm_spgemm_bm_config(cfg, &lgw, &nsub, &pcap, &rounds, &reload_rows));
-  if (pl.amax > reload_rows) return false;
-  const int nwin = (int)std::max<int64_t>(1, (B.n + (int64_t(1) << lgw) - 1) >> lgw);
-  const int64_t nunits = A.m * nwin;
-  if (nunits >= (int64_t(1) << 31)) return false;
+  SpmmBmOpts o{};
+  spmm_spgemm_bm_env_opts(&o);
+  if (spmm_spgemm_bm_choose(&o, A.m, A.nnz, B.n, B.nnz, pl.tot, pl.nz, pl.mx, pl.amax) < 0) return false;
   const double seg = (double)pl.tot / (double)std::max<int64_t>(A.nnz, 1);   // B-segment length per A entry
-  const int lg_count = group_log2(seg * std::min(nsub, nwin) / nwin);
-  const int lg_num = seg / nwin < 48 ? 4 : (seg / nwin < 96 ? 5 : 6);
-  DevBuf<uint32_t> ws((size_t)B.m * (nwin + 1), s);
-  DevBuf<int32_t> ucnt((size_t)nunits, s), err(4, s);
-  DevBuf<int64_t> uoff((size_t)nunits + 1, s);
-  DevBuf<uint8_t> scan_ws(std::max<size_t>(spmm_prim_scan_ws(nunits), 1), s);
-  A4_HIP(hipMemsetAsync(err.get(), 0, 16, s));
-  A4_HIP(hipMemsetAsync(uoff.get(), 0, 8, s));
-  A4_HIP((hipError_t)spmm_spgemm_bm_splits(B.rp.get(), B.ci.get(), B.m, lgw, nwin, ws.get(), s));
-  A4_HIP((hipError_t)spmm_spgemm_bm_count(cfg, A.rp.get(), A.ci.get(), ws.get(), B.ci.get(), A.m, nwin, lg_count,
-                                          ucnt.get(), err.get(), s));
-  A4_HIP((hipError_t)spmm_prim_scan(ucnt.get(), 4, nunits, uoff.get() + 1, 1, scan_ws.get(), s));
-  const std::vector<int64_t> nnzv = down(uoff.get() + nunits, 1, s);   // the one sizing read-back
-  const int64_t nnz = nnzv[0];
-  if (down(err.get(), 1, s)[0] != 0) return false;
-  const int64_t ovf_cap = std::min<int64_t>(nunits, 1 << 20);
-  DCsr C;
-  C.m = A.m;
-  C.n = B.n;
-  C.nnz = nnz;
-  C.ci = DevBuf<int32_t>((size_t)std::max<int64_t>(nnz, 1), s);
-  C.v = DevBuf<float>((size_t)std::max<int64_t>(nnz, 1), s);
-  DevBuf<int32_t> ovf((size_t)ovf_cap, s);
-  A4_HIP((hipError_t)spmm_spgemm_bm_numeric(cfg, A.rp.get(), A.ci.get(), A.v.get(), ws.get(), B.ci.get(), B.v.get(),
-                                            A.m, nwin, lg_num, uoff.get(), nnz, C.ci.get(), C.v.get(), ovf.get(),
-                                            (uint32_t*)(err.get() + 1), ovf_cap, err.get(), 0, nullptr, nullptr, s));
-  const int e = down(err.get(), 1, s)[0];
-  A4_CHECK((e & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
-  if (e & 5) return false;   // a unit beyond the reload kernel's budget: the binned path redoes the product
-  // row pointer: every nwin-th unit offset
-  const std::vector<int64_t> uo = down(uoff.get(), nunits + 1, s);
-  std::vector<int64_t> rp(A.m + 1);
-  for (int64_t i = 0; i <= A.m; ++i) rp[i] = uo[i * nwin];
-  C.rp = up(rp, s);
-  *out = std::move(C);
-  return true;
+  for (int use_ws8 = 1; use_ws8 >= 0; --use_ws8) {
+    o.use_ws8 = use_ws8;
+    SpmmBmPlan p{};
+    if (spmm_spgemm_bm_make_plan(&o, A.m, A.nnz, B.m, B.n, B.nnz, pl.tot, pl.nz, pl.amax, seg, &p)) return false;
+    DevBuf<uint8_t> ws((size_t)std::max<int64_t>(p.ws_bytes, 1), s);
+    DevBuf<int32_t> z(2, s);
+    DevBuf<int64_t> uoff((size_t)p.nunits + 1, s);
+    int built = 0;
+    A4_HIP((hipError_t)spmm_spgemm_bm_front(&p, A.rp.get(), A.ci.get(), B.rp.get(), B.ci.get(), B.v.get(), ws.get(),
+                                            uoff.get(), z.get(), &built, s));
+    const int64_t nnz = down(uoff.get() + p.nunits, 1, s)[0];   // the one sizing read-back
+    const int e0 = down(z.get(), 1, s)[0];
+    A4_CHECK((e0 & 32) == 0, "spgemm bitmap: padded B layout overflow");
+    if (e0 & 8) continue;   // a window segment of >= 65536 entries: per-unit kernels
+    if (e0 != 0) return false;
+    A4_HIP(hipMemsetAsync(z.get(), 0, 4, s));
+    DCsr C;
+    C.m = A.m;
+    C.n = B.n;
+    C.nnz = nnz;
+    C.ci = DevBuf<int32_t>((size_t)std::max<int64_t>(nnz, 1), s);
+    C.v = DevBuf<float>((size_t)std::max<int64_t>(nnz, 1), s);
+    A4_HIP((hipError_t)spmm_spgemm_bm_back(&p, A.rp.get(), A.ci.get(), A.v.get(), B.ci.get(), B.v.get(), built,
+                                           ws.get(), uoff.get(), z.get(), nnz, C.ci.get(), C.v.get(), s));
+    const int e = down(z.get(), 1, s)[0];
+    A4_CHECK((e & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
+    if (e & 5) return false;   // a unit beyond the reload kernel's budget: the binned path redoes the product
+    // row pointer: every nwin-th unit offset, gathered on the device
+    C.rp = DevBuf<int64_t>((size_t)A.m + 1, s);
+    A4_HIP(hipMemcpy2DAsync(C.rp.get(), sizeof(int64_t), uoff.get(), sizeof(int64_t) * p.nwin, sizeof(int64_t),
+                            (size_t)A.m + 1, hipMemcpyDeviceToDevice, s));
+    *out = std::move(C);
+    return true;
+  }
+  return false;
 }
 
 // ---- long rows (ops/spgemm.py _long_rows, routed mode) -----------------------

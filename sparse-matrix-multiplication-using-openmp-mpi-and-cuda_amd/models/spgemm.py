@@ -202,8 +202,8 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
                 if rec is not None:
                     rec[2] = GATHER_STATS.mark(dev)   # the compute stream may read the payload from here
                 # (no interleaved copy here: the bitmap kernels read B through its
-                # padded pair layout, built from col / val by the SpGEMM itself;
-                # ops.spgemm.interleaved makes the plain pairs on demand)
+                # padded pair layout, built from col / val by the SpGEMM itself,
+                # csr_bitmap_plan.hip)
                 unpack(None, g, col, val, None)
                 B = CSR(m, panel.n, rowptr, col, val)
                 got["B"] = B

@@ -683,237 +683,126 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
     return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info, (f4, f1))
 
 
-_BM_CFGS = {}
-BM_FILL = 0.7              # mean products per window <= BM_FILL * fast capacity
+class _BmOpts(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmOpts
+    _fields_ = [(n, C.c_int32) for n in ("mode", "cfg", "rows_mode", "count_windows", "det", "pad", "cv", "pipe",
+                                         "use_ws8")]
 
 
-def interleaved(B: CSR) -> torch.Tensor:
-    """B as [nnz, 2] int32 (column, value bits) pairs: the operand of the
-    row-major bitmap numeric kernel when B's padded pair layout is not built
-    (one native 16-byte-vector copy; ``B._bcv`` if a caller attached one)."""
-    cv = getattr(B, "_bcv", None)
-    if cv is not None and cv.shape[0] == B.nnz:
-        return cv
-    cv = torch.empty((B.nnz, 2), dtype=torch.int32, device=B.device)
-    _native.check(_native.hip().spmm_spgemm_bm_interleave(_native.ptr(B.col), _native.ptr(B.val), B.nnz,
-                                                           _native.ptr(cv), _native.stream_ptr(B.device)),
-                  "spgemm_bm_interleave")
-    return cv
+class _BmPlan(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmPlan
+    _fields_ = ([(n, C.c_int32) for n in ("cfg", "lgw", "nwin", "nsub", "lg_count", "lg_c", "nsub_c", "lg_num",
+                                          "count_rows", "rows", "det", "pipe", "ws8", "pad_num", "pad_cnt",
+                                          "plain_cv")]
+                + [(n, C.c_int64) for n in ("m", "annz", "mb", "nnzb", "tot", "nunits", "ngc", "cap_bcv", "cap_colp",
+                                            "ovf_cap", "o_split", "o_ucnt", "o_ws8", "o_plen", "o_plenc", "o_pbase",
+                                            "o_cbase", "o_colp", "o_bcv", "o_ovf", "o_scan", "ws_bytes")])
 
 
-def _bm_config(cfg: int):
-    """(log2 window, windows per count unit, fast-kernel product capacity,
-    register rounds, longest stageable A row) of bitmap configuration ``cfg``."""
-    if cfg not in _BM_CFGS:
-        v = [C.c_int() for _ in range(5)]
-        _native.check(_native.hip().spmm_spgemm_bm_config(cfg, *[C.byref(x) for x in v]), "spgemm_bm_config")
-        _BM_CFGS[cfg] = tuple(x.value for x in v)
-    return _BM_CFGS[cfg]
+_native.register_hip("spmm_spgemm_bm_choose", c_vp, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64)
+_native.register_hip("spmm_spgemm_bm_make_plan", c_vp, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64,
+                     C.c_double, c_vp)
+_native.register_hip("spmm_spgemm_bm_front", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_back", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, C_I64,
+                     c_vp, c_vp, c_vp)
 
 
-def _bm_pick(mean_row_products: float, ncols: int) -> Optional[int]:
-    """The configuration with the widest window whose mean products per window
-    fit BM_FILL of its fast capacity (widest = fewest units per row)."""
-    best = None
-    for cfg in (0, 2, 1):   # widest window first
-        lgw, _, pcap, _, _ = _bm_config(cfg)
-        W = 1 << lgw
-        per_window = mean_row_products * min(W, ncols) / max(ncols, 1)
-        if per_window <= BM_FILL * pcap:
-            best = cfg
-            break
-    return best
+def _bm_opts(use_ws8: bool = True) -> _BmOpts:
+    """CONFIG -> the native plan's options (csr_bitmap_plan.hip owns the decisions)."""
+    tri = {"off": 0, "auto": 1, "on": 2}
+    return _BmOpts(mode=tri.get(CONFIG.spgemm_bitmap, 1), cfg=CONFIG.spgemm_bitmap_cfg,
+                   rows_mode=tri.get(CONFIG.spgemm_bitmap_rows, 1),
+                   count_windows=CONFIG.spgemm_bitmap_count_windows, det=int(CONFIG.spgemm_deterministic > 0),
+                   pad=int(CONFIG.spgemm_bitmap_pad > 0), cv=int(bool(CONFIG.spgemm_bitmap_cv)),
+                   pipe=int(CONFIG.spgemm_bitmap_pipe > 0), use_ws8=int(use_ws8))
 
 
 def _bitmap_ok(A: CSR, B: CSR, total_products: int, pre: dict) -> bool:
-    """Bitmap-rank path: uint32 B indices, every A row stageable by the reload
-    kernel, row products not far above the mean (the windows are sized from
-    the mean; a skewed matrix, e.g. R-MAT, takes the binned path)."""
-    mode = CONFIG.spgemm_bitmap
-    if mode == "off" or total_products == 0 or _true_nnz(B) >= (1 << 31) or B.n >= (1 << 30) or A.nnz >= (1 << 31):
+    """Bitmap-rank path (the native gate spmm_spgemm_bm_choose: uint32 B
+    indices, every A row stageable by the reload kernel, row products not far
+    above the mean -- a skewed matrix, e.g. R-MAT, takes the binned path) and
+    the product-count bound of C in free device memory."""
+    if CONFIG.spgemm_bitmap == "off" or total_products == 0:
         return False
-    nz = max(pre["nonempty"], 1)
-    mean = total_products / nz
-    cfg = CONFIG.spgemm_bitmap_cfg if CONFIG.spgemm_bitmap_cfg >= 0 else _bm_pick(mean, B.n)
-    if cfg is None:
-        cfg = 1 if mode == "on" else None
-    if cfg is None or pre.get("amax", 1 << 30) > _bm_config(cfg)[4]:
+    o = _bm_opts()
+    cfg = _native.hip().spmm_spgemm_bm_choose(C.byref(o), A.m, A.nnz, B.n, _true_nnz(B), total_products,
+                                              pre["nonempty"], pre["max"], pre.get("amax", 1 << 30))
+    if cfg < 0:
         return False
-    if mode == "on":
+    if CONFIG.spgemm_bitmap == "on":
         return True
-    if pre["max"] > 4 * mean or nz < 0.5 * A.m:
-        return False
     return _FreeMem(A.device).fits(total_products * 8 + A.m * 64)
 
 
 @dataclass
 class BitmapPlan:
-    """Host decisions of one bitmap-rank product (``_bitmap_plan``): window
-    configuration, lane groups, which kernels run, and C's capacity in the
-    lazy flow.  Everything the kernels need besides the operands, so a plan
-    made once can drive a captured HIP graph (``SpgemmGraph``)."""
-    cfg: int
-    nwin: int
-    nsub: int
-    lg_count: int      # per-unit count kernel lane groups
-    lg_c: int          # row count kernel lane groups
-    nsub_c: int        # windows per row-count unit
-    lg_num: int
-    count_rows: bool   # row count kernel (A rows <= 256, ws8 packed)
-    rows: bool         # row-major numeric kernel
-    det: bool
-    tot: int           # intermediate products (C's capacity in the lazy flow)
+    """Host decisions of one bitmap-rank product, made by the native planner
+    (csr_bitmap_plan.hip spmm_spgemm_bm_make_plan, shared with the native
+    engine): window configuration, lane groups, which kernels run, padded
+    layout capacities, one workspace layout, and C's capacity in the lazy flow.
+    Everything the kernels need besides the operands, so a plan made once can
+    drive a captured HIP graph (``SpgemmGraph``)."""
+    raw: _BmPlan
+    opts: _BmOpts
+
+    def __getattr__(self, name):
+        if name in ("raw", "opts"):
+            raise AttributeError(name)
+        v = getattr(self.raw, name)
+        return bool(v) if name in ("count_rows", "rows", "det", "ws8", "pad_num", "pad_cnt", "plain_cv") else v
 
 
-def _bitmap_plan(A: CSR, B: CSR, info: SpgemmInfo, pre: Optional[dict]) -> Optional[BitmapPlan]:
-    m = A.m
-    tot = info.flops // 2
-    nz = max(pre["nonempty"], 1) if pre is not None else max(m, 1)
-    cfg = CONFIG.spgemm_bitmap_cfg if CONFIG.spgemm_bitmap_cfg >= 0 else _bm_pick(tot / nz, B.n)
-    if cfg is None:
-        cfg = 1
-    lgw, nsub, pcap, rounds, _ = _bm_config(cfg)
-    nwin = max(1, -(-B.n // (1 << lgw)))
-    if m * nwin >= (1 << 31):
+def _bitmap_plan(A: CSR, B: CSR, info: SpgemmInfo, pre: Optional[dict], use_ws8: bool = True) -> Optional[BitmapPlan]:
+    o = _bm_opts(use_ws8)
+    p = _BmPlan()
+    nz = pre["nonempty"] if pre is not None else A.m
+    amax = pre.get("amax", -1) if pre is not None else -1
+    if _native.hip().spmm_spgemm_bm_make_plan(C.byref(o), A.m, A.nnz, B.m, B.n, _true_nnz(B), info.flops // 2, nz,
+                                               amax, float(info.mean_seg), C.byref(p)):
         return None
-    seg = info.mean_seg if info.mean_seg > 0 else _true_nnz(B) / max(B.m, 1)
-    rows_mode = CONFIG.spgemm_bitmap_rows
-    ws8_ok = nwin <= 8 and rows_mode != "off"
-    nsub_c = CONFIG.spgemm_bitmap_count_windows if nwin >= 2 else 1
-    sl = seg * nsub_c / nwin   # B-segment length per row-count unit
-    return BitmapPlan(cfg=cfg, nwin=nwin, nsub=nsub, lg_count=_group_log2(seg * min(nsub, nwin) / nwin),
-                      lg_c=4 if sl < 48 else (5 if sl < 96 else 6), nsub_c=nsub_c,
-                      lg_num=4 if seg / nwin < 48 else (5 if seg / nwin < 96 else 6),
-                      count_rows=ws8_ok and pre is not None and pre.get("amax", 1 << 30) <= 256,
-                      rows=ws8_ok and (rows_mode == "on" or cfg == 0),
-                      det=CONFIG.spgemm_deterministic > 0, tot=tot)
+    return BitmapPlan(raw=p, opts=o)
 
 
-def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, info: Optional[SpgemmInfo] = None,
-                   use_ws8: bool = True) -> dict:
-    """The kernels of one bitmap-rank product.  ``lazy``: C at the product
+def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, info: Optional[SpgemmInfo] = None) -> dict:
+    """The kernels of one bitmap-rank product, launched by the native front /
+    back (csr_bitmap_plan.hip) into one workspace.  ``lazy``: C at the product
     bound, no host synchronisation at all (capturable into a HIP graph; the
     nnz and error bits stay on the device in ``out["z"]`` / ``out["uoff"]``).
     Eager: one read-back between count and numeric sizes C exactly."""
     dev = A.device
-    m = A.m
-    cfg, nwin = plan.cfg, plan.nwin
-    lgw = _bm_config(cfg)[0]
     if B_ready is not None:   # columns only: the values may still be in flight (two-stage gather)
         B = getattr(B_ready, "cols", B_ready)()
     lib = _native.hip()
     P = _native.ptr
     st = _native.stream_ptr(dev)
-    ws = torch.empty(B.m * (nwin + 1), dtype=torch.int32, device=dev)
-    _native.check(lib.spmm_spgemm_bm_splits(P(B.rowptr), P(B.col), B.m, lgw, nwin, P(ws), st), "spgemm_bm_splits")
-    nunits = m * nwin
-    z = torch.zeros(2, dtype=torch.int32, device=dev)   # err, deferred count
-    err, novf = z[0:1], z[1:2]
-    ucnt = torch.empty(nunits, dtype=torch.int32, device=dev)
-    # row-major kernels (a row's windows back to back): <= 8 windows, packed
-    # 16-bit window lengths (ws8)
-    ws8 = None
-    # padded layouts for the row kernels: every (row, window) segment of the
-    # numeric kernel's pairs and every (row, count group) segment of the count
-    # kernel's columns starts on a 128-byte line; sized by bounds (no read-back)
-    nnzb = _true_nnz(B)
-    ngc = -(-nwin // plan.nsub_c)
-    pad = CONFIG.spgemm_bitmap_pad > 0 and use_ws8
-    # (the per-unit fast kernel reads the padded pairs too, two per lane; not in deterministic mode)
-    pad_num = pad and (plan.rows or not plan.det) and CONFIG.spgemm_bitmap_cv and nnzb + 15 * nwin * B.m < (1 << 32)
-    pad_cnt = pad and plan.count_rows and nnzb + 31 * ngc * B.m < (1 << 32)
-    plen = torch.empty(B.m, dtype=torch.int64, device=dev) if pad_num else None
-    plen_c = torch.empty(B.m, dtype=torch.int64, device=dev) if pad_cnt else None
-    if use_ws8 and (plan.count_rows or plan.rows or pad_num):
-        ws8 = torch.empty(B.m * 8, dtype=torch.int32, device=dev)
-        _native.check(lib.spmm_spgemm_bm_pack_ws8(P(ws), B.m, nwin, P(ws8), P(err),
-                                                  P(plen) if plen is not None else None,
-                                                  P(plen_c) if plen_c is not None else None, plan.nsub_c, st),
-                      "spgemm_bm_pack_ws8")
-    Bcv = None
-    if ws8 is not None and plan.count_rows:
-        colp = None
-        if plen_c is not None:
-            cbase = device_scan(plen_c, torch.empty_like(plen_c), inclusive=False)
-            colp = torch.empty(nnzb + 31 * ngc * B.m, dtype=torch.int32, device=dev)
-            # B's values are here (no all-gather in flight): both layouts in one pass
-            both = plen is not None and (B_ready is None or getattr(B_ready, "local", False))
-            pbase = None
-            if both:
-                pbase = device_scan(plen, torch.empty_like(plen), inclusive=False)
-                Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
-            # (otherwise columns only: B's values may still be in flight)
-            _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val) if both else None, B.m, nwin, lgw,
-                                                       P(pbase) if both else None, P(ws8), P(Bcv) if both else None,
-                                                       P(cbase), plan.nsub_c, P(colp),
-                                                       Bcv.shape[0] if both else 0, colp.numel(), P(err), st),
-                          "spgemm_bm_pad_pairs(columns)")
-            del cbase, plen_c, pbase
-        _native.check(lib.spmm_spgemm_bm_count_rows(cfg, P(A.rowptr), P(A.col), P(ws8),
-                                                    P(colp) if colp is not None else P(B.col), m, nwin, plan.lg_c,
-                                                    plan.nsub_c, P(ucnt), P(err),
-                                                    colp.numel() if colp is not None else B.col.numel(),
-                                                    int(colp is not None), int(CONFIG.spgemm_bitmap_pipe > 0),
-                                                    _true_nnz(A), st),
-                      "spgemm_bm_count_rows")
-        del colp
-    else:
-        _native.check(lib.spmm_spgemm_bm_count(cfg, P(A.rowptr), P(A.col), P(ws), P(B.col), m, nwin, plan.lg_count,
-                                               P(ucnt), P(err), st), "spgemm_bm_count")
-    uoff = torch.empty(nunits + 1, dtype=torch.int64, device=dev)
-    uoff[:1].zero_()   # (a fill kernel: capturable, unlike a host scalar copy)
-    device_scan(ucnt, uoff[1:], inclusive=True)
-    del ucnt
-    out = dict(uoff=uoff, z=z, nunits=nunits, ws8=ws8 is not None)
+    raw = plan.raw
+    ws = torch.empty(max(raw.ws_bytes, 1), dtype=torch.uint8, device=dev)
+    z = torch.empty(2, dtype=torch.int32, device=dev)   # err, deferred count (zeroed by the front)
+    uoff = torch.empty(raw.nunits + 1, dtype=torch.int64, device=dev)
+    values_here = B_ready is None or getattr(B_ready, "local", False)
+    built = C.c_int(0)
+    _native.check(lib.spmm_spgemm_bm_front(C.byref(raw), P(A.rowptr), P(A.col), P(B.rowptr), P(B.col),
+                                           P(B.val) if values_here else None, P(ws), P(uoff), P(z), C.byref(built),
+                                           st), "spgemm_bm_front")
+    out = dict(uoff=uoff, z=z, nunits=raw.nunits, ws8=bool(raw.ws8))
     if not lazy:
-        nnz, e0 = torch.stack([uoff[-1], err[0].long()]).tolist()   # one read-back
+        nnz, e0 = torch.stack([uoff[-1], z[0].long()]).tolist()   # one read-back
         if e0 & 32:
             raise RuntimeError("spgemm bitmap: padded B layout overflow (kernel invariant violated)")
         out.update(nnz=nnz)
         if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
             out.update(truncated=True)
             return out
-        err.zero_()
-    cap = max(plan.tot, 1) if lazy else out["nnz"]
+        z[0].zero_()
+    cap = max(raw.tot, 1) if lazy else out["nnz"]
     if B_ready is not None:   # the numeric kernels read the values
         B = B_ready()
     Cci = torch.empty(cap, dtype=torch.int32, device=dev)
     Cv = torch.empty(cap, dtype=torch.float32, device=dev)
-    ovf_cap = min(nunits, 1 << 20)
-    ovf = torch.empty(max(ovf_cap, 1), dtype=torch.int32, device=dev)
-    det = int(plan.det)
-    if ws8 is not None and plen is not None and Bcv is None:
-        # interleaved (column, value) pairs with every window segment starting
-        # on a 128-byte line: the numeric kernels take two pairs per 16-byte load
-        pbase = device_scan(plen, torch.empty_like(plen), inclusive=False)
-        Bcv = torch.empty((nnzb + 15 * nwin * B.m, 2), dtype=torch.int32, device=dev)
-        _native.check(lib.spmm_spgemm_bm_pad_pairs(P(ws), P(B.col), P(B.val), B.m, nwin, lgw, P(pbase), P(ws8),
-                                                   P(Bcv), None, 1, None, Bcv.shape[0], 0, P(err), st),
-                      "spgemm_bm_pad_pairs")
-        del pbase
-    if ws8 is not None and plan.rows:
-        # the row-major kernel reads B as interleaved (column, value) pairs: one
-        # stream per chunk instead of two; padded, each window segment starts on
-        # a 128-byte line
-        if Bcv is None:
-            Bcv = interleaved(B) if CONFIG.spgemm_bitmap_cv else None
-        _native.check(lib.spmm_spgemm_bm_numeric_rows(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws8), P(ws), P(B.col),
-                                                      P(B.val), P(Bcv) if Bcv is not None else None, m, nwin,
-                                                      plan.lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf),
-                                                      P(novf), ovf_cap, P(err), det, int(plen is not None),
-                                                      Bcv.shape[0] if Bcv is not None else 0,
-                                                      int(CONFIG.spgemm_bitmap_pipe > 0), _true_nnz(A), st),
-                      "spgemm_bm_numeric_rows")
-        if info is not None:
-            info.rows_per_bin_num["bitmap_rows"] = 1
-    else:
-        wide = Bcv is not None and not det
-        _native.check(lib.spmm_spgemm_bm_numeric(cfg, P(A.rowptr), P(A.col), P(A.val), P(ws), P(B.col), P(B.val), m,
-                                                 nwin, plan.lg_num, P(uoff), cap, P(Cci), P(Cv), P(ovf), P(novf),
-                                                 ovf_cap, P(err), det, P(ws8) if wide else None,
-                                                 P(Bcv) if wide else None, st),
-                      "spgemm_bm_numeric")
-    out.update(Cci=Cci, Cv=Cv, cap=cap, n=B.n)
+    _native.check(lib.spmm_spgemm_bm_back(C.byref(raw), P(A.rowptr), P(A.col), P(A.val), P(B.col), P(B.val),
+                                          built.value, P(ws), P(uoff), P(z), cap, P(Cci), P(Cv), st),
+                  "spgemm_bm_back")
+    if info is not None and raw.ws8 and raw.rows:
+        info.rows_per_bin_num["bitmap_rows"] = 1
+    out.update(Cci=Cci, Cv=Cv, cap=cap, n=B.n, ws=ws)
     return out
 
 
@@ -968,7 +857,8 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     lazy = CONFIG.spgemm_bitmap_lazy > 0 and not plan.det and not _eager
     out = _bitmap_launch(A, B, plan, lazy, B_ready, info)
     if out.get("truncated"):   # eager: per-unit count and numeric kernels
-        out = _bitmap_launch(A, B, plan, False, B_ready, info, use_ws8=False)
+        plan = _bitmap_plan(A, B, info, pre, use_ws8=False)
+        out = _bitmap_launch(A, B, plan, False, B_ready, info)
     if B_ready is not None:
         B = B_ready()
     C_ = _bitmap_finish(A, B, plan, out, info, lazy)

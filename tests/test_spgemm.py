@@ -1253,3 +1253,26 @@ def test_spgemm_graph_replay_structure_change():
         lo, hi = int(C3.rowptr[r]), int(C3.rowptr[r + 1])
         got[C3.col[lo:hi].long()] = C3.val[lo:hi].double()
         assert torch.allclose(got, want, atol=1e-4, rtol=1e-4), r
+
+
+def test_bitmap_plan_defaults_match_native():
+    """The bitmap planner is native (csr_bitmap_plan.hip, shared with the a4 engine); the
+    Python knobs (utils/config.py) and the native engine's environment defaults agree, and
+    the native plan of a 1M-like product picks the wide-window row kernels."""
+    import ctypes as C
+
+    from spmm_amd import _native
+    from spmm_amd.ops import spgemm as SG
+
+    env = SG._BmOpts()
+    _native.hip().spmm_spgemm_bm_env_opts(C.byref(env))
+    py = SG._bm_opts()
+    for f, _ in SG._BmOpts._fields_:
+        assert getattr(env, f) == getattr(py, f), f
+    p = SG._BmPlan()
+    m, n, annz = 1 << 20, 1 << 20, 104857600
+    tot = 10_995_116_277
+    assert _native.hip().spmm_spgemm_bm_make_plan(C.byref(py), m, annz, n, n, annz, tot, m, 140,
+                                                   float(tot / annz), C.byref(p)) == 0
+    assert p.cfg == 0 and p.nwin == 8 and p.rows and p.count_rows and p.pad_num and p.pad_cnt
+    assert p.ws_bytes >= p.cap_bcv * 8 + p.cap_colp * 4
