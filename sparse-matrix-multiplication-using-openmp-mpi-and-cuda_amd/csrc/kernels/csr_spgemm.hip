@@ -1930,6 +1930,35 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
   return 0;
 }
 
+// Row-binning table of the binned two-phase path, the one copy for ops/spgemm.py (_bins) and
+// the native engine (csr_engine.cpp): caps[b] = the most products (numeric) or the most
+// distinct-key bound (symbolic) a row of bin b may have; bins 0..6 are single-pass LDS tables
+// of 128 << b slots at load <= load, symbolic 7..10 the 16384-slot table over 1/2/4/8 column
+// slices at load <= load_sliced, numeric 7..10 the bucketed ESC kernels (kEscPcap products
+// per slice, esc_load per-slice margin from 2 slices up); beyond caps[10]: the long-row path.
+// Numeric rows of more than esc_min products skip the single-pass tables.
+constexpr int64_t kEscPcap = 7680;   // launch_esc<7680, ...>
+constexpr double kEscLoad = 0.9;
+SPMM_EXPORT int spmm_spgemm_bin_caps(int numeric, double load, double load_sliced, int64_t esc_min, int64_t* caps) {
+  for (int b = 0; b < 7; ++b) {
+    const int64_t c = (int64_t)(load * (double)(128 << b));
+    caps[b] = numeric ? std::min(c, esc_min) : c;
+  }
+  for (int k = 0; k < 4; ++k)
+    caps[7 + k] = numeric ? (k == 0 ? kEscPcap : (int64_t)(kEscLoad * kEscPcap) * (1 << k))
+                          : (int64_t)(load_sliced * 16384) * (1 << k);
+  return 0;
+}
+
+// Constants the host planners size their buffers from: the row-plan partials
+// (kPlanBlocks x kPlanStats) and the ordered one-pass caps' ESC margin.
+SPMM_EXPORT int spmm_spgemm_plan_params(int* plan_blocks, int* plan_stats, double* esc_load) {
+  *plan_blocks = kPlanBlocks;
+  *plan_stats = kPlanStats;
+  *esc_load = kEscLoad;
+  return 0;
+}
+
 // nprod / nsl: [m]; part: [1024 * 16] scratch; stats: [16] (see spgemm_row_plan).
 SPMM_EXPORT int spmm_spgemm_row_plan(const int64_t* Arp, const int32_t* Aci, const int64_t* Brp, int64_t m,
                                      int64_t cap1, int64_t cap2, int64_t cap4, int64_t esc_min, int64_t* nprod,

@@ -9,6 +9,7 @@
 #include "../kernels/bitmap_plan.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -37,6 +38,8 @@ int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_
 int spmm_spgemm_long_place(const int64_t* src, const int64_t* dst, const int64_t* cnt, int64_t nrt,
                            const void* scratch, int32_t* Cci, float* Cv, void* stream);
 int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch);
+int spmm_spgemm_bin_caps(int numeric, double load, double load_sliced, int64_t esc_min, int64_t* caps);
+int spmm_spgemm_plan_params(int* plan_blocks, int* plan_stats, double* esc_load);
 // csr_rowsort.hip
 size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen);
 int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64_t nrows, int64_t total, int64_t maxlen,
@@ -59,10 +62,30 @@ namespace a4 {
 
 namespace {
 
-// ops/spgemm.py constants (LOAD, ESC_MIN, ESC_PCAP, ESC_LOAD, GLOBAL_WS_BYTES)
-constexpr double kLoad = 0.5, kEscLoad = 0.9;
-constexpr int64_t kEscMin = 2048, kEscPcap = 7680, kPlanBlocks = 1024, kPlanStats = 16;
-constexpr int64_t kWsProducts = (int64_t(8) << 30) / 8;
+// Knobs shared with ops/spgemm.py through the same environment variables and defaults
+// (utils/config.py: SPMM_SPGEMM_LOAD, _LOAD_SLICED, _ESC_MIN, SPMM_GLOBAL_WS_GB); the bin
+// table itself and the planner constants come from the kernel library.
+double env_f(const char* k, double d) {
+  const char* e = getenv(k);
+  return e && *e ? atof(e) : d;
+}
+struct Knobs {
+  double load = env_f("SPMM_SPGEMM_LOAD", 0.5), load_sliced = env_f("SPMM_SPGEMM_LOAD_SLICED", 0.5);
+  int64_t esc_min = (int64_t)env_f("SPMM_SPGEMM_ESC_MIN", 2048);
+  int64_t ws_products = (int64_t)(env_f("SPMM_GLOBAL_WS_GB", 8.0) * (double)(int64_t(1) << 30)) / 8;
+  int64_t ordered_pcap = (int64_t)env_f("SPMM_SPGEMM_ORDERED_PCAP", 7680);
+  int plan_blocks = 0, plan_stats = 0;
+  double esc_load = 0;
+  int64_t caps[2][11];   // [numeric]
+  Knobs() {
+    spmm_spgemm_plan_params(&plan_blocks, &plan_stats, &esc_load);
+    for (int n = 0; n < 2; ++n) spmm_spgemm_bin_caps(n, load, load_sliced, esc_min, caps[n]);
+  }
+};
+const Knobs& knobs() {
+  static const Knobs k;
+  return k;
+}
 
 template <typename T>
 DevBuf<T> up(const std::vector<T>& h, hipStream_t s) {
@@ -89,12 +112,13 @@ struct Plan {
 Plan row_plan(const DCsr& A, const DCsr& B, hipStream_t s) {
   Plan p;
   p.nprod = DevBuf<int64_t>(std::max<int64_t>(A.m, 1), s);
-  DevBuf<int64_t> nsl(std::max<int64_t>(A.m, 1), s), part((kPlanBlocks + 1) * kPlanStats, s);
-  const int64_t c1 = (int64_t)(kEscLoad * kEscPcap);
-  A4_HIP((hipError_t)spmm_spgemm_row_plan(A.rp.get(), A.ci.get(), B.rp.get(), A.m, c1, 2 * c1, 4 * c1, kEscMin,
-                                          p.nprod.get(), nsl.get(), part.get(), part.get() + kPlanBlocks * kPlanStats,
-                                          s));
-  const std::vector<int64_t> st = down(part.get() + kPlanBlocks * kPlanStats, kPlanStats, s);
+  const Knobs& k = knobs();
+  DevBuf<int64_t> nsl(std::max<int64_t>(A.m, 1), s), part((size_t)(k.plan_blocks + 1) * k.plan_stats, s);
+  const int64_t c1 = (int64_t)(k.esc_load * k.ordered_pcap);
+  const int64_t nst = (int64_t)k.plan_blocks * k.plan_stats;
+  A4_HIP((hipError_t)spmm_spgemm_row_plan(A.rp.get(), A.ci.get(), B.rp.get(), A.m, c1, 2 * c1, 4 * c1, k.esc_min,
+                                          p.nprod.get(), nsl.get(), part.get(), part.get() + nst, s));
+  const std::vector<int64_t> st = down(part.get() + nst, k.plan_stats, s);
   p.tot = st[0];
   p.mx = st[1];
   p.nz = st[2];
@@ -170,7 +194,7 @@ void long_rows(int values, const DCsr& A, const DCsr& B, const std::vector<int32
   const int64_t nrows = (int64_t)rows.size();
   int64_t maxp = 0;
   for (int32_t r : rows) maxp = std::max(maxp, nprod_h[r]);
-  const int64_t cap = std::max(kWsProducts, maxp);
+  const int64_t cap = std::max(knobs().ws_products, maxp);
   for (int64_t start = 0; start < nrows;) {
     int64_t end = start, acc = 0;   // batch: the longest run of rows whose products fit cap (at least one row)
     while (end < nrows && (end == start || acc + nprod_h[rows[end]] <= cap)) acc += nprod_h[rows[end++]];
@@ -248,21 +272,13 @@ void long_rows(int values, const DCsr& A, const DCsr& B, const std::vector<int32
 
 // ---- binned two-phase path (ops/spgemm.py symbolic + numeric) -----------------
 // Bin b of the LDS kernels by a row's product count; -1: empty row; 11: long.
-int sym_bin(int64_t p) {
+// ops/spgemm.py _bins: the first bin whose capacity holds the row (bucketize), 11 = the
+// long-row path, -1 = empty
+int bin_of(int numeric, int64_t p) {
   if (p == 0) return -1;
-  for (int b = 0; b <= 6; ++b)
-    if (p <= (int64_t)(kLoad * (128 << b))) return b;
-  for (int k = 0; k < 4; ++k)
-    if (p <= (int64_t)(kLoad * 16384) * (1 << k)) return 7 + k;
-  return 11;
-}
-int num_bin(int64_t p) {
-  if (p == 0) return -1;
-  for (int b = 0; b <= 6; ++b)
-    if (p <= std::min<int64_t>((int64_t)(kLoad * (128 << b)), kEscMin)) return b;
-  if (p <= kEscPcap) return 7;
-  for (int k = 1; k < 4; ++k)
-    if (p <= (int64_t)(kEscLoad * kEscPcap) * (1 << k)) return 7 + k;
+  const int64_t* caps = knobs().caps[numeric ? 1 : 0];
+  for (int b = 0; b < 11; ++b)
+    if (p <= caps[b]) return b;
   return 11;
 }
 
@@ -287,7 +303,7 @@ DCsr binned_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
   auto run_bins = [&](int numeric, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv) {
     std::vector<std::vector<int32_t>> by(12);
     for (int64_t r = 0; r < A.m; ++r) {
-      const int b = numeric ? num_bin(nprod_h[r]) : sym_bin(nprod_h[r]);
+      const int b = bin_of(numeric, nprod_h[r]);
       if (b >= 0) by[b].push_back((int32_t)r);
     }
     A4_HIP(hipMemsetAsync(flags.get(), 0, std::max<int64_t>(A.m, 1) * sizeof(int32_t), s));

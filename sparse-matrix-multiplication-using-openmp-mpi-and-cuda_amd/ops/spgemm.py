@@ -25,7 +25,7 @@ from __future__ import annotations
 import os
 
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -80,7 +80,7 @@ _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_
 # Symbolic: b = 0..6 single pass (128 << b keys), 7..10 = 16384 keys over
 # 1 / 2 / 4 / 8 column slices.  Numeric: b = 0..6 single pass (128 << b ordered
 # key/value slots) for rows of <= ESC_MIN products, 7..10 = bucketed ESC with
-# ESC_PCAP products per slice over 1 / 2 / 4 / 8 slices.  Then the HBM path.
+# 7680 products per slice over 1 / 2 / 4 / 8 slices (bin_caps).  Then the HBM path.
 # Numeric rows are binned by their PRODUCT count (the ESC capacity is in
 # products, and it bounds the distinct count for the hash bins).
 SYM_SINGLE_TOP = 6
@@ -89,11 +89,9 @@ SYM_SLICED = (7, 8, 9, 10)
 NUM_SLICED = (8, 9, 10)
 SYM_GLOBAL = 11
 NUM_GLOBAL = 11
-ESC_PCAP = 7680
 LOAD = CONFIG.spgemm_load              # max load factor of a single-pass LDS table
 LOAD_SLICED = CONFIG.spgemm_load_sliced   # ... of the big (column-sliced) tables
 ESC_MIN = CONFIG.spgemm_esc_min        # numeric rows with more products use the ESC kernel
-ESC_LOAD = 0.9                         # per-slice margin of the multi-slice ESC bins
 GLOBAL_WS_BYTES = int(CONFIG.spgemm_global_ws_gb * (1 << 30))   # HBM scratch budget per batch of long rows
 
 
@@ -109,16 +107,40 @@ class SpgemmInfo:
     mean_seg: float = 0.0     # mean B-row length per A entry (products / nnz(A)); picks the LDS lane groups
 
 
+_native.register_hip("spmm_spgemm_bin_caps", C_INT, C.c_double, C.c_double, C_I64, c_vp)
+_native.register_hip("spmm_spgemm_plan_params", c_vp, c_vp, c_vp)
+_CAPS: Dict[tuple, List[int]] = {}
+_PARAMS: List = []
+
+
+def bin_caps(numeric: int) -> List[int]:
+    """Capacities of LDS bins 0..10 (csr_spgemm.hip spmm_spgemm_bin_caps, the
+    table the native engine bins with too); a row beyond caps[10] takes the
+    long-row path."""
+    key = (int(numeric), LOAD, LOAD_SLICED, ESC_MIN)
+    if key not in _CAPS:
+        caps = (C.c_int64 * 11)()
+        _native.check(_native.hip().spmm_spgemm_bin_caps(int(numeric), float(LOAD), float(LOAD_SLICED), int(ESC_MIN),
+                                                         caps), "spgemm_bin_caps")
+        _CAPS[key] = list(caps)
+    return _CAPS[key]
+
+
+def plan_params():
+    """(row-plan workgroups, statistics per workgroup, ESC per-slice margin) of
+    csr_spgemm.hip (spmm_spgemm_plan_params)."""
+    if not _PARAMS:
+        pb, ps, el = C.c_int(), C.c_int(), C.c_double()
+        _native.check(_native.hip().spmm_spgemm_plan_params(C.byref(pb), C.byref(ps), C.byref(el)), "plan_params")
+        _PARAMS.append((pb.value, ps.value, el.value))
+    return _PARAMS[0]
+
+
 def _bins(counts: torch.Tensor, numeric: int) -> torch.Tensor:
     """Bin per row: the smallest single-pass table with counts <= LOAD * S, then
     the sliced passes (slice capacity LOAD * S_top * slices), then the HBM path;
     -1 for empty rows."""
-    if numeric:
-        caps = [min(int(LOAD * (128 << b)), ESC_MIN) for b in range(7)]
-        caps += [ESC_PCAP] + [int(ESC_LOAD * ESC_PCAP) * k for k in (2, 4, 8)]
-    else:
-        caps = [int(LOAD * (128 << b)) for b in range(7)]
-        caps += [int(LOAD_SLICED * 16384) * k for k in (1, 2, 4, 8)]
+    caps = bin_caps(numeric)
     b = torch.bucketize(counts, torch.tensor(caps, device=counts.device, dtype=counts.dtype))
     return torch.where(counts == 0, torch.full_like(b, -1), b)
 
@@ -136,8 +158,6 @@ def _group(bins: torch.Tensor, nbins: int):
     return order, groups
 
 
-_PLAN_BLOCKS = 1024   # csr_spgemm.hip kPlanBlocks
-_PLAN_STATS = 16      # csr_spgemm.hip kPlanStats
 
 
 def row_plan(A: CSR, B: CSR):
@@ -148,9 +168,10 @@ def row_plan(A: CSR, B: CSR):
     dev = A.device
     nprod = torch.empty(A.m, dtype=torch.int64, device=dev)
     nsl = torch.empty(A.m, dtype=torch.int64, device=dev)
-    part = torch.empty((_PLAN_BLOCKS + 1) * _PLAN_STATS, dtype=torch.int64, device=dev)
-    stats = part[_PLAN_BLOCKS * _PLAN_STATS:]
-    c1 = int(ESC_LOAD * CONFIG.spgemm_ordered_pcap)
+    nblk, nst, esc_load = plan_params()
+    part = torch.empty((nblk + 1) * nst, dtype=torch.int64, device=dev)
+    stats = part[nblk * nst:]
+    c1 = int(esc_load * CONFIG.spgemm_ordered_pcap)
     P = _native.ptr
     _native.check(_native.hip().spmm_spgemm_row_plan(P(A.rowptr), P(A.col), P(B.rowptr), A.m, c1, 2 * c1, 4 * c1,
                                                       ESC_MIN, P(nprod), P(nsl), P(part), P(stats),
@@ -592,7 +613,7 @@ ORDERED_MAX_LIGHT = 0.05           # ordered mode: at most this share of non-emp
 def _ordered_slices(nprod: torch.Tensor) -> torch.Tensor:
     """Units per row of the ordered one-pass: 1 / 2 / 4 / 8 column ranges by
     product count (0 for empty rows)."""
-    caps = torch.tensor([int(ESC_LOAD * CONFIG.spgemm_ordered_pcap) * k for k in (1, 2, 4)], device=nprod.device,
+    caps = torch.tensor([int(plan_params()[2] * CONFIG.spgemm_ordered_pcap) * k for k in (1, 2, 4)], device=nprod.device,
                         dtype=nprod.dtype)
     nsl = torch.pow(2, torch.bucketize(nprod, caps)).to(torch.int64)
     return torch.where(nprod > 0, nsl, torch.zeros_like(nsl))
@@ -607,7 +628,7 @@ def _ordered_ok(nprod: torch.Tensor, total_products: int, dev: torch.device, pre
     if mode == "off" or total_products == 0:
         return False
     mx = pre["max"] if pre is not None else int(nprod.max())
-    if mx > int(ESC_LOAD * CONFIG.spgemm_ordered_pcap) * 8:
+    if mx > int(plan_params()[2] * CONFIG.spgemm_ordered_pcap) * 8:
         return False
     if mode != "on":
         if pre is not None:

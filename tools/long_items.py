@@ -17,7 +17,7 @@ dev = torch.device("cuda")
 A = gen_csr.rmat_csr(scale, 16, seed=1, device=dev)
 At = A.transpose()
 nprod = SG.row_nprod(A, At)
-cap = int(SG.ESC_LOAD * 7680) * 8
+cap = SG.bin_caps(1)[10]
 rows = (nprod > cap).nonzero().flatten()[:max_rows].to(torch.int32)
 print(f"scale {scale}: total products {int(nprod.sum()):.4g}, long rows {rows.numel()}, "
       f"products in them {int(nprod[rows.long()].sum()):.4g}", flush=True)
