@@ -96,12 +96,14 @@ __device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t 
 // keep ds_add_f32: their adding lanes mostly collide (1M step 61.4 vs 62.6 ms with the try).
 // N independent adds base[idx[u]] += v[u] (idx < 0: none): all reads, then all compare-swap
 // tries in flight together, then ds_add_f32 for the lanes that lost.
+// fresh[u]: the slot is known to hold +0.0 (its occupancy bit was clear): no read.
 template <int N>
-__device__ __forceinline__ void lds_fadd_n(float* base, const int (&idx)[N], const float (&v)[N]) {
+__device__ __forceinline__ void lds_fadd_n(float* base, const int (&idx)[N], const float (&v)[N],
+                                           const bool (&fresh)[N]) {
   uint32_t* q = reinterpret_cast<uint32_t*>(base);
   uint32_t old[N];
 #pragma unroll
-  for (int u = 0; u < N; ++u) old[u] = idx[u] >= 0 ? q[idx[u]] : 0u;
+  for (int u = 0; u < N; ++u) old[u] = (idx[u] >= 0 && !fresh[u]) ? q[idx[u]] : 0u;
   bool lost[N];
 #pragma unroll
   for (int u = 0; u < N; ++u)

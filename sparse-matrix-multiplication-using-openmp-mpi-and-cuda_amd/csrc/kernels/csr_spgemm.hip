@@ -1003,6 +1003,9 @@ __global__ __launch_bounds__(256) void spgemm_compact(const int64_t* __restrict_
 #ifndef SPMM_LONG_EPW                   // (diagnostic builds: tools/bm_variants.py)
 #define SPMM_LONG_EPW 64
 #endif
+#ifndef SPMM_LONG_FRESH
+#define SPMM_LONG_FRESH 1
+#endif
 #ifndef SPMM_LONG_DLOADS
 #define SPMM_LONG_DLOADS 4
 #endif
@@ -1493,13 +1496,22 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
     for (int64_t i0 = tid;;) {
       int ci[LONG_DL];
       float cv[LONG_DL];
+      bool fresh[LONG_DL];
 #pragma unroll
       for (int u = 0; u < LONG_DL; ++u) {
         ci[u] = x[u] == ~0ull ? -1 : (int)(uint32_t)x[u] - c0;
         cv[u] = __uint_as_float((uint32_t)(x[u] >> 32));
-        if (ci[u] >= 0) atomicOr(&bits[ci[u] >> 5], 1u << (ci[u] & 31));
+        fresh[u] = false;
+        if (ci[u] >= 0) {
+          const uint32_t bit = 1u << (ci[u] & 31);
+#if SPMM_LONG_FRESH   // the first product of a column skips the slot read (the slot is +0.0)
+          fresh[u] = !(atomicOr(&bits[ci[u] >> 5], bit) & bit);
+#else
+          atomicOr(&bits[ci[u] >> 5], bit);
+#endif
+        }
       }
-      if constexpr (VALUES) spmm::lds_fadd_n(vals, ci, cv);
+      if constexpr (VALUES) spmm::lds_fadd_n(vals, ci, cv, fresh);
       i0 += LONG_DL * LONG_DNT;
       if (i0 >= n) break;
       // LONG_DL scratch loads in flight per lane before the LDS updates
@@ -1576,13 +1588,15 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
           }
           int ci[LONG_DU];
           float cv[LONG_DU];
+          bool fresh[LONG_DU];
 #pragma unroll
           for (int u = 0; u < LONG_DU; ++u) {
             ci[u] = cc[u] < 0 ? -1 : cc[u] - c0;
             cv[u] = av[u] * vv[u];
+            fresh[u] = false;
             if (ci[u] >= 0) atomicOr(&bits[ci[u] >> 5], 1u << (ci[u] & 31));
           }
-          if constexpr (VALUES) spmm::lds_fadd_n(vals, ci, cv);
+          if constexpr (VALUES) spmm::lds_fadd_n(vals, ci, cv, fresh);
         }
         lr_wave_fence();   // seg / sa reads done before the next block's writes
       }
