@@ -1,4 +1,5 @@
-// Device re-sort of listed CSR rows (the SpGEMM rows whose LDS table could not keep
+// Device row utilities of the binned SpGEMM path: row binning by the shared bin table, flagged-row
+// selection, and the re-sort of listed CSR rows (the SpGEMM rows whose LDS table could not keep
 // its output column-sorted, flag 1): one engine for the Python front end
 // (ops/csr.py sort_rows) and the native chain (csrc/runtime/csr_engine.cpp), which
 // re-sorted them on the host one row at a time (round 4).  The reference keeps its
@@ -19,6 +20,7 @@ int spmm_prim_scan(const void* in, int in_bytes, int64_t n, int64_t* out, int in
 size_t spmm_prim_scan_ws(int64_t n);
 size_t spmm_prim_sort_ws(int64_t n);
 int spmm_prim_sort_pairs_u64(uint64_t* keys, uint64_t* vals, int64_t n, int bits, void* ws, void* stream);
+int spmm_spgemm_bin_caps(int numeric, double load, double load_sliced, int64_t esc_min, int64_t* caps);
 }
 
 namespace {
@@ -130,7 +132,98 @@ __global__ __launch_bounds__(kRsNt) void rs_sort_lds(const int64_t* __restrict__
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// ---- row binning of the binned SpGEMM path (the native engine's device planner) ----------
+struct Caps {
+  int64_t c[11];
+};
+
+// key = bin + 1 (0: empty row, 1..11: LDS bins 0..10, 12: long-row path); hist[key] counts
+__global__ __launch_bounds__(256) void rb_keys(const int64_t* __restrict__ nprod, int64_t m, Caps caps,
+                                               uint64_t* __restrict__ key, uint64_t* __restrict__ val,
+                                               unsigned long long* __restrict__ hist) {
+  __shared__ unsigned int h[13];
+  if (threadIdx.x < 13) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r < m) {
+    const int64_t p = nprod[r];
+    int k = 12;
+    if (p == 0) {
+      k = 0;
+    } else {
+      for (int b = 10; b >= 0; --b)
+        if (p <= caps.c[b]) k = b + 1;
+    }
+    key[r] = (uint64_t)k;
+    val[r] = (uint64_t)r;
+    atomicAdd(&h[k], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 13 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void rb_order(const uint64_t* __restrict__ val, int64_t m, int32_t* __restrict__ order) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < m) order[i] = (int32_t)val[i];
+}
+
+// rows r with flags[r] & mask, appended at out[*count] (any order)
+__global__ __launch_bounds__(256) void rb_select(const int32_t* __restrict__ flags, int64_t m, int mask,
+                                                 int32_t* __restrict__ out, unsigned long long* __restrict__ count) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool hit = r < m && (flags[r] & mask) != 0;
+  const unsigned long long b = __ballot(hit);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  unsigned long long base = 0;
+  if (lane == __ffsll((long long)b) - 1) base = atomicAdd(count, (unsigned long long)__popcll(b));
+  base = __shfl(base, __ffsll((long long)b) - 1);
+  if (hit) out[base + __popcll(b & ((1ull << lane) - 1ull))] = (int32_t)r;
+}
+
 }  // namespace
+
+SPMM_EXPORT size_t spmm_spgemm_bin_rows_ws(int64_t m) {
+  return align256((size_t)m * 8) * 2 + align256(spmm_prim_sort_ws(m));
+}
+
+// The rows of the binned path ordered by bin (stable: ascending row ids inside a bin), with the
+// bin table of spmm_spgemm_bin_caps: order[m] (int32), hist[13] (int64, device) = empty rows,
+// then bins 0..10, then the long-row path.  Launches only (ops/spgemm.py _bins + _group).
+SPMM_EXPORT int spmm_spgemm_bin_rows(const int64_t* nprod, int64_t m, int numeric, double load, double load_sliced,
+                                     int64_t esc_min, int32_t* order, int64_t* hist, void* ws, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(hist, 0, 13 * sizeof(int64_t), s) != hipSuccess) return (int)hipErrorUnknown;
+  if (m <= 0) return 0;
+  if (m >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  Caps caps;
+  spmm_spgemm_bin_caps(numeric, load, load_sliced, esc_min, caps.c);
+  char* p = (char*)ws;
+  uint64_t* key = (uint64_t*)p;
+  p += align256((size_t)m * 8);
+  uint64_t* val = (uint64_t*)p;
+  p += align256((size_t)m * 8);
+  const dim3 g((unsigned)((m + 255) / 256));
+  hipLaunchKernelGGL(rb_keys, g, dim3(256), 0, s, nprod, m, caps, key, val, (unsigned long long*)hist);
+  SPMM_LAUNCH_CHECK();
+  const int rc = spmm_prim_sort_pairs_u64(key, val, m, 4, p, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rb_order, g, dim3(256), 0, s, val, m, order);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Rows whose flag word has a bit of mask: out[0 .. *count) (device count, zeroed here; any order).
+SPMM_EXPORT int spmm_rows_with_flag(const int32_t* flags, int64_t m, int mask, int32_t* out, int64_t* count,
+                                    void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(count, 0, sizeof(int64_t), s) != hipSuccess) return (int)hipErrorUnknown;
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(rb_select, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, flags, m, mask, out,
+                     (unsigned long long*)count);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
 
 // Workspace bytes of spmm_csr_sort_rows for nrows listed rows holding total entries.
 SPMM_EXPORT size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen) {

@@ -38,9 +38,12 @@ int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_
 int spmm_spgemm_long_place(const int64_t* src, const int64_t* dst, const int64_t* cnt, int64_t nrt,
                            const void* scratch, int32_t* Cci, float* Cv, void* stream);
 int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch);
-int spmm_spgemm_bin_caps(int numeric, double load, double load_sliced, int64_t esc_min, int64_t* caps);
 int spmm_spgemm_plan_params(int* plan_blocks, int* plan_stats, double* esc_load);
 // csr_rowsort.hip
+size_t spmm_spgemm_bin_rows_ws(int64_t m);
+int spmm_spgemm_bin_rows(const int64_t* nprod, int64_t m, int numeric, double load, double load_sliced,
+                         int64_t esc_min, int32_t* order, int64_t* hist, void* ws, void* stream);
+int spmm_rows_with_flag(const int32_t* flags, int64_t m, int mask, int32_t* out, int64_t* count, void* stream);
 size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen);
 int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64_t nrows, int64_t total, int64_t maxlen,
                        int32_t* ci, float* v, void* ws, void* stream);
@@ -76,11 +79,7 @@ struct Knobs {
   int64_t ordered_pcap = (int64_t)env_f("SPMM_SPGEMM_ORDERED_PCAP", 7680);
   int plan_blocks = 0, plan_stats = 0;
   double esc_load = 0;
-  int64_t caps[2][11];   // [numeric]
-  Knobs() {
-    spmm_spgemm_plan_params(&plan_blocks, &plan_stats, &esc_load);
-    for (int n = 0; n < 2; ++n) spmm_spgemm_bin_caps(n, load, load_sliced, esc_min, caps[n]);
-  }
+  Knobs() { spmm_spgemm_plan_params(&plan_blocks, &plan_stats, &esc_load); }
 };
 const Knobs& knobs() {
   static const Knobs k;
@@ -271,17 +270,7 @@ void long_rows(int values, const DCsr& A, const DCsr& B, const std::vector<int32
 }
 
 // ---- binned two-phase path (ops/spgemm.py symbolic + numeric) -----------------
-// Bin b of the LDS kernels by a row's product count; -1: empty row; 11: long.
-// ops/spgemm.py _bins: the first bin whose capacity holds the row (bucketize), 11 = the
-// long-row path, -1 = empty
-int bin_of(int numeric, int64_t p) {
-  if (p == 0) return -1;
-  const int64_t* caps = knobs().caps[numeric ? 1 : 0];
-  for (int b = 0; b < 11; ++b)
-    if (p <= caps[b]) return b;
-  return 11;
-}
-
+// Rows binned on the device by their product count (bins 0..10: LDS kernels; 11: long rows).
 DCsr binned_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s, EngineStats* st) {
   const std::vector<int64_t> nprod_h = down(pl.nprod.get(), A.m, s);
   const std::vector<int64_t> Arp_h = down(A.rp.get(), A.m + 1, s);
@@ -299,44 +288,55 @@ DCsr binned_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
   DevBuf<int64_t> d64(1, s);
   DevBuf<int32_t> d32(1, s);
   DevBuf<float> df(1, s);
+  // rows ordered by bin on the device (csr_rowsort.hip spmm_spgemm_bin_rows, the bin table of
+  // ops/spgemm.py _bins): one 13-word read-back per phase instead of a host pass over the rows
+  DevBuf<int32_t> order((size_t)std::max<int64_t>(A.m, 1), s), sel((size_t)std::max<int64_t>(A.m, 1), s);
+  DevBuf<int64_t> hist(13, s), nsel(1, s);
+  DevBuf<uint8_t> bws(std::max<size_t>(spmm_spgemm_bin_rows_ws(A.m), 1), s);
+  const Knobs& kn = knobs();
+  // rows whose flag word has a bit of mask (device selection, the small list read back, sorted)
+  auto flagged = [&](int mask) {
+    A4_HIP((hipError_t)spmm_rows_with_flag(flags.get(), A.m, mask, sel.get(), nsel.get(), s));
+    const int64_t n = down(nsel.get(), 1, s)[0];
+    std::vector<int32_t> r = down(sel.get(), (size_t)n, s);
+    std::sort(r.begin(), r.end());
+    return r;
+  };
   // run the LDS bins of one phase; returns the rows for the long-row path
   auto run_bins = [&](int numeric, int32_t* row_nnz, const int64_t* Crp, int32_t* Cci, float* Cv) {
-    std::vector<std::vector<int32_t>> by(12);
-    for (int64_t r = 0; r < A.m; ++r) {
-      const int b = bin_of(numeric, nprod_h[r]);
-      if (b >= 0) by[b].push_back((int32_t)r);
-    }
+    A4_HIP((hipError_t)spmm_spgemm_bin_rows(pl.nprod.get(), A.m, numeric, kn.load, kn.load_sliced, kn.esc_min,
+                                            order.get(), hist.get(), bws.get(), s));
+    const std::vector<int64_t> hh = down(hist.get(), 13, s);
     A4_HIP(hipMemsetAsync(flags.get(), 0, std::max<int64_t>(A.m, 1) * sizeof(int32_t), s));
-    std::vector<DevBuf<int32_t>> keep;
+    int64_t off = hh[0];   // (empty rows first)
     for (int b = 0; b <= 10; ++b) {
-      if (by[b].empty()) continue;
-      keep.push_back(up(by[b], s));
-      const bool multi = b >= 8;
-      A4_HIP((hipError_t)spmm_spgemm_lds(b, numeric, A.rp.get(), A.ci.get(), A.v.get(), B.rp.get(), B.ci.get(),
-                                         B.v.get(), multi ? splits() : nullptr, keep.back().get(),
-                                         (int64_t)by[b].size(), (int)B.n, group_log2(seg / slices(b)), row_nnz,
-                                         nullptr, Crp ? Crp : d64.get(), Cci ? Cci : d32.get(), Cv ? Cv : df.get(),
-                                         flags.get(), s));
+      const int64_t cnt = hh[b + 1];
+      if (cnt) {
+        const bool multi = b >= 8;
+        A4_HIP((hipError_t)spmm_spgemm_lds(b, numeric, A.rp.get(), A.ci.get(), A.v.get(), B.rp.get(), B.ci.get(),
+                                           B.v.get(), multi ? splits() : nullptr, order.get() + off, cnt, (int)B.n,
+                                           group_log2(seg / slices(b)), row_nnz, nullptr, Crp ? Crp : d64.get(),
+                                           Cci ? Cci : d32.get(), Cv ? Cv : df.get(), flags.get(), s));
+      }
+      off += cnt;
     }
-    const std::vector<int32_t> fl = down(flags.get(), A.m, s);
-    std::vector<int32_t> lr = by[11];
-    for (int64_t r = 0; r < A.m; ++r) {
-      A4_CHECK((fl[r] & 4) == 0, "spgemm: output position out of range (kernel invariant violated)");
-      if (fl[r] & 2) lr.push_back((int32_t)r);   // a slice could overflow its LDS table
-    }
+    std::vector<int32_t> lr = down(order.get() + off, (size_t)hh[12], s);   // bin 11: the long-row path
+    A4_CHECK(flagged(4).empty(), "spgemm: output position out of range (kernel invariant violated)");
+    const std::vector<int32_t> ovf = flagged(2);   // a slice could overflow its LDS table
+    lr.insert(lr.end(), ovf.begin(), ovf.end());
     std::sort(lr.begin(), lr.end());
-    return std::make_pair(lr, fl);
+    return lr;
   };
   // symbolic: exact nnz per row
   DevBuf<int32_t> row_nnz((size_t)std::max<int64_t>(A.m, 1), s);
   A4_HIP(hipMemsetAsync(row_nnz.get(), 0, std::max<int64_t>(A.m, 1) * sizeof(int32_t), s));
-  auto sym = run_bins(0, row_nnz.get(), nullptr, nullptr, nullptr);
+  const std::vector<int32_t> sym = run_bins(0, row_nnz.get(), nullptr, nullptr, nullptr);
   std::vector<int32_t> nnz_h = down(row_nnz.get(), A.m, s);
-  std::vector<int64_t> lcnt(sym.first.size());
-  long_rows(0, A, B, sym.first, nprod_h, Arp_h, s, &lcnt, nullptr, nullptr, nullptr);
-  for (size_t i = 0; i < sym.first.size(); ++i) {
+  std::vector<int64_t> lcnt(sym.size());
+  long_rows(0, A, B, sym, nprod_h, Arp_h, s, &lcnt, nullptr, nullptr, nullptr);
+  for (size_t i = 0; i < sym.size(); ++i) {
     A4_CHECK(lcnt[i] < INT32_MAX, "a row of the product has 2^31 or more entries");
-    nnz_h[sym.first[i]] = (int32_t)lcnt[i];
+    nnz_h[sym[i]] = (int32_t)lcnt[i];
   }
   std::vector<int64_t> Crp_h(A.m + 1, 0);
   for (int64_t r = 0; r < A.m; ++r) Crp_h[r + 1] = Crp_h[r] + nnz_h[r];
@@ -349,13 +349,11 @@ DCsr binned_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
   C.v = DevBuf<float>((size_t)std::max<int64_t>(C.nnz, 1), s);
   row_nnz = up(nnz_h, s);   // the numeric kernels' per-row capacities (exact)
   // numeric: values into the layout fixed by the symbolic phase
-  auto num = run_bins(1, row_nnz.get(), C.rp.get(), C.ci.get(), C.v.get());
-  long_rows(1, A, B, num.first, nprod_h, Arp_h, s, nullptr, &Crp_h, C.ci.get(), C.v.get());
-  st->long_rows += (int64_t)num.first.size();
+  const std::vector<int32_t> num = run_bins(1, row_nnz.get(), C.rp.get(), C.ci.get(), C.v.get());
+  long_rows(1, A, B, num, nprod_h, Arp_h, s, nullptr, &Crp_h, C.ci.get(), C.v.get());
+  st->long_rows += (int64_t)num.size();
   // rows the ordered LDS tables could not keep sorted (flag 1): re-sorted here
-  std::vector<int32_t> bad;
-  for (int64_t r = 0; r < A.m; ++r)
-    if (num.second[r] & 1) bad.push_back((int32_t)r);
+  const std::vector<int32_t> bad = flagged(1);
   // ... on the device (csr_rowsort.hip, the kernels ops/csr.py sort_rows uses): the row
   // lengths are host values here, so no read-back at all
   if (!bad.empty()) {
