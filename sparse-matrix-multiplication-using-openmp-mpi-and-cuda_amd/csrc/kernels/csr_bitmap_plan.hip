@@ -144,7 +144,9 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   if (m * nwin >= ((int64_t)1 << 31)) return 1;
   const double seg = mean_seg > 0 ? mean_seg : (double)bnnz / (double)std::max<int64_t>(mb, 1);
   const bool ws8_ok = nwin <= 8 && o->rows_mode != 0;
-  const int nsub_c = nwin >= 2 ? o->count_windows : 1;
+  // windows per row-count unit: the count kernels exist for 1, 2 and 4 (other requests: 2)
+  const int cw = (o->count_windows == 1 || o->count_windows == 4) ? o->count_windows : 2;
+  const int nsub_c = nwin >= 2 ? cw : 1;
   const double sl = seg * nsub_c / nwin;   // B-segment length per row-count unit
   p->cfg = cfg;
   p->lgw = k.lgw;
