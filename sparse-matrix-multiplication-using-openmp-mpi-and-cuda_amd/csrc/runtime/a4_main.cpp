@@ -925,6 +925,9 @@ int run(const Options& o, int rank, int world, double t_start) {
   }
   if (gpu) A4_HIP(hipDeviceSynchronize());
   st.t_comm = now_s() - t1;
+  // whole-job work for the metrics: every rank's tile pairs (local chains + its tree steps)
+  int64_t pairs_all = st.tile_pairs;
+  MPI_Reduce(&st.tile_pairs, &pairs_all, 1, MPI_INT64_T, MPI_SUM, 0, MPI_COMM_WORLD);
 
   if (rank == 0) {
     Range r("prune + write");
@@ -955,10 +958,10 @@ int run(const Options& o, int rank, int world, double t_start) {
       const double t_h2d = Stats::drain(st.ev_h2d), t_kernel = gpu ? Stats::drain(st.ev_kernel) : st.t_kernel_cpu;
       const double busy = st.t_parse + t_h2d + t_kernel;
       std::ofstream m(o.metrics);
-      const double ops = (double)st.tile_pairs * 2.0 * k * k * k;
+      const double ops = (double)pairs_all * 2.0 * k * k * k;
       m << "{\"engine\": \"native\", \"device\": \"" << (gpu ? "hip" : "cpu") << "\", \"comm\": \"" << comm->name()
         << "\", \"ranks\": " << world << ", \"split\": " << (o.split ? "true" : "false") << ", \"n\": " << N << ", \"k\": " << k << ", \"products\": " << st.products
-        << ", \"tile_pairs\": " << st.tile_pairs << ", \"int_ops\": " << ops << ", \"t_reduce_s\": " << st.t_reduce
+        << ", \"tile_pairs\": " << pairs_all << ", \"int_ops\": " << ops << ", \"t_reduce_s\": " << st.t_reduce
         << ", \"t_comm_s\": " << st.t_comm << ", \"t_write_s\": " << st.t_write << ", \"bytes_h2d\": " << st.bytes_h2d
         << ", \"bytes_p2p\": " << (comm->bytes_sent + comm->bytes_recv) << ", \"reduce_gops\": "
         << (st.t_reduce > 0 ? ops / st.t_reduce / 1e9 : 0.0) << ", \"wall_s\": " << (now_s() - t_start)

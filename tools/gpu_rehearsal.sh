@@ -16,7 +16,7 @@ for wl in ${WORKLOADS:-spgemm spgemm64k spmm rmat chain}; do
   extra=""
   [ "$wl" = rmat ] && extra="--scale ${RMAT_SCALE:-20}"
   [ "$wl" = spgemm ] && extra="--matrix-n ${SPGEMM_N:-262144}"   # gloo moves B through the host: keep it small
-  [ "$wl" = chain ] && extra="--chain-preset small"                 # weak scaling: N chains share the one card
+  [ "$wl" = chain ] && extra="--chain-preset small"                 # (one chain; its split over N ranks shares the card)
   for n in ${NRANKS:-1 8}; do
     port=$((port + 1))
     log=$O/rehearsal_${wl}_$n.log
@@ -40,7 +40,7 @@ for wl in wls:
     for n, r in recs.items():
         print(f"| {wl} | {n} | {r['ms_per_step']} | {r['value']} {r['unit'].split()[0]} | {r.get('flops_per_step')} | "
               f"{r.get('nnz_C', '')} | {r['config'].get('parallelism')} |")
-    if wl != "chain":   # chain is weak scaling: work grows with the ranks
+    if wl != "chain":   # chain: the N-rank split changes the association tree, so the tile-pair count differs
         ref = recs[ns[0]]
         for n, r in recs.items():
             for k in ("flops_per_step", "nnz_C", "nnz_A"):
