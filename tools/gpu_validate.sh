@@ -1,9 +1,9 @@
 #!/bin/bash
-# round-5 validation: full GPU suite + smoke, 1M / 64k benches, kernel stats of both graph steps (full CSVs),
+# validation run: full GPU suite + smoke, 1M / 64k benches, kernel stats of both graph steps (full CSVs),
 # rank emulation N = 1 / 8
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r5g29; mkdir -p $O
+O=$R/gpurun_out/validate; mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 echo "gpu suite: $(tail -1 $O/pytest_gpu.log)"
@@ -18,8 +18,8 @@ for w in 1 8; do
 done
 cat $O/rank_emulate.jsonl
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/pp29a -o prof --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 > $O/prof1m.log 2>&1 || { tail -20 $O/prof1m.log; exit 1; }
-cp $(find /tmp/pp29a -name "*kernel_stats.csv" | head -1) $O/spgemm1m_kernel_stats.csv
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/pp29b -o prof --output-format csv -- python3 $R/bench.py --workload spgemm64k --steps 50 --warmup 5 > $O/prof64.log 2>&1 || { tail -20 $O/prof64.log; exit 1; }
-cp $(find /tmp/pp29b -name "*kernel_stats.csv" | head -1) $O/spgemm64k_kernel_stats.csv
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/ppva -o prof --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 > $O/prof1m.log 2>&1 || { tail -20 $O/prof1m.log; exit 1; }
+cp $(find /tmp/ppva -name "*kernel_stats.csv" | head -1) $O/spgemm1m_kernel_stats.csv
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/ppvb -o prof --output-format csv -- python3 $R/bench.py --workload spgemm64k --steps 50 --warmup 5 > $O/prof64.log 2>&1 || { tail -20 $O/prof64.log; exit 1; }
+cp $(find /tmp/ppvb -name "*kernel_stats.csv" | head -1) $O/spgemm64k_kernel_stats.csv
 echo profiles done

@@ -1,12 +1,12 @@
 """Long-row statistics of R-MAT A.A^T: rows by log2(products), their A entries, entries
 on long B rows (>= 4 per 2^15-column chunk) and the products those carry.
-usage: python tools/r5/rmat_rows.py [scale]"""
+usage: python tools/rmat_rows.py [scale]"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import spmm_amd  # noqa: F401,E402
 from spmm_amd.ops import spgemm as SG  # noqa: E402
 from spmm_amd.utils import gen_csr  # noqa: E402

@@ -1,13 +1,13 @@
 """R-MAT A.A^T: build the problem, run K streamed steps (consume = count nnz only, as the
 timed bench step), print ms per step.  For kernel profiles of the step alone (no setup
-checksum).  usage: python tools/r5/rmat_steps.py [scale] [steps]"""
+checksum).  usage: python tools/rmat_steps.py [scale] [steps]"""
 import sys
 import time
 
 import torch
 
 import os  # noqa: E402
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import spmm_amd  # noqa: F401,E402
 from spmm_amd.models import spgemm as MS  # noqa: E402
 from spmm_amd.parallel import comm as CM  # noqa: E402
