@@ -782,8 +782,17 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         bool tri = false;
         for (int i0 = 0; i0 < nr; i0 += RR) {
           fetch(i0, nr, TC, clo);
+          // the value adds: one compare-swap try each, ds_add_f32 for the lanes that lost (the
+          // reload's adds land on distinct slots almost always: ~3x fewer LDS cycles than
+          // ds_add_f32 alone, common.hpp lds_fadd_n)
+          int ri[RR];
+          float rv[RR];
+          bool rf[RR];
 #pragma unroll
           for (int d = 0; d < RR; ++d) {
+            ri[d] = -1;
+            rv[d] = v[d];
+            rf[d] = false;
             if (c[d] >= 0) {
               const int rr = rank(c[d]);
               uint32_t* cw = reinterpret_cast<uint32_t*>(&items[rr]);
@@ -793,9 +802,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
               } else {
                 cw[0] = (uint32_t)(c[d] + clo);
               }
-              atomicAdd(reinterpret_cast<float*>(&items[rr]) + 1, v[d]);
+              ri[d] = 2 * rr + 1;
             }
           }
+          spmm::lds_fadd_n(reinterpret_cast<float*>(items), ri, rv, rf);
         }
         if (DET && tri) sfix = 1;
       }
