@@ -123,7 +123,7 @@ struct LdsGeom {
   static constexpr int NWIN = TS / 64;
   static_assert(((TS + 63) >> 6) + NT <= CCAP, "descriptor buffer too small even for 64-lane chunks");
   static_assert(NWIN <= CCAP, "window counts reuse the descriptor buffer");
-  static_assert(NT <= 512, "entry index is 9 bits in a chunk descriptor");
+  static_assert(NT <= 1024, "entry index is 10 bits in a chunk descriptor");
 };
 
 // Chunk count of this thread's entry and one block scan giving the chunk
@@ -164,11 +164,13 @@ __device__ __forceinline__ void stage_batch(const int32_t* __restrict__ Aci, con
 }
 
 
+// A chunk descriptor: entry index (bits 0-9: workgroups of up to 1024 threads), lanes
+// (10-16), chunk of the entry (17-30).
 __device__ __forceinline__ void write_chunks(int* clist, int len, int nch, int pre, int lgE) {
   const int G = 1 << lgE;
   for (int k = 0; k < nch; ++k) {
     const int lim = (len - (k << lgE)) < G ? (len - (k << lgE)) : G;
-    clist[pre + k] = threadIdx.x | (lim << 9) | (k << 16);
+    clist[pre + k] = threadIdx.x | (lim << 10) | (k << 17);
   }
 }
 
@@ -188,13 +190,13 @@ __device__ __forceinline__ void fetch_chunks(int i0, int gid, int ngrp, int gl, 
   int64_t eb[D];
 #pragma unroll
   for (int u = 0; u < D; ++u) {
-    eb[u] = abeg[d[u] & 511];
-    if constexpr (VALUES) av[u] = aval[d[u] & 511];
+    eb[u] = abeg[d[u] & 1023];
+    if constexpr (VALUES) av[u] = aval[d[u] & 1023];
   }
   int64_t f[D];
 #pragma unroll
   for (int u = 0; u < D; ++u) {
-    const int lim = (d[u] >> 9) & 127, k = d[u] >> 16;
+    const int lim = (d[u] >> 10) & 127, k = d[u] >> 17;
     v[u] = (t[u] < TC) & (gl < lim);
     f[u] = v[u] ? eb[u] + (k << lgE) + gl : 0;   // 0: a valid B index (TC > 0); loads never predicated off
   }
@@ -580,7 +582,7 @@ __device__ __forceinline__ int64_t ord_lookback(unsigned long long* status, int6
 }
 
 template <int PCAP, int NT, int NP, bool ORD = false, int NBT = ESC_NB>
-__global__ __launch_bounds__(NT, 4) void spgemm_esc(
+__global__ __launch_bounds__(NT, NT >= 1024 ? 1 : 4) void spgemm_esc(
     const int64_t* __restrict__ Arp, const int32_t* __restrict__ Aci, const float* __restrict__ Av,
     const int64_t* __restrict__ Brp, const int32_t* __restrict__ Bci, const float* __restrict__ Bv,
     const int64_t* __restrict__ bsplit, const int32_t* __restrict__ rows, int ncols, int lg,
@@ -596,6 +598,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_esc(
   static_assert(PCAP % 64 == 0 && PCAP < 65536, "16-bit bucket counters");
   static_assert(BPT % 2 == 0 && BPT <= 8, "a thread owns whole counter words, at most 8 buckets");
   static_assert(NWIN <= CCAP, "window counts reuse the descriptor buffer");
+  static_assert(NT <= 1024, "entry index is 10 bits in a chunk descriptor");
   __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];   // key (low) | value bits (high)
   __shared__ __attribute__((aligned(16))) uint32_t hist[NB / 2];            // two 16-bit counters per word
   __shared__ int64_t abeg[ACAP];
@@ -1952,6 +1955,15 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
 // per slice, esc_load per-slice margin from 2 slices up); beyond caps[10]: the long-row path.
 // Numeric rows of more than esc_min products skip the single-pass tables.
 constexpr int64_t kEscPcap = 7680;   // launch_esc<7680, ...>
+// Top numeric bin (8 slices): kEscTopPcap products a slice, the 512-thread kernel of bins
+// 7..9.  Diagnostic build -DSPMM_ESC_TOP_PCAP=15360: 1024-thread workgroups, 148 KB of LDS
+// (one per CU), R-MAT rows of 55K-110K products kept off the HBM long-row pipeline --
+// R-MAT 24 13.41 / 13.45 s vs 13.03 / 12.95 s a step (PERF_LOG round 5).
+#ifndef SPMM_ESC_TOP_PCAP
+#define SPMM_ESC_TOP_PCAP 7680
+#endif
+constexpr int64_t kEscTopPcap = SPMM_ESC_TOP_PCAP;
+static_assert(kEscTopPcap == 7680 || kEscTopPcap == 15360, "instantiated top-bin capacities");
 constexpr double kEscLoad = 0.9;
 SPMM_EXPORT int spmm_spgemm_bin_caps(int numeric, double load, double load_sliced, int64_t esc_min, int64_t* caps) {
   for (int b = 0; b < 7; ++b) {
@@ -1959,7 +1971,7 @@ SPMM_EXPORT int spmm_spgemm_bin_caps(int numeric, double load, double load_slice
     caps[b] = numeric ? std::min(c, esc_min) : c;
   }
   for (int k = 0; k < 4; ++k)
-    caps[7 + k] = numeric ? (k == 0 ? kEscPcap : (int64_t)(kEscLoad * kEscPcap) * (1 << k))
+    caps[7 + k] = numeric ? (k == 0 ? kEscPcap : (int64_t)(kEscLoad * (k == 3 ? kEscTopPcap : kEscPcap)) * (1 << k))
                           : (int64_t)(load_sliced * 16384) * (1 << k);
   return 0;
 }
@@ -2025,7 +2037,8 @@ SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, i
 // using bigger tables.
 //   symbolic bins 0..6: 128 << b keys, one pass; 7..10: 16384 keys x 1/2/4/8 slices
 //   numeric  bins 0..6: 128 << b key/value slots, one pass (ordered hash);
-//            7..10: bucketed ESC, 7680 products per slice x 1/2/4/8 slices
+//            7..10: bucketed ESC, 7680 products per slice x 1/2/4 slices, then
+//            kEscTopPcap x 8 slices
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
                                 const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz,
@@ -2042,7 +2055,7 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
     if (bin == 7) return launch_esc<7680, 512, 1>(SPMM_NARGS);
     if (bin == 8) return launch_esc<7680, 512, 2>(SPMM_NARGS);
     if (bin == 9) return launch_esc<7680, 512, 4>(SPMM_NARGS);
-    if (bin == 10) return launch_esc<7680, 512, 8>(SPMM_NARGS);
+    if (bin == 10) return launch_esc<(int)kEscTopPcap, (kEscTopPcap > 7680 ? 1024 : 512), 8>(SPMM_NARGS);
   } else {
     if (bin == 7) return launch_sym<16384, 512, 1>(SPMM_SARGS);
     if (bin == 8) return launch_sym<16384, 512, 2>(SPMM_SARGS);
