@@ -38,6 +38,22 @@
 
 using namespace spmm_bitmap;
 
+// Wave priority while a pipelined kernel stages the next unit and issues its gathers: the
+// other workgroups of the CU are in their VALU / LDS phases, so the raised waves get their
+// requests out first.  1M step 60.8-60.9 -> 58.8-58.9 ms, rank 0 of 8 9.43-9.51 -> 9.10-9.24 ms
+// (PERF_LOG round 5).  SPMM_BM_SETPRIO bits: 1 numeric, 2 count kernel (diagnostic builds).
+#ifndef SPMM_BM_SETPRIO
+#define SPMM_BM_SETPRIO 3
+#endif
+#define SPMM_BM_PRIO_HI(BIT) \
+  do {                       \
+    if ((SPMM_BM_SETPRIO) & (BIT)) __builtin_amdgcn_s_setprio(3); \
+  } while (0)
+#define SPMM_BM_PRIO_LO(BIT) \
+  do {                       \
+    if ((SPMM_BM_SETPRIO) & (BIT)) __builtin_amdgcn_s_setprio(0); \
+  } while (0)
+
 #ifndef SPMM_BM_ROWS_R   // register rounds of the row-major numeric kernel (chunk capacity 16 * R per unit)
 #define SPMM_BM_ROWS_R 10
 #endif
@@ -1736,8 +1752,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
         sq = q + 1;
       }
       if (more) {
+        SPMM_BM_PRIO_HI(1);
         stage();
         issue_loads();
+        SPMM_BM_PRIO_LO(1);
       } else {
         __syncthreads();   // this unit's pass 2 done before its slots are read
       }
@@ -2213,7 +2231,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     BM_STAMP(5);
     if (more) scan_end(LAST ? (row + NG) * nwin : row * nwin + 2 * (g + 1), LAST ? 0 : 2 * (g + 1));
     __syncthreads();   // E: the next unit's descriptors written
-    if (more) issue_loads();
+    if (more) {
+      SPMM_BM_PRIO_HI(2);
+      issue_loads();
+      SPMM_BM_PRIO_LO(2);
+    }
     // ---- popcount of this wave's bitmap rows (unit k), clearing them ------
     int cnt = 0;
     if (P != 0) {   // uniform (an empty unit left the bitmap clean)
