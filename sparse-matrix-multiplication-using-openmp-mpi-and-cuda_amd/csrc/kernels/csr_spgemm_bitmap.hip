@@ -41,9 +41,10 @@ using namespace spmm_bitmap;
 // Wave priority while a pipelined kernel stages the next unit and issues its gathers: the
 // other workgroups of the CU are in their VALU / LDS phases, so the raised waves get their
 // requests out first.  1M step 60.8-60.9 -> 58.8-58.9 ms, rank 0 of 8 9.43-9.51 -> 9.10-9.24 ms
-// (PERF_LOG round 5).  SPMM_BM_SETPRIO bits: 1 numeric, 2 count kernel (diagnostic builds).
+// (PERF_LOG round 5).  SPMM_BM_SETPRIO bits: 1 numeric, 2 count kernel, 4 the per-unit
+// kernel's pass-1 gathers (diagnostic builds).
 #ifndef SPMM_BM_SETPRIO
-#define SPMM_BM_SETPRIO 3
+#define SPMM_BM_SETPRIO 7
 #endif
 #define SPMM_BM_PRIO_HI(BIT) \
   do {                       \
@@ -665,7 +666,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       const int nr = (TC + ngrp - 1) / ngrp;
       uint32_t dupm = 0;
       if constexpr (MODE == 1) {
+        SPMM_BM_PRIO_HI(4);
         fetch(0, nr, TC, clo);
+        SPMM_BM_PRIO_LO(4);
         dupm = or_all();
       } else {
         for (int i0 = 0; i0 < nr; i0 += RR) {
