@@ -46,9 +46,12 @@ using namespace spmm_bitmap;
 #ifndef SPMM_BM_SETPRIO
 #define SPMM_BM_SETPRIO 7
 #endif
+#ifndef SPMM_BM_PRIO_LEVEL
+#define SPMM_BM_PRIO_LEVEL 3
+#endif
 #define SPMM_BM_PRIO_HI(BIT) \
   do {                       \
-    if ((SPMM_BM_SETPRIO) & (BIT)) __builtin_amdgcn_s_setprio(3); \
+    if ((SPMM_BM_SETPRIO) & (BIT)) __builtin_amdgcn_s_setprio(SPMM_BM_PRIO_LEVEL); \
   } while (0)
 #define SPMM_BM_PRIO_LO(BIT) \
   do {                       \
