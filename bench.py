@@ -74,19 +74,23 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
     flops_local = info.flops
     del C
     graph = None
-    if not comm.is_dist and comm.device.type == "cuda" and args.decomp != "inner" and args.graph == "on":
-        # one GPU: the product's kernels (splits, count, scan, numeric) replayed
-        # from a captured HIP graph, no host synchronisation inside the step
+    if comm.device.type == "cuda" and args.decomp != "inner" and args.graph == "on" and (
+            not comm.is_dist or comm.device_collectives):
+        # the product's kernels (splits, count, scan, numeric) replayed from
+        # captured HIP graphs, no host synchronisation inside the step; on N
+        # ranks (RowblockGraph) the two payload all-gathers run between the
+        # graphs, every step
         import torch
 
         from spmm_amd.ops.spgemm import SpgemmGraph
 
         try:
             torch.cuda.empty_cache()
-            graph = SpgemmGraph(prob.A, prob.B)
+            graph = MS.RowblockGraph(prob.A, prob.B, comm) if comm.is_dist else SpgemmGraph(prob.A, prob.B)
             step = lambda: graph.run()  # noqa: E731
-        except Exception as e:   # noqa: BLE001  (no graph for this product: eager steps, said so)
-            print(f"[bench] spgemm graph unavailable ({e}); eager steps", file=sys.stderr, flush=True)
+        except ValueError as e:   # (no graph for this product on some rank: every rank takes eager steps, said so)
+            if comm.rank == 0:
+                print(f"[bench] spgemm graph unavailable ({e}); eager steps", file=sys.stderr, flush=True)
             graph = None
             torch.cuda.empty_cache()
 
@@ -94,9 +98,11 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
             """After the timed loop: (1) the last replay's C equals an eager
             product's (row pointer and column sum exactly, value sum to fp32
             accumulation-order tolerance); (2) the eager step -- row-plan
-            inspector, three host read-backs, exact C allocation: everything
-            the graph does once at capture -- timed on its own and reported
-            next to the replayed step as ``eager_ms_per_step``."""
+            inspector, host read-backs, exact C allocation (and on N ranks the
+            size / row-count gathers): everything the graph does once at
+            construction -- timed on its own and reported next to the
+            replayed step as ``eager_ms_per_step`` (5 steps, not the timed
+            loop: a sanity field, not a like-for-like number)."""
             if graph is None:
                 return {}
             gi = SpgemmInfo()
@@ -110,7 +116,7 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
             ne = max(1, min(args.steps, 5))
             Ce = eager_step()   # (warm: allocator)
             del Ce
-            torch.cuda.synchronize()
+            _sync_barrier(comm)
             t = time.perf_counter()
             for _ in range(ne):
                 Ce = None
@@ -126,7 +132,7 @@ def run_spgemm(comm, args, n: int, density: float, model: str):
                                  f"col sums {g_col} / {e_col}, value sums {g_val} / {e_val}")
             return dict(graph_replay_nnz=gi.nnz, bitmap_cfg=gi.rows_per_bin_num.get("bitmap_cfg"),
                         bitmap_deferred=gi.rows_per_bin_num.get("bitmap_deferred"),
-                        eager_ms_per_step=round(eager_ms, 3),
+                        eager_ms_per_step=round(comm.allreduce_max(eager_ms), 3),
                         graph_vs_eager_check=dict(rowptr_equal=same_rp, col_sum=e_col, val_sum=e_val))
         if graph is not None:
             step.verify = verify

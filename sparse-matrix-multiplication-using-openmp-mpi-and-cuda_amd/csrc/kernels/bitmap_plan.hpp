@@ -10,7 +10,6 @@ struct SpmmBmOpts {
   int32_t mode;            // 0 off, 1 auto, 2 on (SPMM_SPGEMM_BITMAP)
   int32_t cfg;             // window configuration, -1 = pick from the mean row products
   int32_t rows_mode;       // row-major kernels: 0 off, 1 auto, 2 on
-  int32_t count_windows;   // windows per row-count unit
   int32_t det;             // deterministic summation order
   int32_t pad;             // padded 128-byte B segments
   int32_t cv;              // interleaved (column, value) pairs for the numeric kernels

@@ -96,9 +96,7 @@ __device__ __forceinline__ uint64_t spec_mac(uint64_t acc, uint64_t a, uint64_t 
 // keep ds_add_f32: their adding lanes mostly collide (1M step 61.4 vs 62.6 ms with the try).
 // N independent adds base[idx[u]] += v[u] (idx < 0: none): all reads, then all compare-swap
 // tries in flight together, then ds_add_f32 for the lanes that lost.
-#ifndef SPMM_LDS_FADD_TRIES
-#define SPMM_LDS_FADD_TRIES 1
-#endif
+// (Two / three tries before the fallback measured within run-to-run spread: one try.)
 // fresh[u]: the slot is known to hold +0.0 (its occupancy bit was clear): no read.
 template <int N>
 __device__ __forceinline__ void lds_fadd_n(float* base, const int (&idx)[N], const float (&v)[N],
@@ -117,17 +115,6 @@ __device__ __forceinline__ void lds_fadd_n(float* base, const int (&idx)[N], con
       old[u] = prev;
     }
   }
-#if SPMM_LDS_FADD_TRIES > 1   // (diagnostic builds) further tries with the value the lost try returned
-  for (int t = 1; t < SPMM_LDS_FADD_TRIES; ++t) {
-#pragma unroll
-    for (int u = 0; u < N; ++u)
-      if (lost[u]) {
-        const uint32_t prev = atomicCAS(q + idx[u], old[u], __float_as_uint(__uint_as_float(old[u]) + v[u]));
-        lost[u] = prev != old[u];
-        old[u] = prev;
-      }
-  }
-#endif
 #pragma unroll
   for (int u = 0; u < N; ++u)
     if (lost[u]) atomicAdd(base + idx[u], v[u]);

@@ -89,7 +89,7 @@ T* at(void* ws, int64_t off) {
 }  // namespace
 
 // Options from the environment, with the defaults of utils/config.py (the same variables:
-// SPMM_SPGEMM_BITMAP, _CFG, _ROWS, _COUNT_WINDOWS, _PAD, _CV, _PIPE, SPMM_SPGEMM_DETERMINISTIC;
+// SPMM_SPGEMM_BITMAP, _CFG, _ROWS, _PAD, _CV, _PIPE, SPMM_SPGEMM_DETERMINISTIC;
 // tests/test_spgemm.py checks the two sets of defaults agree).  For the native engine.
 SPMM_EXPORT int spmm_spgemm_bm_env_opts(SpmmBmOpts* o) {
   auto num = [](const char* k, int d) {
@@ -104,7 +104,6 @@ SPMM_EXPORT int spmm_spgemm_bm_env_opts(SpmmBmOpts* o) {
   o->mode = tri("SPMM_SPGEMM_BITMAP");
   o->cfg = num("SPMM_SPGEMM_BITMAP_CFG", -1);
   o->rows_mode = tri("SPMM_SPGEMM_BITMAP_ROWS");
-  o->count_windows = num("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2);
   o->det = num("SPMM_SPGEMM_DETERMINISTIC", 0) > 0;
   o->pad = num("SPMM_SPGEMM_BITMAP_PAD", 1) > 0;
   o->cv = num("SPMM_SPGEMM_BITMAP_CV", 1) != 0;
@@ -144,9 +143,9 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   if (m * nwin >= ((int64_t)1 << 31)) return 1;
   const double seg = mean_seg > 0 ? mean_seg : (double)bnnz / (double)std::max<int64_t>(mb, 1);
   const bool ws8_ok = nwin <= 8 && o->rows_mode != 0;
-  // windows per row-count unit: the count kernels exist for 1, 2 and 4 (other requests: 2)
-  const int cw = (o->count_windows == 1 || o->count_windows == 4) ? o->count_windows : 2;
-  const int nsub_c = nwin >= 2 ? cw : 1;
+  // windows per row-count unit: two (a B row's two-window segment read once for both; units of
+  // 1 / 4 windows measured slower, PERF_LOG rounds 4-5), one when the row has one window
+  const int nsub_c = nwin >= 2 ? 2 : 1;
   const double sl = seg * nsub_c / nwin;   // B-segment length per row-count unit
   p->cfg = cfg;
   p->lgw = k.lgw;

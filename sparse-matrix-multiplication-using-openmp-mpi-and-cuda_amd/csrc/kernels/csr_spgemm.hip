@@ -1955,15 +1955,9 @@ SPMM_EXPORT int spmm_spgemm_row_nprod(const int64_t* Arp, const int32_t* Aci, co
 // per slice, esc_load per-slice margin from 2 slices up); beyond caps[10]: the long-row path.
 // Numeric rows of more than esc_min products skip the single-pass tables.
 constexpr int64_t kEscPcap = 7680;   // launch_esc<7680, ...>
-// Top numeric bin (8 slices): kEscTopPcap products a slice, the 512-thread kernel of bins
-// 7..9.  Diagnostic build -DSPMM_ESC_TOP_PCAP=15360: 1024-thread workgroups, 148 KB of LDS
-// (one per CU), R-MAT rows of 55K-110K products kept off the HBM long-row pipeline --
-// R-MAT 24 13.41 / 13.45 s vs 13.03 / 12.95 s a step (PERF_LOG round 5).
-#ifndef SPMM_ESC_TOP_PCAP
-#define SPMM_ESC_TOP_PCAP 7680
-#endif
-constexpr int64_t kEscTopPcap = SPMM_ESC_TOP_PCAP;
-static_assert(kEscTopPcap == 7680 || kEscTopPcap == 15360, "instantiated top-bin capacities");
+// (A 15360-product top bin on 1024-thread workgroups, which keeps R-MAT rows of 55K-110K
+// products off the long-row pipeline, measured slower: R-MAT 24 13.41 / 13.45 s vs 13.03 /
+// 12.95 s a step, PERF_LOG round 5; removed.)
 constexpr double kEscLoad = 0.9;
 SPMM_EXPORT int spmm_spgemm_bin_caps(int numeric, double load, double load_sliced, int64_t esc_min, int64_t* caps) {
   for (int b = 0; b < 7; ++b) {
@@ -1971,7 +1965,7 @@ SPMM_EXPORT int spmm_spgemm_bin_caps(int numeric, double load, double load_slice
     caps[b] = numeric ? std::min(c, esc_min) : c;
   }
   for (int k = 0; k < 4; ++k)
-    caps[7 + k] = numeric ? (k == 0 ? kEscPcap : (int64_t)(kEscLoad * (k == 3 ? kEscTopPcap : kEscPcap)) * (1 << k))
+    caps[7 + k] = numeric ? (k == 0 ? kEscPcap : (int64_t)(kEscLoad * kEscPcap) * (1 << k))
                           : (int64_t)(load_sliced * 16384) * (1 << k);
   return 0;
 }
@@ -2037,8 +2031,7 @@ SPMM_EXPORT int spmm_spgemm_row_splits(const int64_t* Brp, const int32_t* Bci, i
 // using bigger tables.
 //   symbolic bins 0..6: 128 << b keys, one pass; 7..10: 16384 keys x 1/2/4/8 slices
 //   numeric  bins 0..6: 128 << b key/value slots, one pass (ordered hash);
-//            7..10: bucketed ESC, 7680 products per slice x 1/2/4 slices, then
-//            kEscTopPcap x 8 slices
+//            7..10: bucketed ESC, 7680 products per slice x 1/2/4/8 slices
 SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                 const int64_t* Brp, const int32_t* Bci, const float* Bv, const int64_t* bsplit,
                                 const int32_t* rows, int64_t nrows, int ncols, int lg, int32_t* row_nnz,
@@ -2055,7 +2048,7 @@ SPMM_EXPORT int spmm_spgemm_lds(int bin, int numeric, const int64_t* Arp, const 
     if (bin == 7) return launch_esc<7680, 512, 1>(SPMM_NARGS);
     if (bin == 8) return launch_esc<7680, 512, 2>(SPMM_NARGS);
     if (bin == 9) return launch_esc<7680, 512, 4>(SPMM_NARGS);
-    if (bin == 10) return launch_esc<(int)kEscTopPcap, (kEscTopPcap > 7680 ? 1024 : 512), 8>(SPMM_NARGS);
+    if (bin == 10) return launch_esc<7680, 512, 8>(SPMM_NARGS);
   } else {
     if (bin == 7) return launch_sym<16384, 512, 1>(SPMM_SARGS);
     if (bin == 8) return launch_sym<16384, 512, 2>(SPMM_SARGS);

@@ -38,37 +38,23 @@
 
 using namespace spmm_bitmap;
 
-// Wave priority while a pipelined kernel stages the next unit and issues its gathers: the
-// other workgroups of the CU are in their VALU / LDS phases, so the raised waves get their
-// requests out first.  1M step 60.8-60.9 -> 58.8-58.9 ms, rank 0 of 8 9.43-9.51 -> 9.10-9.24 ms
-// (PERF_LOG round 5).  SPMM_BM_SETPRIO bits: 1 numeric, 2 count kernel, 4 the per-unit
-// kernel's pass-1 gathers (diagnostic builds).
-#ifndef SPMM_BM_SETPRIO
-#define SPMM_BM_SETPRIO 7
-#endif
-#ifndef SPMM_BM_PRIO_LEVEL
-#define SPMM_BM_PRIO_LEVEL 3
-#endif
-#define SPMM_BM_PRIO_HI(BIT) \
-  do {                       \
-    if ((SPMM_BM_SETPRIO) & (BIT)) __builtin_amdgcn_s_setprio(SPMM_BM_PRIO_LEVEL); \
-  } while (0)
-#define SPMM_BM_PRIO_LO(BIT) \
-  do {                       \
-    if ((SPMM_BM_SETPRIO) & (BIT)) __builtin_amdgcn_s_setprio(0); \
-  } while (0)
+// Wave priority while a kernel stages the next unit and issues its gathers: the other
+// workgroups of the CU are in their VALU / LDS phases, so the raised waves get their
+// requests out first.  1M step 60.8-60.9 -> 58.8-58.9 ms, rank 0 of 8 9.43-9.51 -> 9.10-9.24 ms;
+// any level 1-3 measures the same (PERF_LOG round 5).
+#define SPMM_BM_PRIO_HI() __builtin_amdgcn_s_setprio(3)
+#define SPMM_BM_PRIO_LO() __builtin_amdgcn_s_setprio(0)
 
+// Build-time geometry (every value below was swept in PERF_LOG rounds 3-5; tools/bm_variants.py
+// builds diagnostic variants of these, normal builds never override them):
 #ifndef SPMM_BM_ROWS_R   // register rounds of the row-major numeric kernel (chunk capacity 16 * R per unit)
 #define SPMM_BM_ROWS_R 10
 #endif
-
-#ifndef SPMM_BM_SWEEP_G   // numeric rank prefix: bitmap words per lane and scan step (1, 2, 4 or 8)
-#define SPMM_BM_SWEEP_G 2
-#endif
-
-#ifndef SPMM_BM_P2_G   // per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity)
-#define SPMM_BM_P2_G 2   // 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586 (fewer empty rounds past the chunk count); 7 spills
-#endif
+// numeric rank prefix: bitmap words per lane and scan step (2 and 4 measured identical)
+constexpr int kSweepG = 2;
+// per-unit pass 2: rank lookups in flight per group of rounds (and the skip granularity;
+// 65536^2: 2 = 1.547 / 1.556 ms vs 4 = 1.562 / 1.586, 7 spills)
+constexpr int kP2G = 2;
 
 #define BM_OUT(ptr, val) __builtin_nontemporal_store((val), (ptr))
 
@@ -150,6 +136,10 @@ __device__ __forceinline__ void bm_write_unit(const unsigned long long* items, i
 // that delimit it, in registers, flushed once at the end; [7] counts units.
 __device__ int g_bm_stamp_on = 0;
 __device__ unsigned long long g_bm_stamps[8];
+// per workgroup of the pipelined numeric kernel (stamps build): start / end of its row loop on
+// the 100 MHz real-time counter (one clock for every XCD), XCD id << 32 | units formed
+constexpr int kBmWgMax = 8192;
+__device__ unsigned long long g_bm_wg[3 * kBmWgMax];
 #ifdef SPMM_BM_STAMPS
 #define BM_STAMP_DECL                                                              \
   const int stamp_on = g_bm_stamp_on;                                              \
@@ -167,11 +157,22 @@ __device__ unsigned long long g_bm_stamps[8];
 #define BM_STAMP_FLUSH()                                                           \
   if (stamp_on && threadIdx.x == 0)                                                \
     for (int i = 0; i < 8; ++i) atomicAdd(&g_bm_stamps[i], st_acc[i])
+#define BM_WG_DECL const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+#define BM_WG_FLUSH()                                                              \
+  if (stamp_on && threadIdx.x == 0 && blockIdx.x < kBmWgMax) {                      \
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();                 \
+    const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u; \
+    atomicExch(&g_bm_wg[3 * blockIdx.x], wg_t0);                                    \
+    atomicExch(&g_bm_wg[3 * blockIdx.x + 1], t1);                                   \
+    atomicExch(&g_bm_wg[3 * blockIdx.x + 2], ((unsigned long long)xcc << 32) | st_acc[7]); \
+  }
 #else
 #define BM_STAMP_DECL
 #define BM_STAMP(i) do {} while (0)
 #define BM_STAMP_UNIT() do {} while (0)
 #define BM_STAMP_FLUSH() do {} while (0)
+#define BM_WG_DECL
+#define BM_WG_FLUSH() do {} while (0)
 #endif
 
 // ---- deterministic mode (DET kernels) ---------------------------------------
@@ -669,9 +670,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       const int nr = (TC + ngrp - 1) / ngrp;
       uint32_t dupm = 0;
       if constexpr (MODE == 1) {
-        SPMM_BM_PRIO_HI(4);
+        SPMM_BM_PRIO_HI();
         fetch(0, nr, TC, clo);
-        SPMM_BM_PRIO_LO(4);
+        SPMM_BM_PRIO_LO();
         dupm = or_all();
       } else {
         for (int i0 = 0; i0 < nr; i0 += RR) {
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       // ---- rank prefix per 64-bit word: wave w owns words [w*WPW, (w+1)*WPW)
       // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
       // wave scan of their sum, 16-bit prefixes stored SG at a time)
-      constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+      constexpr int SG = (kSweepG > 1 && WPW % (64 * kSweepG) == 0) ? kSweepG : 1;
       constexpr bool PAIRS = SG > 1;
       int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
       int wtot = 0;
@@ -765,7 +766,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       };
       if constexpr (MODE == 1) {
         // ranks of P2G rounds at a time (their LDS reads in flight together)
-        constexpr int P2G = SPMM_BM_P2_G;
+        constexpr int P2G = kP2G;
 #pragma unroll
         for (int d0 = 0; d0 < RR; d0 += P2G) {
           if (d0 >= nr * PPL) break;   // uniform: slots past the unit's chunks hold no product
@@ -1178,7 +1179,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
       // ---- rank prefix per 64-bit word ---------------------------------
       // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
       // wave scan of their sum, 16-bit prefixes stored SG at a time)
-      constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+      constexpr int SG = (kSweepG > 1 && WPW % (64 * kSweepG) == 0) ? kSweepG : 1;
       constexpr bool PAIRS = SG > 1;
       int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
       int wtot = 0;
@@ -1370,7 +1371,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   constexpr int RL = RR / 2;     // load rounds (two pairs per lane and load)
   constexpr int NWR = (PCAP + 4 * NT - 1) / (4 * NT);   // write-out rounds: four entries per lane and round
   static_assert(RR % 2 == 0 && WPW % 64 == 0 && PCAP < 65536, "geometry");
-  constexpr int SG = (SPMM_BM_SWEEP_G > 1 && WPW % (64 * SPMM_BM_SWEEP_G) == 0) ? SPMM_BM_SWEEP_G : 1;
+  constexpr int SG = (kSweepG > 1 && WPW % (64 * kSweepG) == 0) ? kSweepG : 1;
   constexpr bool PAIRS = SG > 1;
 
   __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
@@ -1395,6 +1396,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   const int nwin = p.nwin;
   uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
   BM_STAMP_DECL
+  BM_WG_DECL
   if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
   const auto rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(p.Bcv), 0, (int)pa.bcv_bytes, 0x00020000);
 
@@ -1758,10 +1760,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
         sq = q + 1;
       }
       if (more) {
-        SPMM_BM_PRIO_HI(1);
+        SPMM_BM_PRIO_HI();
         stage();
         issue_loads();
-        SPMM_BM_PRIO_LO(1);
+        SPMM_BM_PRIO_LO();
       } else {
         __syncthreads();   // this unit's pass 2 done before its slots are read
       }
@@ -1774,6 +1776,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
     unit(std::true_type{}, row, nwin - 1);
   }
   BM_STAMP_FLUSH();
+  BM_WG_FLUSH();
 }
 
 // ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
@@ -2238,9 +2241,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     if (more) scan_end(LAST ? (row + NG) * nwin : row * nwin + 2 * (g + 1), LAST ? 0 : 2 * (g + 1));
     __syncthreads();   // E: the next unit's descriptors written
     if (more) {
-      SPMM_BM_PRIO_HI(2);
+      SPMM_BM_PRIO_HI();
       issue_loads();
-      SPMM_BM_PRIO_LO(2);
+      SPMM_BM_PRIO_LO();
     }
     // ---- popcount of this wave's bitmap rows (unit k), clearing them ------
     int cnt = 0;
@@ -2254,7 +2257,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
       cnt = __builtin_amdgcn_readlane(bm_wave_incl(cnt), 63);
     }
     if (lane == 0) csum[w] = cnt;
-    if (TC > CCAP && tid == 0) atomicOr(p.err, 2);   // (never: A rows <= NT entries, checked by the host)
+    // a unit of more chunks than the descriptor buffer (long two-window segments under a
+    // 256-entry A row): its count is short -> err bit 6, the host recounts the product on
+    // the flat row kernel, which takes descriptors in batches (a batch loop here changes
+    // hipcc's schedule of the ORs above: every OR became its own branch)
+    if (TC > CCAP && tid == 0) atomicOr(p.err, 64);
     __syncthreads();   // F: bitmap clear for the next ORs, csum written
     // ucnt of unit k's windows: one buffer store per wave (lanes past NSUB, other waves: dropped)
     int t = 0;
@@ -2407,7 +2414,6 @@ template <int C>
 int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s) {
   using K1 = BmRowCountKernel<C, 1>;
   using K2 = BmRowCountKernel<C, 2>;
-  using K4 = BmRowCountKernel<C, 4>;
   const int64_t colp_bytes = ra.a.cap * 4;
   // (pipelined from two units per row up: with one, every unit is a row's last and the
   // pipeline only adds work -- 65536^2 count 1.32 -> 1.36 ms step, PERF_LOG round 5)
@@ -2416,10 +2422,8 @@ int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s)
     return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz}, ra.a.m, s,
                        BmRowCountPipe<C>::NT);
   if (ra.pad)
-    return nsub == 4 ? launch_rows(K4::kp, ra, s, K4::NT)
-                     : (nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT));
-  return nsub == 4 ? launch_rows(K4::k, ra, s, K4::NT)
-                   : (nsub == 2 ? launch_rows(K2::k, ra, s, K2::NT) : launch_rows(K1::k, ra, s, K1::NT));
+    return nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT);
+  return nsub == 2 ? launch_rows(K2::k, ra, s, K2::NT) : launch_rows(K1::k, ra, s, K1::NT);
 }
 
 // det: the deterministic kernels (fixed summation order)
@@ -2524,6 +2528,19 @@ SPMM_EXPORT int spmm_spgemm_bm_stamps(int on, unsigned long long* out8) {
   return (int)e;
 }
 
+// Diagnostics (stamps build): per-workgroup {start, end, xcd << 32 | units} of the last
+// pipelined numeric launch, n <= kBmWgMax workgroups; on = 1 clears them first.
+SPMM_EXPORT int spmm_spgemm_bm_wg_times(int on, unsigned long long* out, int n) {
+  if (n < 0 || n > kBmWgMax) return (int)hipErrorInvalidValue;
+  if (on) {
+    static unsigned long long z[3 * kBmWgMax];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_bm_wg), z, sizeof z);
+  }
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bm_wg), 3 * (size_t)n * sizeof(unsigned long long));
+  return (int)e;
+}
+
 // Row-major numeric (nwin <= 8, ws8 from spmm_spgemm_bm_pack_ws8), then the
 // reload kernel over the deferred units; same contract as spmm_spgemm_bm_numeric.
 // Bcv: optional [nnz(B)] (column, value bits) pairs read by the row-major kernel.
@@ -2564,7 +2581,7 @@ SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int
                       nullptr, 0, nnzb, nullptr, err},
                (const uint4*)ws8, pad ? 1 : 0};
   hipStream_t s = (hipStream_t)stream;
-  if (nsub != 1 && nsub != 2 && nsub != 4) return (int)hipErrorInvalidValue;
+  if (nsub != 1 && nsub != 2) return (int)hipErrorInvalidValue;
   switch (cfg) {
     case 0: return bm_count_rows<0>(ra, nsub, pipe, annz, s);
     case 1: return bm_count_rows<1>(ra, nsub, pipe, annz, s);

@@ -284,7 +284,26 @@ __global__ __launch_bounds__(PT) void bsr_emit(const uint64_t* __restrict__ code
 
 unsigned grid(int64_t n) { return (unsigned)((n + PT - 1) / PT); }
 
+// One wave that returns after `ticks` of the 100 MHz real-time counter (a bounded wait: the
+// loop ends whatever the clock does, after at most 2^31 polls): a stand-in for a link
+// transfer's duration on a stream (tools/rank_emulate.py models the all-gather with it).
+__global__ __launch_bounds__(64) void prim_spin(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < (1 << 31) - 1; ++i) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
 }  // namespace
+
+// Stream-ordered delay of `us` microseconds on one wave (diagnostics / emulation).
+SPMM_EXPORT int spmm_prim_spin(double us, void* stream) {
+  if (!(us > 0)) return 0;
+  hipLaunchKernelGGL(prim_spin, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint64_t)(us * 100.0));
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
 
 // ---- exports ----------------------------------------------------------------
 SPMM_EXPORT size_t spmm_prim_scan_ws(int64_t n) { return scan_ws(n); }

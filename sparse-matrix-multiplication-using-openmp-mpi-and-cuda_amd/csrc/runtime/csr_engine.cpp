@@ -156,7 +156,9 @@ bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
     const int64_t nnz = down(uoff.get() + p.nunits, 1, s)[0];   // the one sizing read-back
     const int e0 = down(z.get(), 1, s)[0];
     A4_CHECK((e0 & 32) == 0, "spgemm bitmap: padded B layout overflow");
-    if (e0 & 8) continue;   // a window segment of >= 65536 entries: per-unit kernels
+    // a window segment of >= 65536 entries (bit 3), or a count unit of more chunks than the
+    // pipelined count kernel's descriptors (bit 6): per-unit kernels
+    if (e0 & (8 | 64)) continue;
     if (e0 != 0) return false;
     A4_HIP(hipMemsetAsync(z.get(), 0, 4, s));
     DCsr C;
@@ -169,7 +171,10 @@ bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
                                            ws.get(), uoff.get(), z.get(), nnz, C.ci.get(), C.v.get(), s));
     const int e = down(z.get(), 1, s)[0];
     A4_CHECK((e & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
-    if (e & 5) return false;   // a unit beyond the reload kernel's budget: the binned path redoes the product
+    // a unit beyond the reload kernel's budget (bits 0 / 2), or, deterministic, a unit no
+    // deterministic kernel could form (bit 4: nothing was written for it): the binned path
+    // redoes the product (correct C; its fp32 sums are not in the fixed order)
+    if (e & (p.det ? 21 : 5)) return false;
     // row pointer: every nwin-th unit offset, gathered on the device
     C.rp = DevBuf<int64_t>((size_t)A.m + 1, s);
     A4_HIP(hipMemcpy2DAsync(C.rp.get(), sizeof(int64_t), uoff.get(), sizeof(int64_t) * p.nwin, sizeof(int64_t),

@@ -29,6 +29,7 @@ large relative to C (deep inner dimension, few products per output).
 from __future__ import annotations
 
 import itertools
+import threading
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Tuple
 
@@ -252,6 +253,174 @@ def rowblock_spgemm(A_panel: CSR, B_panel: CSR, comm: Comm, info: Optional[Spgem
     and row binning run."""
     B_meta, ready = allgather_operand_async(B_panel, comm)
     return spgemm(A_panel, B_meta, info, B_ready=ready)
+
+
+_CAPTURE_LOCK = threading.Lock()   # one graph capture at a time per process (loopback ranks are threads)
+
+
+def _agree(comm: Comm, ok: bool) -> bool:
+    """True on every rank iff ``ok`` on every rank (the ranks must take the
+    same collective sequence afterwards)."""
+    return comm.allreduce_sum(1.0 if ok else 0.0) == comm.world
+
+
+class RowblockGraph:
+    """The row-block SpGEMM step (B's panels all-gathered over RCCL, then
+    C_panel = A_panel . B on the bitmap-rank kernels) with NO host
+    synchronisation inside the step, for operands of fixed structure: the
+    reference's per-rank product + merge (sparse_matrix_mult.cu:437-571) as
+    an inspector / executor pair.
+
+    Built once per operand structure (collective: every rank constructs it):
+    the panel sizes and row counts are gathered here, once (the only host
+    read-backs), B's full row pointer is formed, the bitmap plan is made from
+    A's row plan against it, and every buffer the step touches is allocated
+    -- the send buffers, the [world, emax] receive buffers, B's unpacked
+    columns and values, the plan's workspace, C at its product-count bound.
+    Two HIP graphs are captured on a side stream:
+
+      graph 1: unpack the gathered columns, B's column layouts (window splits,
+               packed bounds, padded count columns), count kernel, unit scan;
+      graph 2: unpack the gathered values, padded pairs, numeric + reload.
+
+    ``run()`` = copy this rank's B panel (columns, value bits) into the send
+    buffers, start the two payload all-gathers (RCCL runs them in issue order
+    on its own stream), make the compute stream wait for the columns and
+    replay graph 1 -- the count kernel runs while the values cross xGMI --
+    then wait for the values and replay graph 2.  Every step re-gathers and
+    recomputes everything from the panels' current columns and values (only
+    the row counts are fixed); :meth:`result` reads the nnz and error bits
+    of the last step once.  A product that does not take the bitmap-rank
+    path raises ``ValueError`` on every rank (the caller runs the eager
+    ``rowblock_spgemm``)."""
+
+    def __init__(self, A_panel: CSR, B_panel: CSR, comm: Comm):
+        from ..ops import spgemm as SG
+
+        dev = A_panel.device
+        local_ok = (dev.type == "cuda" and comm.device_collectives and B_panel.col.dtype == torch.int32
+                    and B_panel.val.dtype == torch.float32 and A_panel.val.dtype == torch.float32)
+        if not _agree(comm, local_ok):
+            raise ValueError("RowblockGraph: fp32 / int32 GPU operands and device collectives on every rank")
+        W = comm.world
+        self.A, self.Bp, self.comm = A_panel, B_panel, comm
+        # ---- the operand structure: gathered once ---------------------------
+        meta = comm.all_gather(torch.tensor([B_panel.m, B_panel.nnz], dtype=torch.int64, device=dev)).view(-1, 2)
+        ms, nnzs = meta[:, 0].tolist(), meta[:, 1].tolist()
+        mmax, emax = max(ms), max(nnzs)
+        cbuf = torch.zeros(max(mmax, 1), dtype=torch.int64, device=dev)
+        cbuf[:B_panel.m] = B_panel.rowptr[1:] - B_panel.rowptr[:-1]
+        cnt = comm.all_gather(cbuf).view(W, -1)
+        m, nnz = sum(ms), sum(nnzs)
+        rowptr = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(torch.cat([cnt[r, :ms[r]] for r in range(W)]), 0, out=rowptr[1:])
+        self.B = CSR(m, B_panel.n, rowptr, torch.zeros(nnz, dtype=torch.int32, device=dev),
+                     torch.zeros(nnz, dtype=torch.float32, device=dev))
+        self.emax = emax
+        # ---- the plan (A's row plan reads only B's row pointer) --------------
+        plan = None
+        info = SG.SpgemmInfo()
+        if emax > 0 and A_panel.n == m and A_panel.nnz > 0:
+            nprod, _, st = SG.row_plan(A_panel, self.B)
+            tot, mx, nz, light, _h1, _h2, _h4, _h8, amax = st.tolist()[:9]
+            pre = dict(max=mx, nonempty=nz, light=light, amax=amax)
+            info.flops, info.mean_seg = 2 * tot, tot / max(A_panel.nnz, 1)
+            if SG._bitmap_ok(A_panel, self.B, tot, pre):
+                plan = SG._bitmap_plan(A_panel, self.B, info, pre)
+                if plan is not None and plan.det:
+                    plan = None
+        if not _agree(comm, plan is not None):
+            raise ValueError("RowblockGraph: the product does not take the bitmap-rank path on every rank")
+        self.plan, self.flops = plan, info.flops
+        self.cb = torch.zeros(emax, dtype=torch.int32, device=dev)
+        self.vb = torch.zeros(emax, dtype=torch.int32, device=dev)
+        self.gc = torch.empty(W * emax, dtype=torch.int32, device=dev)
+        self.gv = torch.empty(W * emax, dtype=torch.int32, device=dev)
+        self.base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=dev)
+        self.bufs = SG.bitmap_buffers(plan, dev, cap=max(plan.raw.tot, 1))
+        self.bufs["n"] = B_panel.n
+        self.gather_bytes = W * (2 * emax * 4)
+        # ---- one eager step (checks every launch and the kernels' error bits:
+        # a product the row kernels cannot take, or with units beyond the reload
+        # kernel, is not replayed), then the capture ---------------------------
+        self._step(None, None)
+        if not _agree(comm, int(self.bufs["z"][0]) == 0):
+            raise ValueError("RowblockGraph: the bitmap kernels flagged this product on a rank (eager steps)")
+        err = None
+        # (every rank past its eager launches before any captures, and each capture
+        # alone: in-process loopback ranks are threads of one device, and no thread
+        # may launch while another's capture is open)
+        comm.barrier()
+        try:
+            with _CAPTURE_LOCK:
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g1, stream=side, capture_error_mode="thread_local"):
+                    self._front()
+                with torch.cuda.graph(self.g2, stream=side, capture_error_mode="thread_local"):
+                    self._back()
+                torch.cuda.current_stream(dev).wait_stream(side)
+        except RuntimeError as e:   # (a capture failure on one rank: every rank takes the eager step)
+            err = e
+        comm.barrier()
+        if not _agree(comm, err is None):
+            raise ValueError(f"RowblockGraph: graph capture failed on a rank ({err})")
+
+    def _unpack(self, gc, gv) -> None:
+        from ..ops.spgemm import _native as _nat
+
+        W = self.comm.world
+        P = _nat.ptr
+        _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(
+            P(gc) if gc is not None else None, P(gv) if gv is not None else None, W, self.emax, P(self.base),
+            self.emax, P(self.B.col), P(self.B.val) if gv is not None else None, None, _nat.stream_ptr(self.A.device)),
+            "spgemm_bm_unpack_gathered")
+
+    def _front(self) -> None:
+        from ..ops import spgemm as SG
+
+        self._unpack(self.gc, None)
+        self.built = SG.bitmap_front(self.A, self.B, self.plan, self.bufs, values=False)
+
+    def _back(self) -> None:
+        from ..ops import spgemm as SG
+
+        self._unpack(None, self.gv)
+        SG.bitmap_back(self.A, self.B, self.plan, self.bufs, self.built)
+
+    def _step(self, g1, g2) -> dict:
+        n = self.Bp.nnz
+        if n:
+            self.cb[:n].copy_(self.Bp.col)
+            self.vb[:n].copy_(self.Bp.val.view(torch.int32))
+        rec = None
+        if GATHER_STATS.enabled:
+            rec = [self.gather_bytes, GATHER_STATS.mark(self.A.device), None]
+            GATHER_STATS.calls.append(rec)
+        wait_c = self.comm.all_gather_into(self.gc, self.cb)
+        wait_v = self.comm.all_gather_into(self.gv, self.vb)
+        wait_c()
+        g1.replay() if g1 is not None else self._front()
+        wait_v()
+        if rec is not None:
+            rec[2] = GATHER_STATS.mark(self.A.device)
+        g2.replay() if g2 is not None else self._back()
+        return self.bufs
+
+    def run(self) -> dict:
+        """One step: gathers + both graphs, no host synchronisation."""
+        return self._step(self.g1, self.g2)
+
+    def result(self, info: Optional[SpgemmInfo] = None) -> Optional[CSR]:
+        """This rank's C row panel of the last step (one read-back)."""
+        from ..ops import spgemm as SG
+
+        info = info if info is not None else SpgemmInfo()
+        C_ = SG._bitmap_finish(self.A, self.B, self.plan, self.bufs, info, True)
+        if isinstance(C_, str):
+            raise RuntimeError("RowblockGraph: B's window segments no longer fit the packed 16-bit lengths")
+        return C_
 
 
 def sparse_reduce_scatter(partial: CSR, comm: Comm, row_counts: List[int],

@@ -476,6 +476,7 @@ def _true_nnz(B: CSR) -> int:
     return max(B.nnz, getattr(B, "_nnz_total", 0))
 
 
+_native.register_hip("spmm_prim_spin", C.c_double, c_vp)
 _native.register_hip("spmm_prim_scan_ws", C_I64, restype=C.c_size_t)
 _native.register_hip("spmm_prim_scan", c_vp, C_INT, C_I64, c_vp, C_INT, c_vp, c_vp)
 
@@ -705,7 +706,7 @@ def onepass_ordered(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_rea
 
 
 class _BmOpts(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmOpts
-    _fields_ = [(n, C.c_int32) for n in ("mode", "cfg", "rows_mode", "count_windows", "det", "pad", "cv", "pipe",
+    _fields_ = [(n, C.c_int32) for n in ("mode", "cfg", "rows_mode", "det", "pad", "cv", "pipe",
                                          "use_ws8")]
 
 
@@ -731,7 +732,7 @@ def _bm_opts(use_ws8: bool = True) -> _BmOpts:
     tri = {"off": 0, "auto": 1, "on": 2}
     return _BmOpts(mode=tri.get(CONFIG.spgemm_bitmap, 1), cfg=CONFIG.spgemm_bitmap_cfg,
                    rows_mode=tri.get(CONFIG.spgemm_bitmap_rows, 1),
-                   count_windows=CONFIG.spgemm_bitmap_count_windows, det=int(CONFIG.spgemm_deterministic > 0),
+                   det=int(CONFIG.spgemm_deterministic > 0),
                    pad=int(CONFIG.spgemm_bitmap_pad > 0), cv=int(bool(CONFIG.spgemm_bitmap_cv)),
                    pipe=int(CONFIG.spgemm_bitmap_pipe > 0), use_ws8=int(use_ws8))
 
@@ -782,6 +783,45 @@ def _bitmap_plan(A: CSR, B: CSR, info: SpgemmInfo, pre: Optional[dict], use_ws8:
     return BitmapPlan(raw=p, opts=o)
 
 
+def bitmap_buffers(plan: BitmapPlan, dev: torch.device, cap: Optional[int] = None) -> dict:
+    """Device buffers of one bitmap-rank product: the plan's workspace, the
+    {error bits, deferred units} word pair, the unit offsets and (``cap``
+    given) C's arrays.  Allocated outside any capture, so the launches that
+    use them are graph-capturable as they are."""
+    raw = plan.raw
+    out = dict(ws=torch.empty(max(raw.ws_bytes, 1), dtype=torch.uint8, device=dev),
+               z=torch.empty(2, dtype=torch.int32, device=dev),   # err, deferred count (zeroed by the front)
+               uoff=torch.empty(raw.nunits + 1, dtype=torch.int64, device=dev), nunits=raw.nunits, ws8=bool(raw.ws8))
+    if cap is not None:
+        out.update(Cci=torch.empty(cap, dtype=torch.int32, device=dev),
+                   Cv=torch.empty(cap, dtype=torch.float32, device=dev), cap=cap)
+    return out
+
+
+def bitmap_front(A: CSR, B: CSR, plan: BitmapPlan, bufs: dict, values: bool) -> int:
+    """B layouts + count kernel + unit-offset scan (csr_bitmap_plan.hip front)
+    on the current stream; ``values``: B's values are readable (else only its
+    columns: the padded pairs are then built by :func:`bitmap_back`).
+    Returns whether the padded pairs were built."""
+    P = _native.ptr
+    built = C.c_int(0)
+    _native.check(_native.hip().spmm_spgemm_bm_front(
+        C.byref(plan.raw), P(A.rowptr), P(A.col), P(B.rowptr), P(B.col), P(B.val) if values else None,
+        P(bufs["ws"]), P(bufs["uoff"]), P(bufs["z"]), C.byref(built), _native.stream_ptr(A.device)),
+        "spgemm_bm_front")
+    return built.value
+
+
+def bitmap_back(A: CSR, B: CSR, plan: BitmapPlan, bufs: dict, built: int) -> None:
+    """Padded pairs (unless built by the front) + numeric and reload kernels
+    into ``bufs["Cci"] / ["Cv"]`` (csr_bitmap_plan.hip back)."""
+    P = _native.ptr
+    _native.check(_native.hip().spmm_spgemm_bm_back(
+        C.byref(plan.raw), P(A.rowptr), P(A.col), P(A.val), P(B.col), P(B.val), built, P(bufs["ws"]),
+        P(bufs["uoff"]), P(bufs["z"]), bufs["cap"], P(bufs["Cci"]), P(bufs["Cv"]), _native.stream_ptr(A.device)),
+        "spgemm_bm_back")
+
+
 def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, info: Optional[SpgemmInfo] = None) -> dict:
     """The kernels of one bitmap-rank product, launched by the native front /
     back (csr_bitmap_plan.hip) into one workspace.  ``lazy``: C at the product
@@ -791,39 +831,32 @@ def _bitmap_launch(A: CSR, B: CSR, plan: BitmapPlan, lazy: bool, B_ready=None, i
     dev = A.device
     if B_ready is not None:   # columns only: the values may still be in flight (two-stage gather)
         B = getattr(B_ready, "cols", B_ready)()
-    lib = _native.hip()
-    P = _native.ptr
-    st = _native.stream_ptr(dev)
     raw = plan.raw
-    ws = torch.empty(max(raw.ws_bytes, 1), dtype=torch.uint8, device=dev)
-    z = torch.empty(2, dtype=torch.int32, device=dev)   # err, deferred count (zeroed by the front)
-    uoff = torch.empty(raw.nunits + 1, dtype=torch.int64, device=dev)
+    out = bitmap_buffers(plan, dev)
     values_here = B_ready is None or getattr(B_ready, "local", False)
-    built = C.c_int(0)
-    _native.check(lib.spmm_spgemm_bm_front(C.byref(raw), P(A.rowptr), P(A.col), P(B.rowptr), P(B.col),
-                                           P(B.val) if values_here else None, P(ws), P(uoff), P(z), C.byref(built),
-                                           st), "spgemm_bm_front")
-    out = dict(uoff=uoff, z=z, nunits=raw.nunits, ws8=bool(raw.ws8))
+    built = bitmap_front(A, B, plan, out, values_here)
+    z, uoff = out["z"], out["uoff"]
     if not lazy:
         nnz, e0 = torch.stack([uoff[-1], z[0].long()]).tolist()   # one read-back
         if e0 & 32:
             raise RuntimeError("spgemm bitmap: padded B layout overflow (kernel invariant violated)")
         out.update(nnz=nnz)
-        if e0 & 8:   # a window segment does not fit 16 bits: per-unit kernels
+        # a window segment does not fit 16 bits (bit 3), or a count unit has more chunks
+        # than the pipelined count kernel's descriptors (bit 6): the per-unit kernels
+        if e0 & (8 | 64):
             out.update(truncated=True)
             return out
+        if e0:
+            raise RuntimeError(f"spgemm bitmap: count kernels flagged error bits {e0} (kernel invariant violated)")
         z[0].zero_()
     cap = max(raw.tot, 1) if lazy else out["nnz"]
     if B_ready is not None:   # the numeric kernels read the values
         B = B_ready()
-    Cci = torch.empty(cap, dtype=torch.int32, device=dev)
-    Cv = torch.empty(cap, dtype=torch.float32, device=dev)
-    _native.check(lib.spmm_spgemm_bm_back(C.byref(raw), P(A.rowptr), P(A.col), P(A.val), P(B.col), P(B.val),
-                                          built.value, P(ws), P(uoff), P(z), cap, P(Cci), P(Cv), st),
-                  "spgemm_bm_back")
+    out.update(Cci=torch.empty(cap, dtype=torch.int32, device=dev), Cv=torch.empty(cap, dtype=torch.float32, device=dev),
+               cap=cap, n=B.n)
+    bitmap_back(A, B, plan, out, built)
     if info is not None and raw.ws8 and raw.rows:
         info.rows_per_bin_num["bitmap_rows"] = 1
-    out.update(Cci=Cci, Cv=Cv, cap=cap, n=B.n, ws=ws)
     return out
 
 
@@ -834,7 +867,7 @@ def _bitmap_finish(A: CSR, B: CSR, plan: BitmapPlan, out: dict, info: SpgemmInfo
     z, uoff = out["z"], out["uoff"]
     if lazy:
         nnz, e, deferred = torch.stack([uoff[-1], z[0].long(), z[1].long()]).tolist()   # the one read-back
-        if e & 8:   # ws8 lengths truncated: the count and numeric kernels stood down
+        if e & (8 | 64):   # ws8 lengths truncated / a count unit past the descriptors: rerun eagerly
             return "eager"
     else:
         nnz = out["nnz"]
@@ -863,19 +896,21 @@ def _bitmap_finish(A: CSR, B: CSR, plan: BitmapPlan, out: dict, info: SpgemmInfo
 
 
 def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional[dict] = None,
-                   _eager: bool = False) -> Optional[CSR]:
+                   lazy: bool = False) -> Optional[CSR]:
     """Bitmap-rank SpGEMM (csr_spgemm_bitmap.hip): a count kernel gives the
     exact nnz of every (row, column window) unit, one scan gives every unit's
     final offset, and the numeric kernel writes each unit there once (no
     look-back, no staging buffer, no compaction).  Returns None when a unit
     does not fit even the reload kernel; the caller then runs the binned
-    path.  Lazy flow (``SPMM_SPGEMM_BITMAP_LAZY=1``): C at the product-count
-    bound (what ``_bitmap_ok`` admitted), no host sync between the kernels,
-    one read-back after the product."""
+    path.  ``lazy`` (the flow the captured graphs replay, ``SpgemmGraph``):
+    C at the product-count bound (what ``_bitmap_ok`` admitted), no host sync
+    between the kernels, one read-back after the product; eager (default):
+    one read-back between count and numeric sizes C exactly (the two measure
+    the same, PERF_LOG round 3)."""
     plan = _bitmap_plan(A, B, info, pre)
     if plan is None:
         return None
-    lazy = CONFIG.spgemm_bitmap_lazy > 0 and not plan.det and not _eager
+    lazy = lazy and not plan.det
     out = _bitmap_launch(A, B, plan, lazy, B_ready, info)
     if out.get("truncated"):   # eager: per-unit count and numeric kernels
         plan = _bitmap_plan(A, B, info, pre, use_ws8=False)
@@ -885,7 +920,7 @@ def onepass_bitmap(A: CSR, B: CSR, info: SpgemmInfo, B_ready=None, pre: Optional
     C_ = _bitmap_finish(A, B, plan, out, info, lazy)
     if isinstance(C_, str):
         del out
-        return onepass_bitmap(A, B, info, None, pre, _eager=True)
+        return onepass_bitmap(A, B, info, None, pre)
     return C_
 
 
@@ -941,7 +976,8 @@ class SpgemmGraph:
         info = info if info is not None else SpgemmInfo()
         C_ = _bitmap_finish(self.A, self.B, self.plan, self.out, info, True)
         if isinstance(C_, str):
-            raise RuntimeError("SpgemmGraph: B's window segments no longer fit the packed 16-bit lengths")
+            raise RuntimeError("SpgemmGraph: the operands no longer fit the row kernels (16-bit window lengths "
+                               "or count descriptors)")
         return C_
 
 

@@ -122,6 +122,24 @@ class Comm:
             return torch.cat(parts).to(dev)
         return finish_host
 
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> Callable[[], None]:
+        """Start an all-gather of equally sized ``t`` into the preallocated
+        ``out`` ([world * t.numel()], rank order) and return the function
+        that makes the current stream wait for it (RCCL: a stream wait, no
+        host wait).  Persistent buffers, so a captured HIP graph can read the
+        result every step (``models.spgemm.RowblockGraph``)."""
+        flat = t.reshape(-1)
+        if out.numel() != self.world * flat.numel():
+            raise ValueError(f"all_gather_into: {out.numel()} != {self.world} x {flat.numel()}")
+        if not self.is_dist:
+            out.copy_(flat)
+            return lambda: None
+        if self.device_collectives and out.device == self.device and out.is_contiguous():
+            work = dist.all_gather_into_tensor(out, flat.contiguous(), async_op=True)
+            return lambda: (work.wait(), None)[1]
+        got = self.all_gather_async(t)
+        return lambda: (out.copy_(got()), None)[1]
+
     def all_to_all_v(self, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
         """Rank r sends x[sum(send[:p]) : sum(send[:p + 1])] to rank p and
         receives recv[p] elements from each rank p (concatenated, rank

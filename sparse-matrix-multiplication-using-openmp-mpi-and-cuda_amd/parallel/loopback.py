@@ -84,7 +84,10 @@ def _mark(t: torch.Tensor):
 def _take(item, device: torch.device) -> torch.Tensor:
     t, ev = item
     if ev is not None and device.type == "cuda":
-        torch.cuda.current_stream(device).wait_event(ev)
+        cur = torch.cuda.current_stream(device)
+        cur.wait_event(ev)
+        if t.device == device:   # the poster's block stays allocated until this stream has read it
+            t.record_stream(cur)
     elif ev is not None:
         ev.synchronize()
     return t.to(device)
@@ -131,6 +134,10 @@ class LoopbackComm(Comm):
         # (RCCL's stream-ordered collective gives the caller the same freedom)
         got = self._post(_mark(flat.clone()))
         return lambda: torch.cat([_take(x, dev) for x in got()])
+
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> Callable[[], None]:
+        got = self.all_gather_async(t)
+        return lambda: (out.copy_(got()), None)[1]
 
     def all_to_all_v(self, x: torch.Tensor, send: List[int], recv: List[int]) -> torch.Tensor:
         got = self._exchange((_mark(x.clone()), list(send)))   # (a copy: see all_gather_async)
@@ -232,3 +239,63 @@ def run_loopback(world: int, fn: Callable[[LoopbackComm], object], device: str =
     if errs:
         raise errs[0]
     return out
+
+
+class PanelComm(Comm):
+    """Rank ``rank`` of ``world`` in ONE thread, for the row-block step's
+    operand gathers only (``models.spgemm.RowblockGraph``: the panel sizes,
+    row counts and the two payload gathers, plus agreements): the other ranks'
+    contributions are computed from ``panels`` (every rank's B row panel), so
+    rank r's whole step runs on one GPU with no peer threads.  ``gbps`` > 0
+    delivers each payload late, on a separate "link" stream after a
+    stream-ordered delay of (bytes this rank receives) / gbps, in RCCL's
+    issue order (columns, then values): ``tools/rank_emulate.py`` models a
+    rank of an N-GPU node with it; tests drive the W-rank branches with it."""
+
+    def __init__(self, rank: int, world: int, dev: torch.device, panels, gbps: float = 0.0):
+        super().__init__(rank, world, rank, dev, "panels")
+        if len(panels) != world:
+            raise ValueError("PanelComm: one B panel per rank")
+        self.panels, self.gbps = panels, gbps
+        self.link = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._n = 0
+
+    @property
+    def device_collectives(self) -> bool:
+        return self.device.type == "cuda"
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        if t.numel() == 2:   # [m, nnz] of every panel
+            return torch.tensor([[p.m, p.nnz] for p in self.panels], dtype=torch.int64, device=t.device).view(-1)
+        out = torch.zeros(self.world, t.numel(), dtype=t.dtype, device=t.device)   # row counts, padded
+        for r, p in enumerate(self.panels):
+            out[r, :p.m] = p.rowptr[1:] - p.rowptr[:-1]
+        return out.view(-1)
+
+    def _allreduce_scalar(self, x: float, op: str) -> float:
+        return x * self.world if op == "sum" else x
+
+    def barrier(self) -> None:
+        pass
+
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> Callable[[], None]:
+        values = self._n % 2 == 1   # RowblockGraph's order: columns, then value bits
+        self._n += 1
+        emax = t.numel()
+        if out.numel() != self.world * emax or any(p.nnz > emax for p in self.panels):
+            raise ValueError(f"PanelComm: receive buffer of {out.numel()} for {self.world} panels of <= {emax}")
+        cur = torch.cuda.current_stream(self.device)
+        self.link.wait_stream(cur)   # (RCCL: a collective starts after the producer of its input)
+        recv_bytes = (self.world - 1) * t.numel() * t.element_size()
+        with torch.cuda.stream(self.link):
+            if self.gbps > 0:
+                from .. import _native
+
+                _native.check(_native.hip().spmm_prim_spin(recv_bytes / (self.gbps * 1e3),
+                                                           _native.stream_ptr(self.device)), "prim_spin")
+            for r, p in enumerate(self.panels):   # every panel's current columns / values
+                if p.nnz:
+                    out[r * emax:r * emax + p.nnz].copy_(p.val.view(torch.int32) if values else p.col)
+        ev = torch.cuda.Event()
+        ev.record(self.link)
+        return lambda: cur.wait_event(ev)

@@ -51,12 +51,6 @@ class Config:
     spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
     # ... with every (row, window) segment of those pairs starting on a 128-byte line (1) or packed (0)
     spgemm_bitmap_pad: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_PAD", 1, int))
-    # bitmap path: C allocated at the product-count bound and the nnz read back once, after the
-    # numeric kernels (1), or C allocated exactly after a read-back between count and numeric (0,
-    # default: the two measure the same, 64k 1.564 vs 1.567 ms, 1M 75.7-76.0 vs 75.7-76.1 ms)
-    spgemm_bitmap_lazy: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_LAZY", 0, int))
-    # windows per row-major count unit (1, 2 or 4; cfg 0: 1 = 16 KB bitmaps, 8 per CU; 2 = 32 KB, 4 per CU)
-    spgemm_bitmap_count_windows: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_COUNT_WINDOWS", 2, int))
     # fixed fp32 summation order (Gustavson order: bitwise run-to-run reproducible, equal to the CPU
     # engine) on the bitmap-rank path: 0 = off, 1 = on (other GPU paths stay unordered), 2 = strict
     # (a product no deterministic GPU kernel covers runs on the CPU engine)

@@ -316,3 +316,111 @@ def test_local_flag_survives_the_spgemm_wrapper(monkeypatch):
     assert seen == {"local": True, "cols": True}
     Cd = C.to_dense().double().cpu()
     assert torch.allclose(Cd, A.to_dense().double().cpu() @ B.to_dense().double().cpu(), atol=1e-4)
+
+
+def _graph_case(world: int, steps: int = 3):
+    """RowblockGraph on W loopback ranks (uneven panels, empty ones at W >= 3)
+    of a product every rank takes on the bitmap-rank path; B's values (and
+    A's) change in place between steps: every replay re-gathers and
+    recomputes."""
+    dev = torch.device("cuda")
+    m, k, n = 4000, 20000, 300000
+    A = gen_csr.uniform_csr(m, k, 0.002, seed=95)
+    B = gen_csr.uniform_csr(k, n, 2.7e-4, seed=96)
+    rc = _cuts(m, world, 7)
+    kc = [0] + [k * (r + 1) // world for r in range(world)]
+    if world >= 3:   # an empty B panel too
+        kc[2] = kc[1]
+    scales = [1.0 + 0.25 * s for s in range(steps)]
+
+    def body(comm):
+        r = comm.rank
+        with torch.cuda.stream(torch.cuda.Stream(dev)):   # a stream per rank, as separate processes have
+            Ap = A.row_slice(rc[r], rc[r + 1]).to(dev)
+            Bp = B.row_slice(kc[r], kc[r + 1]).to(dev)
+            if Ap.m == 0:   # an empty A panel: no graph (every rank must agree: the class raises everywhere)
+                Ap = A.row_slice(0, 1).to(dev)
+            g = MS.RowblockGraph(Ap, Bp, comm)
+            outs = []
+            v0 = Bp.val.clone()
+            for s in scales:
+                Bp.val.copy_(v0 * s)
+                g.run()
+                C = g.result()
+                outs.append((C.rowptr.cpu(), C.col.cpu(), C.val.cpu()))
+            torch.cuda.current_stream(dev).synchronize()
+            del g
+            return outs
+
+    got = run_loopback(world, body, device="cuda", timeout_s=600)
+    Ad = A.to(dev)
+    for i, s in enumerate(scales):
+        ref = SG.spgemm(Ad, B.with_values(B.val * s).to(dev))
+        for r in range(world):
+            lo, hi = (rc[r], rc[r + 1]) if rc[r + 1] > rc[r] else (0, 1)
+            exp = ref.row_slice(lo, hi)
+            rp, col, val = got[r][i]
+            assert torch.equal(rp, exp.rowptr.cpu()) and torch.equal(col, exp.col.cpu()), (world, r, i)
+            assert torch.allclose(val, exp.val.cpu(), rtol=1e-5, atol=1e-6), (world, r, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 7, 8])
+def test_loopback_gpu_rowblock_graph(world):
+    """The host-sync-free row-block step (gathers between two captured HIP
+    graphs) at W = 2 / 7 / 8 on one GPU equals the one-process product, step
+    after step, with B's values changing in place."""
+    _graph_case(world)
+
+
+def test_all_gather_into_gloo_and_loopback():
+    """``Comm.all_gather_into`` (the persistent-buffer gather the graph step
+    uses) on the loopback backend at W = 3 (CPU)."""
+    def body(comm):
+        t = torch.arange(5, dtype=torch.int32) + 10 * comm.rank
+        out = torch.full((comm.world * 5,), -1, dtype=torch.int32)
+        comm.all_gather_into(out, t)()
+        return out
+
+    got = run_loopback(3, body, timeout_s=60)
+    exp = torch.cat([torch.arange(5, dtype=torch.int32) + 10 * r for r in range(3)])
+    assert all(torch.equal(g, exp) for g in got)
+
+
+def _graph_case_panels(world: int):
+    """RowblockGraph of every rank r of W in ONE thread (``PanelComm``: the
+    peers' panels are known), uneven and empty panels, B's values changing in
+    place between steps; C of each rank equals its rows of the one-process
+    product."""
+    from spmm_amd.parallel.loopback import PanelComm
+
+    dev = torch.device("cuda")
+    m, k, n = 4000, 20000, 300000
+    A = gen_csr.uniform_csr(m, k, 0.002, seed=95)
+    B = gen_csr.uniform_csr(k, n, 2.7e-4, seed=96)
+    rc = [0] + [m * (r + 1) // world for r in range(world)]
+    kc = [0] + [k * (r + 1) // world for r in range(world)]
+    if world >= 3:   # an empty B panel, an uneven neighbour
+        kc[2] = kc[1]
+    for r in range(world):
+        panels = [B.row_slice(kc[q], kc[q + 1]).to(dev) for q in range(world)]
+        Ap = A.row_slice(rc[r], rc[r + 1]).to(dev)
+        g = MS.RowblockGraph(Ap, panels[r], PanelComm(r, world, dev, panels))
+        for s in (1.0, -2.0):
+            for q in range(world):   # every rank's panel changes (PanelComm gathers their current values)
+                panels[q].val.mul_(s)
+            g.run()
+            C = g.result()
+            ref = SG.spgemm(A.to(dev), CS.CSR(k, n, B.rowptr.to(dev),
+                                              torch.cat([p.col for p in panels]),
+                                              torch.cat([p.val for p in panels]))).row_slice(rc[r], rc[r + 1])
+            assert torch.equal(C.rowptr, ref.rowptr) and torch.equal(C.col, ref.col), (world, r, s)
+            assert torch.allclose(C.val, ref.val, rtol=1e-5, atol=1e-6), (world, r, s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 7, 8])
+def test_rowblock_graph_panel_comm(world):
+    """The host-sync-free row-block step of every rank at W = 2 / 7 / 8 (one
+    thread per test, no concurrent captures)."""
+    _graph_case_panels(world)

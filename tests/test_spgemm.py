@@ -348,6 +348,18 @@ def test_rowblock_spgemm_rccl_one_rank(monkeypatch):
         # the second one ran the bitmap kernels on the two-stage gather (columns
         # unpacked first for the count kernel, values + pairs before the numeric)
         assert "bitmap_units" in info.rows_per_bin_num
+        # the host-sync-free step: RCCL gathers between two captured graphs,
+        # replayed after in-place value changes of both operands
+        g = MS.RowblockGraph(prob.A, prob.B, comm)
+        va, vb = prob.A.val.clone(), prob.B.val.clone()
+        for s in (1.0, -0.5, 2.0):
+            prob.A.val.copy_(va * s)
+            prob.B.val.copy_(vb * (s + 1.0))
+            g.run()
+            C1 = g.result()
+            C2 = SG.spgemm(prob.A, prob.B)
+            assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+            assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
     finally:
         comm.close()
 
@@ -582,18 +594,18 @@ def test_spgemm_gpu_bitmap_matches_binned(monkeypatch, cfg, m, k, n, da, db):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("count_windows,n", [(2, 700000), (4, 700000), (2, 1 << 20), (4, 1 << 20)])
-def test_spgemm_gpu_bitmap_count_units(monkeypatch, count_windows, n):
-    """Row count kernel with units of 2 and 4 windows over the padded column
-    groups (16-byte column loads), the 1M config's window (cfg 0: 2^17):
-    ragged last window (n = 700000: 6 windows, the last count unit partly
-    past the end) and exactly 8 windows."""
+@pytest.mark.parametrize("n", [700000, 1 << 20, 300000])
+def test_spgemm_gpu_bitmap_count_units(monkeypatch, n):
+    """Row count kernel (units of 2 windows) over the padded column groups
+    (16-byte column loads), the 1M config's window (cfg 0: 2^17): ragged last
+    window (n = 700000: 6 windows, the last count unit partly past the end),
+    exactly 8 windows, and 3 windows (an odd count: the last unit is one
+    window)."""
     from spmm_amd.utils.config import CONFIG
 
     dev = torch.device("cuda")
     A = gen_csr.uniform_csr(3000, 20000, 0.004, seed=61, device=dev)
     B = gen_csr.uniform_csr(20000, n, 100.0 / n, seed=62, device=dev)
-    monkeypatch.setattr(CONFIG, "spgemm_bitmap_count_windows", count_windows)
     info = _bitmap_vs_binned(monkeypatch, A, B, 0)
     assert info.rows_per_bin_num.get("bitmap_cfg") == 0 and info.rows_per_bin_num.get("bitmap_rows") == 1, \
         info.rows_per_bin_num
@@ -673,8 +685,20 @@ def test_spgemm_gpu_bitmap_truncated_window_lengths(monkeypatch, lazy):
     A = gen_csr.uniform_csr(600, k, 0.01, seed=32)
     ka = A.col.long() != 17
     A = CS.from_coo(A.row_ids()[ka], A.col.long()[ka], A.val[ka], 600, k).to(dev)
-    monkeypatch.setattr(CONFIG, "spgemm_bitmap_lazy", lazy)
-    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    if lazy:   # the flow the captured graphs replay: numeric stands down too, the product reruns eagerly
+        monkeypatch.setattr(CONFIG, "spgemm_bitmap", "on")
+        monkeypatch.setattr(CONFIG, "spgemm_bitmap_cfg", 0)
+        info = SG.SpgemmInfo()
+        nprod, _, st = SG.row_plan(A, B)
+        tot, mx, nz, light, h1, h2, h4, h8, amax = st.tolist()[:9]
+        info.flops, info.mean_seg = 2 * tot, tot / max(A.nnz, 1)
+        C1 = SG.onepass_bitmap(A, B, info, pre=dict(max=mx, nonempty=nz, light=light, amax=amax), lazy=True)
+        monkeypatch.setattr(CONFIG, "spgemm_bitmap", "off")
+        C2 = SG.spgemm(A, B)
+        assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+        assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+    else:
+        info = _bitmap_vs_binned(monkeypatch, A, B, 0)
     assert "bitmap_units" in info.rows_per_bin_num
 
 
@@ -702,6 +726,38 @@ def test_spgemm_gpu_bitmap_deferred_units_and_fallback(monkeypatch):
     info = _bitmap_vs_binned(monkeypatch, Ac, Bc, 0)
     assert info.rows_per_bin_num.get("bitmap_fallback") is None   # info reset by the fallback
     assert "bitmap_units" not in info.rows_per_bin_num
+
+
+@pytest.mark.gpu
+def test_spgemm_gpu_bitmap_count_descriptor_batches(monkeypatch):
+    """A two-window count unit of more chunks than the pipelined count
+    kernel's 768 descriptors: 256-entry A rows over B rows of exactly 65 or
+    97 entries inside the first two windows (cfg 0, 8 windows; the mean
+    segment gives 32-column chunks: 3 or 4 chunks per entry, ~800 per unit)
+    while every window stays inside the reload kernel's 12288 products.
+    The pipelined count kernel flags such a unit (err bit 6) and the product
+    is recounted on the per-unit kernels, which take descriptors in batches;
+    before, the chunks past the buffer were dropped and the numeric kernel
+    raised on the short count."""
+    dev = torch.device("cuda")
+    k, n = 2000, 1 << 20
+    g = torch.Generator().manual_seed(7)
+    rows, cols = [], []
+    for j in range(k):
+        w0, w1 = (49, 48) if j % 8 == 0 else (33, 32)   # 97 or 65 columns in [0, 2^18)
+        c = torch.cat([torch.randperm(1 << 17, generator=g)[:w0], (1 << 17) + torch.randperm(1 << 17, generator=g)[:w1]])
+        rows.append(torch.full((c.numel(),), j))
+        cols.append(c)
+    rows, cols = torch.cat(rows), torch.cat(cols)
+    B = CS.from_coo(rows, cols, torch.rand(rows.numel(), generator=g) - 0.5, k, n).to(dev)
+    m = 48
+    ar = torch.arange(m).repeat_interleave(256)
+    ac = torch.cat([torch.randperm(k, generator=g)[:256] for _ in range(m)])
+    A = CS.from_coo(ar, ac, torch.rand(ar.numel(), generator=g) - 0.5, m, k).to(dev)
+    info = _bitmap_vs_binned(monkeypatch, A, B, 0)
+    assert info.rows_per_bin_num.get("bitmap_cfg") == 0 and "bitmap_units" in info.rows_per_bin_num, \
+        info.rows_per_bin_num
+    assert info.rows_per_bin_num["bitmap_deferred"] >= m   # every row's first windows: the reload kernel
 
 
 def sampled_rows_check(A, B, C, nrows: int, seed: int = 0) -> float:

@@ -1,12 +1,24 @@
 """Per-rank cost of the row-block SpGEMM step at world size N, on one GPU.
 
-Builds exactly what rank r of an N-GPU run holds (A's row panel r; B already
-all-gathered, i.e. the full B) and times the local part of the step
-(``spgemm(A_panel, B)``), plus a device copy of the B bytes a rank would
-receive as a stand-in for the all-gather.  Used to predict strong scaling of
-``bench.py`` without an 8-GPU node.
+Builds exactly what rank r of an N-GPU run holds (A's row panel r; every
+rank's B row panel) and times:
 
-    python tools/rank_emulate.py --world 8 [--rank 0] [--n 1048576] [--density 1e-4]
+* ``local_ms``: the local product against the full B (``spgemm(A_panel, B)``,
+  eager, or ``--graph``: a SpgemmGraph replay) -- the step without the gather;
+* ``step_ms[gbps]`` (``--gather-gbps 0,300,...``): the whole rank-r step of
+  ``bench.py`` at N ranks, i.e. ``models.spgemm.RowblockGraph.run`` (copy of
+  the own panel into the send buffers, column gather, graph 1 = unpack +
+  B layouts + count kernel, value gather, graph 2 = unpack + padded pairs +
+  numeric), through ``parallel.loopback.PanelComm``: the gathered payloads
+  are copied into the receive buffers on a separate "link" stream after a
+  stream-ordered delay of (bytes this rank receives) / gbps, in RCCL's issue
+  order (columns, then values, one after the other), so the columns / values
+  become readable exactly when a link of that rate would deliver them and
+  the count kernel overlaps the value transfer as on the real node.  Not
+  modelled: the CUs and HBM bandwidth RCCL's own kernels take while they
+  run.  0 = delay-free (the copies only).
+
+    python tools/rank_emulate.py --world 8 [--rank 0] [--gather-gbps 0,150,300]
 """
 import argparse
 import json
@@ -20,9 +32,20 @@ import torch  # noqa: E402
 
 import spmm_amd  # noqa: E402,F401
 from spmm_amd import _native  # noqa: E402
+from spmm_amd.models import spgemm as MS  # noqa: E402
 from spmm_amd.ops.spgemm import SpgemmGraph, SpgemmInfo, spgemm  # noqa: E402
+from spmm_amd.parallel.loopback import PanelComm  # noqa: E402
 from spmm_amd.parallel.partition import row_panels  # noqa: E402
 from spmm_amd.utils.gen_csr import uniform_csr  # noqa: E402
+
+def timed(fn, steps: int) -> float:
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
 
 
 def main() -> None:
@@ -34,49 +57,40 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--graph", action="store_true", help="time the local product as a SpgemmGraph replay")
-    ap.add_argument("--per-step", action="store_true", help="print every timed step's ms and the path taken")
+    ap.add_argument("--gather-gbps", default="", help="comma list: emulate the whole step at these link rates")
+    ap.add_argument("--no-local", action="store_true", help="skip the local-product timings")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     _native.hip()
-    lo, hi = row_panels(a.n, a.world)[a.rank]
+    pan = row_panels(a.n, a.world)
+    lo, hi = pan[a.rank]
     A = uniform_csr(a.n, a.n, a.density, seed=a.seed, device=dev, rows=(lo, hi))
-    B = uniform_csr(a.n, a.n, a.density, seed=a.seed + 1, device=dev)
-    info = SpgemmInfo()
-    C = spgemm(A, B, info)
-    del C
-    recv = (a.world - 1) / a.world * (B.nnz * 8 + B.m * 8)
-    src = torch.empty(int(recv) // 4 + 1, dtype=torch.int32, device=dev)
-    dst = torch.empty_like(src)
-    run = lambda: spgemm(A, B)  # noqa: E731
-    if a.graph:
-        g = SpgemmGraph(A, B)
-        run = g.run
-    if a.per_step:
-        print(json.dumps(dict(first_run=info.rows_per_bin_num)), file=sys.stderr, flush=True)
-        for k in range(a.steps):
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            si = SpgemmInfo()
-            C = spgemm(A, B, si) if not a.graph else run()
-            del C
-            torch.cuda.synchronize()
-            print(json.dumps(dict(step=k, ms=round((time.perf_counter() - t1) * 1e3, 3), path=si.rows_per_bin_num)),
-                  file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        C = run()
+    rec = dict(world=a.world, rank=a.rank, rows=hi - lo)
+    if not a.no_local:
+        B = uniform_csr(a.n, a.n, a.density, seed=a.seed + 1, device=dev)
+        info = SpgemmInfo()
+        C = spgemm(A, B, info)
         del C
-    torch.cuda.synchronize()
-    t_local = (time.perf_counter() - t0) / a.steps
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        dst.copy_(src)
-    torch.cuda.synchronize()
-    t_copy = (time.perf_counter() - t0) / a.steps
-    print(json.dumps(dict(world=a.world, rank=a.rank, graph=a.graph, rows=hi - lo, flops=info.flops, nnz_C=info.nnz,
-                          local_ms=round(t_local * 1e3, 3), gflops_local=round(info.flops / t_local / 1e9, 1),
-                          allgather_recv_bytes=int(recv), device_copy_ms=round(t_copy * 1e3, 3))), flush=True)
+        rec.update(flops=info.flops, nnz_C=info.nnz)
+        run = (lambda: spgemm(A, B)) if not a.graph else SpgemmGraph(A, B).run
+        rec.update(graph=a.graph, local_ms=round(timed(run, a.steps), 3))
+        rec["gflops_local"] = round(info.flops / rec["local_ms"] / 1e6, 1)
+        rec["allgather_recv_bytes"] = int((a.world - 1) / a.world * (B.nnz * 8))
+        del B, run
+        torch.cuda.empty_cache()
+    if a.gather_gbps:
+        panels = [uniform_csr(a.n, a.n, a.density, seed=a.seed + 1, device=dev, rows=p) for p in pan]
+        steps = {}
+        for g in [float(x) for x in a.gather_gbps.split(",")]:
+            comm = PanelComm(a.rank, a.world, dev, panels, g)
+            rg = MS.RowblockGraph(A, panels[a.rank], comm)
+            steps[str(g)] = round(timed(rg.run, a.steps), 3)
+            C = rg.result()
+            rec.setdefault("step_nnz_C", C.nnz)
+            del rg, C, comm
+            torch.cuda.empty_cache()
+        rec["step_ms"] = steps
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
