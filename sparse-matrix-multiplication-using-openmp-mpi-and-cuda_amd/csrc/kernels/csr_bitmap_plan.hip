@@ -205,14 +205,14 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
 
 // Layouts + count kernel + unit offsets.  Bv may be null (B's values still in flight:
 // the padded pairs are then built by spmm_spgemm_bm_back).  uoff: nunits + 1 entries;
-// z: {error bits, deferred units} (zeroed here).  *pairs_built: whether the padded
+// z: int32[4] {error bits, deferred units, numeric row ticket, count row ticket} (zeroed here).  *pairs_built: whether the padded
 // pairs exist after this call (pass it to spmm_spgemm_bm_back).
 SPMM_EXPORT int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const int64_t* Brp,
                                      const int32_t* Bci, const float* Bv, void* ws, int64_t* uoff, int32_t* z,
                                      int* pairs_built, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   *pairs_built = 0;
-  if (hipMemsetAsync(z, 0, 8, s) != hipSuccess || hipMemsetAsync(uoff, 0, 8, s) != hipSuccess)
+  if (hipMemsetAsync(z, 0, 16, s) != hipSuccess || hipMemsetAsync(uoff, 0, 8, s) != hipSuccess)
     return (int)hipErrorUnknown;
   uint32_t* split = at<uint32_t>(ws, p->o_split);
   int32_t* ucnt = at<int32_t>(ws, p->o_ucnt);

@@ -1454,6 +1454,11 @@ __global__ __launch_bounds__(256) void long_btab(const int64_t* __restrict__ Brp
 // gives each wave whole blocks; a row of fewer spreads every block's windows
 // over all the waves (one hub B row can hold all of an item's products).
 constexpr int LONG_DU = 4;
+// long_dense item schedule: tickets (1, the default) or static items (0, diagnostic builds)
+#ifndef SPMM_LONG_TICKETS
+#define SPMM_LONG_TICKETS 1
+#endif
+
 template <bool VALUES, bool DIRECT>
 __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restrict__ list,
                                                          const int32_t* __restrict__ nlist,
@@ -1466,7 +1471,8 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
                                                          const int64_t* __restrict__ dl_rp,
                                                          const uint32_t* __restrict__ btab,
                                                          const int32_t* __restrict__ Bci,
-                                                         const float* __restrict__ Bv) {
+                                                         const float* __restrict__ Bv,
+                                                         int32_t* __restrict__ ticket) {
   constexpr int NW = LONG_DNT / 64;
   __shared__ float vals[VALUES ? LONG_W : 1];
   __shared__ uint32_t bits[LONG_W / 32];
@@ -1474,6 +1480,7 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
   __shared__ int own_all[DIRECT ? NW : 1][64];
   __shared__ uint2 seg_all[DIRECT ? NW : 1][64];
   __shared__ float sa_all[DIRECT ? NW : 1][64];
+  __shared__ int s_tk[2];
   static_assert(LONG_W / 32 == LONG_DNT, "one occupancy word per thread");
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   bits[tid] = 0u;
@@ -1481,6 +1488,17 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
     for (int i = tid; i < LONG_W / 4; i += LONG_DNT) reinterpret_cast<float4*>(vals)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   // the items of this kernel (long_partition: more than LR_CAP products)
   const int64_t nl = *nlist;
+  // Item schedule: the first two items static (blockIdx.x, + gridDim.x), then tickets (2 G + a
+  // global counter).  Items span 10^3 .. 10^7 products (R-MAT hub rows), so equal item counts
+  // per workgroup are far from equal work.  Thread 0 fetches a ticket at the top of an item and
+  // publishes it to LDS before the item's last barrier; it names the item after next.
+  // (A zero hipcc cannot see through makes the atomic's offset look divergent: the atomic
+  // optimizer would otherwise wait for it on the spot.)
+  int tkz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(tkz));
+  const auto rtk = __builtin_amdgcn_make_buffer_rsrc(ticket, 0, 4, 0x00020000);
+  const int64_t G = gridDim.x;
+  int kd = 0;   // items done by this workgroup
   int64_t it = blockIdx.x;   // position in the list
   int64_t rt = it < nl ? list[it] : -1;
   int64_t n = 0, base = 0;
@@ -1493,7 +1511,9 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
   }
   __syncthreads();
   while (it < nl) {
-    const int64_t it2 = it + gridDim.x;
+    int tk = 0;
+    if (tid == 0) tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rtk, tkz, 0, 0);
+    const int64_t it2 = (kd == 0 || !SPMM_LONG_TICKETS) ? it + G : 2 * G + __builtin_amdgcn_readfirstlane(s_tk[(kd + 1) & 1]);
     const int64_t rt2 = it2 < nl ? list[it2] : -1;   // in flight during the atomics
     const int c0 = (int)(rt % nch) << LONG_LGW;
     for (int64_t i0 = tid;;) {
@@ -1605,6 +1625,9 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
       }
     }
     __syncthreads();
+    // (the products' loads are all consumed here: waiting for the ticket costs nothing; it is
+    // read as the item after next, after this item's last barrier)
+    if (tid == 0) s_tk[kd & 1] = tk;
     int64_t n2 = 0, base2 = 0;
     if (rt2 >= 0) { n2 = rt_cnt[rt2]; base2 = rt_off[rt2]; }
     // one occupancy word per thread: its columns in order; the write-back
@@ -1638,6 +1661,7 @@ __global__ __launch_bounds__(LONG_DNT, 2) void long_dense(const int32_t* __restr
       x[u] = i < n2 ? scratch[base2 + i] : ~0ull;
     }
     it = it2; rt = rt2; n = n2; base = base2;
+    ++kd;
     __syncthreads();   // write-back clears and wsum reads done before the next item's atomics / wsum writes
   }
 }
@@ -2205,7 +2229,7 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
                                        void* scratch, int64_t* rt_nnz, int32_t* ws, const int64_t* dt_cnt,
                                        const void* dl, const int64_t* dl_rp, const uint32_t* btab, const int32_t* Bci,
                                        const float* Bv, void* stream) {
-  // ws: 2 * nrt + 2 int32 (the two work lists and their lengths)
+  // ws: 2 * nrt + 4 int32 (the two work lists, their lengths and long_dense's item ticket counter)
   // direct products (optional): dt_cnt per item, dl / dl_rp the batch rows'
   // long entries (long_route), btab, B
   if (nrt <= 0) return 0;
@@ -2227,9 +2251,10 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
     return e && e[0] == '0' ? 0 : 1;
   }();
   int32_t* nl = ws;
-  int32_t* rank_list = ws + 2;
-  int32_t* dense_list = ws + 2 + nrt;
-  hipError_t e = hipMemsetAsync(nl, 0, 2 * sizeof(int32_t), s);
+  int32_t* ticket = ws + 2;
+  int32_t* rank_list = ws + 4;
+  int32_t* dense_list = ws + 4 + nrt;
+  hipError_t e = hipMemsetAsync(nl, 0, 4 * sizeof(int32_t), s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(long_partition, dim3((unsigned)((nrt + 255) / 256)), dim3(256), 0, s, rt_cnt, nrt,
                      use_rank ? (int64_t)LR_CAP : int64_t(0), rank_list, dense_list, nl, rt_nnz, dt_cnt);
@@ -2250,7 +2275,7 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, LONG_DNT, 0) != hipSuccess || per <= 0) per = 1;
     const unsigned grid = (unsigned)std::min<int64_t>(nrt, (int64_t)per * ncu);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
-                       (unsigned long long*)scratch, rt_nnz, dt_cnt, (const uint4*)dl, dl_rp, btab, Bci, Bv);
+                       (unsigned long long*)scratch, rt_nnz, dt_cnt, (const uint4*)dl, dl_rp, btab, Bci, Bv, ticket);
   };
   if (dt_cnt != nullptr) {
     if (values) launch(long_dense<true, true>);

@@ -45,6 +45,13 @@ using namespace spmm_bitmap;
 #define SPMM_BM_PRIO_HI() __builtin_amdgcn_s_setprio(3)
 #define SPMM_BM_PRIO_LO() __builtin_amdgcn_s_setprio(0)
 
+// Work schedule (diagnostic builds only): ticket rows (bit 0: the pipelined numeric row
+// kernel, the default; bit 1: the pipelined count kernel) or static ones (me, me + NG, ...).
+// 1M step: static 58.5 ms, numeric tickets 54.7 ms, both 56.2-56.8 ms (PERF_LOG round 6).
+#ifndef SPMM_BM_TICKETS
+#define SPMM_BM_TICKETS 1
+#endif
+
 // Build-time geometry (every value below was swept in PERF_LOG rounds 3-5; tools/bm_variants.py
 // builds diagnostic variants of these, normal builds never override them):
 #ifndef SPMM_BM_ROWS_R   // register rounds of the row-major numeric kernel (chunk capacity 16 * R per unit)
@@ -136,7 +143,7 @@ __device__ __forceinline__ void bm_write_unit(const unsigned long long* items, i
 // that delimit it, in registers, flushed once at the end; [7] counts units.
 __device__ int g_bm_stamp_on = 0;
 __device__ unsigned long long g_bm_stamps[8];
-// per workgroup of the pipelined numeric kernel (stamps build): start / end of its row loop on
+// per workgroup of the numeric kernel (pipelined row or per-unit; stamps build): start / end on
 // the 100 MHz real-time counter (one clock for every XCD), XCD id << 32 | units formed
 constexpr int kBmWgMax = 8192;
 __device__ unsigned long long g_bm_wg[3 * kBmWgMax];
@@ -325,6 +332,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   int vz;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
   BM_STAMP_DECL
+  BM_WG_DECL
   if constexpr (MODE != 0) {
     // numeric / reload after a row count that stood down (ws8 lengths
     // truncated, err bit 3; the host reruns the product on the per-unit count):
@@ -641,7 +649,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       }
       int pre, plen, TC, P;
       bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-      if (P == 0) continue;   // uniform; the count kernel wrote 0 for this unit
+      if (P == 0) {   // uniform; the count kernel wrote 0 for this unit
+        continue;
+      }
       const bool too_big = na > NT || P > PCAP || TC > CCAP || (MODE == 1 && TC > RL * ngrp);
       if (too_big) {   // uniform
         if (tid == 0) {
@@ -892,6 +902,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
     }
   }
   BM_STAMP_FLUSH();
+  if constexpr (MODE == 1) BM_WG_FLUSH();
 }
 
 // ---- row-major numeric kernel (nwin <= 8) ---------------------------------
@@ -1358,6 +1369,7 @@ struct BmPipeArgs {
   BmRowArgs r;
   uint32_t bcv_bytes;   // bytes of the padded pair array (< 2^32: checked by the host)
   int64_t annz;         // nnz(A) > 0
+  int32_t* ticket;      // row ticket counter, zero at launch
 };
 
 
@@ -1383,6 +1395,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   __shared__ int wscan[2 * NW];   // staging scan
   __shared__ __attribute__((aligned(8))) int64_t suo[9];   // unit offsets of the staged row (uoff[row * nwin + q])
   __shared__ int sdup;
+  __shared__ int s_tk[2];   // row tickets: row ids, double-buffered (see next_row)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1408,13 +1421,35 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
   const int m = (int)p.m;
   const int annz = (int)pa.annz;   // > 0 (checked by the host)
+  // Row schedule.  The first six rows of a workgroup are static (me, me + NG, ..), every
+  // later one is a ticket: 6 NG + a global counter.  Equal rows per workgroup are not equal
+  // time: the four workgroups of a CU arbitrate unequally and the statically scheduled grid's
+  // ends spread over +-13 % of the kernel (tools/bm_wg_times.py, PERF_LOG round 6), so the
+  // faster workgroups take more rows and every slot stays busy to the end.  Thread 0 fetches
+  // a ticket at the top of a row's last unit (a global atomic into a unit-local register)
+  // and writes it to LDS at the end of that unit -- straight-line code, so hipcc's wait for
+  // the atomic there covers only what was issued after it; the slot is read two rows later
+  // (the row pointers of row k + 4 are loaded in row k's last unit).  A buffer atomic whose
+  // result crosses the loop back-edge got no wait from hipcc: garbage row ids.
+  int kl = 0;   // last units (rows) done by this workgroup
+  // a zero hipcc cannot see through: the ticket atomic's offset looks divergent, so the atomic
+  // optimizer leaves it alone (it would combine the lanes and wait for the result on the spot);
+  // a buffer atomic keeps the address in scalar registers
+  int tkz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(tkz));
+  const auto rtk = __builtin_amdgcn_make_buffer_rsrc(pa.ticket, 0, 4, 0x00020000);
+  int id1 = me, id2 = me + NG, id3 = me + 2 * NG;   // rows in the "1" / "2" / "3" pipeline registers
+  auto next_row = [&]() {   // row k + 4 in row k's last unit
+    if constexpr (!(SPMM_BM_TICKETS & 1)) return id3 + NG;
+    return kl < 2 ? me + (kl + 4) * NG : __builtin_amdgcn_readfirstlane(s_tk[kl & 1]);
+  };
 
   // ---- row pipeline --------------------------------------------------------
   // The per-row inputs (A entries, packed window bounds, unit offsets) are
   // loaded ONCE per row, unconditionally at the top of the row loop, each
-  // from values that landed during the previous row: row r + NG's bounds
-  // (from its A columns), row r + 2 NG's A entries (from its row pointers),
-  // row r + 3 NG's row pointers.  No load sits under a branch inside the
+  // from values that landed during the previous row: the next row's bounds
+  // (from its A columns), the row after's A entries (from its row pointers),
+  // the third row's row pointers (rows in the order of the row schedule).  No load sits under a branch inside the
   // loops and none is consumed in the row that issues it, so hipcc never
   // merges or copies a register whose load is still in flight (a merge it
   // materialises as copies that wait for the load: a full memory latency
@@ -1436,42 +1471,45 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
     return p.uoff[(int64_t)rr * nwin + (lane <= nwin ? lane : nwin)];
   };
   int a1 = 0, b1 = 0, a2 = 0, b2 = 0, a3 = 0, b3 = 0;
-  arp2(me, a1, b1);
+  arp2(id1, a1, b1);
   int e2 = entry(a1, b1);
   uint32_t jj1 = (uint32_t)p.Aci[e2];   // row me: A column / value of this thread's entry
   float av1 = p.Av[e2];
   uint4 wa1 = ra.ws8[2 * (int64_t)jj1];   // ... its packed bounds and the row's unit offsets
   uint2 wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj1 + 1);
-  int64_t uo1 = uoff_of(me);
+  int64_t uo1 = uoff_of(id1);
   int na1 = __builtin_amdgcn_readfirstlane(b1 - a1);
-  arp2(me + NG, a2, b2);
+  arp2(id2, a2, b2);
   e2 = entry(a2, b2);
   uint32_t jj2 = (uint32_t)p.Aci[e2];   // row me + NG: its A entries
   float av2 = p.Av[e2];
   int na2 = b2 - a2;
-  arp2(me + 2 * NG, a3, b3);            // row me + 2 NG: its row pointers
-  // Once per row, in the LAST unit of row r (after its pass 1, with loads
-  // that land while the unit finishes): row r + NG's inputs are taken into
-  // the staging registers, then row r + 2 NG's bounds and offsets are loaded
-  // from its A columns (landed one row ago), row r + 3 NG's A entries from its
-  // row pointers (idem) and row r + 4 NG's row pointers.  No load sits under
-  // a branch and none is consumed in the unit that issues it.
-  auto row_block = [&](int r) {
+  arp2(id3, a3, b3);                    // row me + 2 NG: its row pointers
+  // Once per row, in the LAST unit of the current row (after its pass 1, with
+  // loads that land while the unit finishes): the next row's inputs are taken
+  // into the staging registers, then the row after's bounds and offsets are
+  // loaded from its A columns (landed one row ago), the third row's A entries
+  // from its row pointers (idem) and the fourth row's row pointers.  No load
+  // sits under a branch and none is consumed in the unit that issues it.
+  auto row_block = [&](int next_id) {
+    id1 = id2;
+    id2 = id3;
+    id3 = next_id;
     jj1 = jj2;
     wa1 = ra.ws8[2 * (int64_t)jj1];
     wb1 = *reinterpret_cast<const uint2*>(ra.ws8 + 2 * (int64_t)jj1 + 1);
-    uo1 = uoff_of(r + 2 * NG);
+    uo1 = uoff_of(id1);
     av1 = av2;
     na1 = __builtin_amdgcn_readfirstlane(na2);
     e2 = entry(a3, b3);
     jj2 = (uint32_t)p.Aci[e2];
     av2 = p.Av[e2];
     na2 = b3 - a3;
-    arp2(r + 4 * NG, a3, b3);
+    arp2(id3, a3, b3);
   };
 
   // staging registers of the row being staged
-  int cna = 0;
+  int cna = 0, cid = me;   // (cid: its row id)
   float cav = 0.f;
   uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0;   // 16-bit window lengths, two per word; cl0 = the word
                                                   // of the window being staged (shifted down every two
@@ -1479,6 +1517,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
                                                   // put in scratch)
   uint32_t bq = 0;   // this thread's entry: first pair of the next window to stage
   auto take_row = [&]() {   // the next row's inputs -> staging registers (their loads have landed)
+    cid = id1;
     cna = na1;
     cav = av1;
     bq = wb1.y;   // first pair of the entry's B row in the padded pair array
@@ -1593,8 +1632,8 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
     }
   };
 
-  take_row();           // staging registers: row me
-  row_block(me - NG);   // next-row registers: row me + NG's bounds; A entries of me + 2 NG; Arp of me + 3 NG
+  take_row();     // staging registers: row me
+  row_block(me + 3 * NG);   // next-row registers: row me + NG's bounds; A entries of me + 2 NG; Arp of me + 3 NG
   stage();
   issue_loads();
   // the loop is entered with the same stores behind the first unit's B
@@ -1610,11 +1649,14 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
       const int TC = sTC, nr = snr, clo = sclo, want = swant;
       const int64_t off = soff;
       int lim = 0;
+      int tk = 0;
+      if constexpr (LAST && (SPMM_BM_TICKETS & 1))
+        if (tid == 0) tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rtk, tkz, 0, 0);   // (to LDS at the unit's end)
       BM_STAMP(4);   // (the previous unit's write-out)
       if (sskip) {   // uniform
         if constexpr (LAST) {
           take_row();
-          row_block(row);
+          row_block(next_row());
         }
       } else {
         // ---- pass 1: the landed products, columns into the bitmap --------
@@ -1644,7 +1686,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
         __syncthreads();
         if constexpr (LAST) {   // the next row into the staging registers; the row inputs move along
           take_row();
-          row_block(row);
+          row_block(next_row());
         }
         BM_STAMP(1);
         // ---- rank prefix per 64-bit word (as spgemm_bm_rows) ------------
@@ -1753,7 +1795,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
       // ---- stage the next unit and issue its B gathers; then this unit's write-out
       bool more = true;
       if constexpr (LAST) {
-        srow = row + NG;
+        srow = cid;   // (taken in this unit)
         sq = 0;
         more = srow < m;
       } else {
@@ -1770,8 +1812,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
       BM_STAMP(0);
       BM_STAMP_UNIT();
       write_out(off, lim);
+      if constexpr (LAST && (SPMM_BM_TICKETS & 1)) {
+        if (tid == 0) s_tk[kl & 1] = 6 * NG + tk;   // (read in row kl + 2's last unit, barriers between)
+        ++kl;
+      }
       };
-  for (int row = me; row < m; row += NG) {
+  for (int row = me; row < m; row = srow) {   // (srow: the next row, staged by the row's last unit)
     for (int q = 0; q + 1 < nwin; ++q) unit(std::false_type{}, row, q);
     unit(std::true_type{}, row, nwin - 1);
   }
@@ -2030,6 +2076,7 @@ struct BmCountPipeArgs {
   BmRowArgs r;
   uint32_t colp_bytes;   // bytes of the padded column array (< 2^32: checked by the host)
   int64_t annz;          // nnz(A) > 0
+  int32_t* ticket;       // row ticket counter, zero at launch
 };
 
 template <int LGW, int NT, int RR, int CCAP>
@@ -2048,6 +2095,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
   __shared__ int wscan[2 * NW];
   __shared__ int csum[NW];
+  __shared__ int s_tk[2];   // row tickets (as spgemm_bm_rows_pipe)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2071,6 +2119,16 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   const int m = (int)p.m;
   const int annz = (int)pa.annz;
   const int ngc = (nwin + 1) / 2;   // units per row
+  // row schedule: six static rows, then tickets (as spgemm_bm_rows_pipe)
+  int kl = 0;
+  int tkz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(tkz));
+  const auto rtk = __builtin_amdgcn_make_buffer_rsrc(pa.ticket, 0, 4, 0x00020000);
+  int id1 = me, id2 = me + NG, id3 = me + 2 * NG;
+  auto next_row = [&]() {
+    if constexpr (!(SPMM_BM_TICKETS & 2)) return id3 + NG;
+    return kl < 2 ? me + (kl + 4) * NG : __builtin_amdgcn_readfirstlane(s_tk[kl & 1]);
+  };
 
   // ---- row pipeline (as spgemm_bm_rows_pipe) --------------------------------
   auto arp2 = [&](int r, int& a, int& b) {   // (low words: nnz(A) < 2^31)
@@ -2085,31 +2143,35 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     return e < annz ? e : annz - 1;
   };
   int a1 = 0, b1 = 0, a2 = 0, b2 = 0, a3 = 0, b3 = 0;
-  arp2(me, a1, b1);
+  arp2(id1, a1, b1);
   uint32_t jj1 = (uint32_t)p.Aci[entry(a1, b1)];
   uint4 wa1 = ra.ws8[2 * (int64_t)jj1];       // {., lengths of windows 0-1, 2-3, 4-5}
   uint4 wb1 = ra.ws8[2 * (int64_t)jj1 + 1];   // {lengths 6-7, ., first padded column, .}
   int na1 = __builtin_amdgcn_readfirstlane(b1 - a1);
-  arp2(me + NG, a2, b2);
+  arp2(id2, a2, b2);
   uint32_t jj2 = (uint32_t)p.Aci[entry(a2, b2)];
   int na2 = b2 - a2;
-  arp2(me + 2 * NG, a3, b3);
-  // once per row, at the top of row r's last unit (after take_row took row
-  // r + NG): row r + 2 NG's bounds, row r + 3 NG's A columns, row r + 4 NG's
-  // row pointers (as spgemm_bm_rows_pipe's row_block)
-  auto row_block = [&](int r) {
+  arp2(id3, a3, b3);
+  // once per row, at the top of the row's last unit (after take_row took the
+  // next row): the row after's bounds, the third row's A columns, the fourth
+  // row's row pointers (as spgemm_bm_rows_pipe's row_block)
+  auto row_block = [&](int next_id) {
+    id1 = id2;
+    id2 = id3;
+    id3 = next_id;
     wa1 = ra.ws8[2 * (int64_t)jj2];
     wb1 = ra.ws8[2 * (int64_t)jj2 + 1];
     na1 = __builtin_amdgcn_readfirstlane(na2);
     jj2 = (uint32_t)p.Aci[entry(a3, b3)];
     na2 = b3 - a3;
-    arp2(r + 4 * NG, a3, b3);
+    arp2(id3, a3, b3);
   };
 
-  int cna = 0;
+  int cna = 0, cid = me;   // (cid: the staged row's id)
   uint32_t cl0 = 0, cl1 = 0, cl2 = 0, cl3 = 0;   // a unit's two 16-bit lengths: cl0 (shifted down per unit)
   uint32_t bq = 0;
   auto take_row = [&]() {
+    cid = id1;
     cna = na1;
     bq = wb1.z;
     cl0 = wa1.y;
@@ -2206,7 +2268,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
 
   // prologue: the first unit staged and its loads issued
   take_row();
-  row_block(me - NG);
+  row_block(me + 3 * NG);
   next_inputs();
   scan_begin();
   __syncthreads();
@@ -2219,9 +2281,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   auto unit = [&](auto last_tag, int row, int g) {
     constexpr bool LAST = decltype(last_tag)::value;
     const int u = su, q0 = sq, TC = sTC, nr = snr, clo = sclo, P = sP;
+    int tk = 0;
+    if constexpr (LAST && (SPMM_BM_TICKETS & 2))
+      if (tid == 0) tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rtk, tkz, 0, 0);   // (to LDS at the unit's end)
     if constexpr (LAST) {   // the next row into the staging registers; the row inputs move along
       take_row();
-      row_block(row);
+      row_block(next_row());
     }
     // ---- ORs of unit k (its loads landed) --------------------------------
 #pragma unroll
@@ -2233,12 +2298,12 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
       or_cols(x, ok4, clo);
     }
     // the next unit's scan inputs
-    const bool more = !LAST || row + NG < m;
+    const bool more = !LAST || cid < m;
     next_inputs();
     scan_begin();
     __syncthreads();   // A: every OR of unit k done; the next scan's wave sums written
     BM_STAMP(5);
-    if (more) scan_end(LAST ? (row + NG) * nwin : row * nwin + 2 * (g + 1), LAST ? 0 : 2 * (g + 1));
+    if (more) scan_end(LAST ? cid * nwin : row * nwin + 2 * (g + 1), LAST ? 0 : 2 * (g + 1));
     __syncthreads();   // E: the next unit's descriptors written
     if (more) {
       SPMM_BM_PRIO_HI();
@@ -2259,7 +2324,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     if (lane == 0) csum[w] = cnt;
     // a unit of more chunks than the descriptor buffer (long two-window segments under a
     // 256-entry A row): its count is short -> err bit 6, the host recounts the product on
-    // the flat row kernel, which takes descriptors in batches (a batch loop here changes
+    // the per-unit kernels, which take descriptors in batches (a batch loop here changes
     // hipcc's schedule of the ORs above: every OR became its own branch)
     if (TC > CCAP && tid == 0) atomicOr(p.err, 64);
     __syncthreads();   // F: bitmap clear for the next ORs, csum written
@@ -2269,9 +2334,13 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[(lane & 1) * WAVES_PER_WIN + i];
     const bool wr = w == 0 && lane < NSUB && q0 + lane < nwin;
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, rsu, wr ? (u + lane) * 4 : -1, 0, 0);
+    if constexpr (LAST && (SPMM_BM_TICKETS & 2)) {
+      if (tid == 0) s_tk[kl & 1] = 6 * NG + tk;   // (read in row kl + 2's last unit, barriers between)
+      ++kl;
+    }
     BM_STAMP(6);
   };
-  for (int row = me; row < m; row += NG) {
+  for (int row = me; row < m; row = cid) {   // (cid: the next row, taken by the row's last unit)
     for (int g = 0; g + 1 < ngc; ++g) unit(std::false_type{}, row, g);
     unit(std::true_type{}, row, ngc - 1);
   }
@@ -2419,7 +2488,7 @@ int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s)
   // pipeline only adds work -- 65536^2 count 1.32 -> 1.36 ms step, PERF_LOG round 5)
   if (ra.pad && pipe && nsub == 2 && ra.a.nwin >= 3 && K2::NT == BmRowCountPipe<C>::NT && annz > 0 &&
       colp_bytes < (int64_t(1) << 32) && ra.a.m * ra.a.nwin < (int64_t(1) << 30))
-    return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz}, ra.a.m, s,
+    return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz, ra.a.err + 3}, ra.a.m, s,
                        BmRowCountPipe<C>::NT);
   if (ra.pad)
     return nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT);
@@ -2435,7 +2504,7 @@ int bm_numeric_rows(BmRowArgs ra, int det, int64_t nbcv, int pipe, int64_t annz,
   // the padded pairs fit 32-bit buffer offsets
   const bool wide = ra.a.Bcv && ra.pad && ra.a.lg >= 1;
   const bool piped = wide && !det && pipe && annz > 0 && nbcv > 0 && nbcv * 8 < (int64_t(1) << 32);
-  const int rc = piped ? launch_rows(K::kpipe, BmPipeArgs{ra, (uint32_t)(nbcv * 8), annz}, ra.a.m, s, K::NT)
+  const int rc = piped ? launch_rows(K::kpipe, BmPipeArgs{ra, (uint32_t)(nbcv * 8), annz, ra.a.err + 2}, ra.a.m, s, K::NT)
                : det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
                      : (wide ? launch_rows(K::kcvw, ra, s, K::NT)
                              : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT)));
@@ -2545,7 +2614,8 @@ SPMM_EXPORT int spmm_spgemm_bm_wg_times(int on, unsigned long long* out, int n) 
 // reload kernel over the deferred units; same contract as spmm_spgemm_bm_numeric.
 // Bcv: optional [nnz(B)] (column, value bits) pairs read by the row-major kernel.
 // nbcv: pairs in Bcv; pipe: the software-pipelined kernel (padded pairs, unordered
-// sum, nbcv * 8 < 2^32, annz = nnz(A) > 0), else the flat one.
+// sum, nbcv * 8 < 2^32, annz = nnz(A) > 0; err then int32[4]: err[2] is its row-ticket
+// counter, zero at launch), else the flat one.
 SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                             const void* ws8, const uint32_t* ws, const int32_t* Bci, const float* Bv,
                                             const void* Bcv,
@@ -2571,7 +2641,8 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
 // output as spmm_spgemm_bm_count.  Returns without counting when err bit 3
 // is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
 // pad: Bci is the padded column array of spmm_spgemm_bm_pad_pairs (gc = nsub).
-// pipe: the pipelined kernel (pad, nsub 2, nnzb * 4 < 2^32, annz = nnz(A) > 0).
+// pipe: the pipelined kernel (pad, nsub 2, nnzb * 4 < 2^32, annz = nnz(A) > 0; err then
+// int32[4]: err[3] is its row-ticket counter, zero at launch).
 SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
                                           const int32_t* Bci, int64_t m, int nwin, int lg, int nsub, int32_t* ucnt,
                                           int32_t* err, int64_t nnzb, int pad, int pipe, int64_t annz, void* stream) {

@@ -148,7 +148,7 @@ bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
     SpmmBmPlan p{};
     if (spmm_spgemm_bm_make_plan(&o, A.m, A.nnz, B.m, B.n, B.nnz, pl.tot, pl.nz, pl.amax, seg, &p)) return false;
     DevBuf<uint8_t> ws((size_t)std::max<int64_t>(p.ws_bytes, 1), s);
-    DevBuf<int32_t> z(2, s);
+    DevBuf<int32_t> z(4, s);   // err, deferred units, row tickets (csr_bitmap_plan.hip front)
     DevBuf<int64_t> uoff((size_t)p.nunits + 1, s);
     int built = 0;
     A4_HIP((hipError_t)spmm_spgemm_bm_front(&p, A.rp.get(), A.ci.get(), B.rp.get(), B.ci.get(), B.v.get(), ws.get(),
@@ -245,7 +245,7 @@ void long_rows(int values, const DCsr& A, const DCsr& B, const std::vector<int32
                                               scratch.get(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                               nullptr, s));
     DevBuf<int64_t> rt_nnz((size_t)R * nch, s);
-    DevBuf<int32_t> lists((size_t)2 * R * nch + 2, s);
+    DevBuf<int32_t> lists((size_t)2 * R * nch + 4, s);
     A4_HIP((hipError_t)spmm_spgemm_long_dense(values, drt_off.get(), T.get(), R * nch, nch, scratch.get(), rt_nnz.get(),
                                               lists.get(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s));
     const std::vector<int64_t> nz = down(rt_nnz.get(), (size_t)R * nch, s);

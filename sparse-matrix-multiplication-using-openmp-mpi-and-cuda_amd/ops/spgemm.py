@@ -398,7 +398,7 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         if LONG_STATS is not None:
             _long_stats(rt_cnt + D.reshape(-1) if direct else rt_cnt)
         rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
-        lists = torch.empty(2 * R * nch + 2, dtype=torch.int32, device=dev)   # the two kernels' item lists
+        lists = torch.empty(2 * R * nch + 4, dtype=torch.int32, device=dev)   # the two kernels' item lists + counters
         _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
                                                  P(lists), P(D) if direct else nil, P(dl) if direct else nil,
                                                  P(dl_rp) if direct else nil, P(btab) if direct else nil,
@@ -790,7 +790,8 @@ def bitmap_buffers(plan: BitmapPlan, dev: torch.device, cap: Optional[int] = Non
     use them are graph-capturable as they are."""
     raw = plan.raw
     out = dict(ws=torch.empty(max(raw.ws_bytes, 1), dtype=torch.uint8, device=dev),
-               z=torch.empty(2, dtype=torch.int32, device=dev),   # err, deferred count (zeroed by the front)
+               # err, deferred count, numeric / count row tickets (zeroed by the front)
+               z=torch.empty(4, dtype=torch.int32, device=dev),
                uoff=torch.empty(raw.nunits + 1, dtype=torch.int64, device=dev), nunits=raw.nunits, ws8=bool(raw.ws8))
     if cap is not None:
         out.update(Cci=torch.empty(cap, dtype=torch.int32, device=dev),
@@ -871,7 +872,7 @@ def _bitmap_finish(A: CSR, B: CSR, plan: BitmapPlan, out: dict, info: SpgemmInfo
             return "eager"
     else:
         nnz = out["nnz"]
-        e, deferred = z.tolist()
+        e, deferred = z[:2].tolist()
     info.nnz = nnz
     info.rows_per_bin_num["bitmap_units"] = out["nunits"]
     info.rows_per_bin_num["bitmap_cfg"] = plan.cfg

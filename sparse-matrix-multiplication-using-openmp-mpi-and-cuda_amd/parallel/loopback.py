@@ -252,12 +252,14 @@ class PanelComm(Comm):
     issue order (columns, then values): ``tools/rank_emulate.py`` models a
     rank of an N-GPU node with it; tests drive the W-rank branches with it."""
 
-    def __init__(self, rank: int, world: int, dev: torch.device, panels, gbps: float = 0.0):
+    def __init__(self, rank: int, world: int, dev: torch.device, panels, gbps: float = 0.0, link_priority: int = 0):
         super().__init__(rank, world, rank, dev, "panels")
         if len(panels) != world:
             raise ValueError("PanelComm: one B panel per rank")
         self.panels, self.gbps = panels, gbps
-        self.link = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        # (``link_priority`` -1: a high-priority stream, whose transfers the dispatcher puts
+        # ahead of the compute stream's large grids; tools/rank_emulate.py --link-priority)
+        self.link = torch.cuda.Stream(dev, priority=link_priority) if dev.type == "cuda" else None
         self._n = 0
 
     @property

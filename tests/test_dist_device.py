@@ -349,6 +349,7 @@ def _graph_case(world: int, steps: int = 3):
                 C = g.result()
                 outs.append((C.rowptr.cpu(), C.col.cpu(), C.val.cpu()))
             torch.cuda.current_stream(dev).synchronize()
+            comm.barrier()   # every rank past its last replay before any graph is destroyed
             del g
             return outs
 
@@ -402,15 +403,21 @@ def _graph_case_panels(world: int):
     kc = [0] + [k * (r + 1) // world for r in range(world)]
     if world >= 3:   # an empty B panel, an uneven neighbour
         kc[2] = kc[1]
+    panels = [B.row_slice(kc[q], kc[q + 1]).to(dev) for q in range(world)]
+    # every rank's graph built first and kept to the end: no captured graph is destroyed while
+    # another is still replayed (on ROCm 7.2 that sequence faulted after eager launches in
+    # between: gpurun_out/r6g07, PERF_LOG round 6)
+    graphs = [MS.RowblockGraph(A.row_slice(rc[r], rc[r + 1]).to(dev), panels[r], PanelComm(r, world, dev, panels))
+              for r in range(world)]
     for r in range(world):
-        panels = [B.row_slice(kc[q], kc[q + 1]).to(dev) for q in range(world)]
-        Ap = A.row_slice(rc[r], rc[r + 1]).to(dev)
-        g = MS.RowblockGraph(Ap, panels[r], PanelComm(r, world, dev, panels))
+        g = graphs[r]
         for s in (1.0, -2.0):
             for q in range(world):   # every rank's panel changes (PanelComm gathers their current values)
                 panels[q].val.mul_(s)
             g.run()
-            C = g.result()
+            info = SG.SpgemmInfo()
+            C = g.result(info)
+            assert C is not None, (world, r, s, g.bufs["z"].tolist(), info.rows_per_bin_num)
             ref = SG.spgemm(A.to(dev), CS.CSR(k, n, B.rowptr.to(dev),
                                               torch.cat([p.col for p in panels]),
                                               torch.cat([p.val for p in panels]))).row_slice(rc[r], rc[r + 1])

@@ -59,6 +59,8 @@ def main() -> None:
     ap.add_argument("--graph", action="store_true", help="time the local product as a SpgemmGraph replay")
     ap.add_argument("--gather-gbps", default="", help="comma list: emulate the whole step at these link rates")
     ap.add_argument("--no-local", action="store_true", help="skip the local-product timings")
+    ap.add_argument("--link-priority", type=int, default=0,
+                    help="stream priority of the emulated link (-1: high, dispatched ahead of the compute grids)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     _native.hip()
@@ -82,7 +84,7 @@ def main() -> None:
         panels = [uniform_csr(a.n, a.n, a.density, seed=a.seed + 1, device=dev, rows=p) for p in pan]
         steps = {}
         for g in [float(x) for x in a.gather_gbps.split(",")]:
-            comm = PanelComm(a.rank, a.world, dev, panels, g)
+            comm = PanelComm(a.rank, a.world, dev, panels, g, link_priority=a.link_priority)
             rg = MS.RowblockGraph(A, panels[a.rank], comm)
             steps[str(g)] = round(timed(rg.run, a.steps), 3)
             C = rg.result()
