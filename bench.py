@@ -319,7 +319,7 @@ def main() -> None:
     ap.add_argument("--matrix-density", dest="density", type=float, default=1e-4)
     ap.add_argument("--spmm-n", type=int, default=65536)
     ap.add_argument("--spmm-density", type=float, default=1e-3)
-    ap.add_argument("--spmm-method", default="auto", choices=["auto", "mfma", "sweep", "rowwise"],
+    ap.add_argument("--spmm-method", default="auto", choices=["auto", "mfma", "panel", "sweep", "rowwise"],
                     help="spmm workload: executor (auto: the fastest measured on the real operands)")
     ap.add_argument("--scale", type=int, default=24, help="R-MAT scale (BASELINE config 5: 24)")
     ap.add_argument("--rmat-stream", default="auto", choices=["auto", "on", "off"],

@@ -19,7 +19,7 @@ struct SpmmBmOpts {
 
 struct SpmmBmPlan {
   int32_t cfg, lgw, nwin, nsub, lg_count, lg_c, nsub_c, lg_num;
-  int32_t count_rows, rows, det, pipe, ws8, pad_num, pad_cnt, plain_cv;
+  int32_t count_rows, rows, det, pipe, ws8, pad_num, pad_cnt;
   int64_t m, annz, mb, nnzb, tot, nunits, ngc, cap_bcv, cap_colp, ovf_cap;
   // workspace byte offsets (-1: not used) and size
   int64_t o_split, o_ucnt, o_ws8, o_plen, o_plenc, o_pbase, o_cbase, o_colp, o_bcv, o_ovf, o_scan, ws_bytes;

@@ -3,8 +3,8 @@
 // the packed 16-bit window lengths (ws8) of the row kernels, B's padded
 // layouts (every (row, window) pair segment and every (row, count group)
 // column segment starting on a 128-byte line, so the kernels gather them 16
-// bytes per lane), the plain interleaved (column, value) pairs, and the unpack
-// of an all-gathered operand payload (models/spgemm.py).
+// bytes per lane), and the pack / unpack of an all-gathered operand payload
+// (models/spgemm.py).
 #include "bitmap_common.hpp"
 #include "common.hpp"
 
@@ -129,44 +129,66 @@ __global__ __launch_bounds__(256) void bm_window_splits(const int64_t* __restric
   ws[t] = (uint32_t)lo;
 }
 
-// ---- operand layout kernels ------------------------------------------------
-// B as interleaved (column, value bits) pairs for the row-major numeric
-// kernel: 4 entries per thread, 16-byte loads and stores.
-__global__ __launch_bounds__(256) void bm_interleave(const int32_t* __restrict__ col, const uint32_t* __restrict__ val,
-                                                    int64_t n, uint2* __restrict__ cv) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i + 3 < n && ((reinterpret_cast<uintptr_t>(col + i) | reinterpret_cast<uintptr_t>(val + i)) & 15) == 0) {
-    const int4 c = *reinterpret_cast<const int4*>(col + i);
-    const uint4 v = *reinterpret_cast<const uint4*>(val + i);
-    reinterpret_cast<uint4*>(cv + i)[0] = make_uint4((uint32_t)c.x, v.x, (uint32_t)c.y, v.y);
-    reinterpret_cast<uint4*>(cv + i)[1] = make_uint4((uint32_t)c.z, v.z, (uint32_t)c.w, v.w);
-    return;
-  }
-  for (int64_t k = i; k < i + 4 && k < n; ++k) cv[k] = make_uint2((uint32_t)col[k], val[k]);
-}
-
 // The all-gathered right operand of a row-block SpGEMM -> contiguous arrays
 // in one pass (replaces concatenations and an interleave copy).  Rank r's
-// columns are gc[r * gstride + i] and its value bits gv[r * gstride + i],
+// columns are at gc + r * cstride (bits < 32: packed by bm_pack_bits, entry i
+// at bit i * bits; else one word each), its value bits gv[r * gstride + i],
 // i < base[r + 1] - base[r] (base[r] = first output index of rank r).  Any of
 // col / val / cv may be null; with gc null the columns are read back from
 // col (already unpacked: the two-stage gather, columns first).
+// A workgroup takes kUnpackPer x 256 consecutive entries of one rank (strided
+// by 256: coalesced), so the grid is small enough that workgroup dispatch does
+// not bound the pass (one entry a thread ran at ~2 TB/s).
+constexpr int kUnpackPer = 8;
 __global__ __launch_bounds__(256) void bm_unpack_gathered(const uint32_t* __restrict__ gc, const uint32_t* __restrict__ gv,
-                                                         int64_t gstride, const int64_t* __restrict__ base,
+                                                         int64_t gstride, int64_t cstride, int bits,
+                                                         const int64_t* __restrict__ base,
                                                          int32_t* __restrict__ col, uint32_t* __restrict__ val,
                                                          uint2* __restrict__ cv) {
   const int r = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t b0 = base[r], n = base[r + 1] - b0;
-  if (i >= n) return;
-  const int64_t src = (int64_t)r * gstride + i;
-  const uint32_t c = gc ? gc[src] : (uint32_t)col[b0 + i];
-  if (gc && col) col[b0 + i] = (int32_t)c;
-  if (gv) {
-    const uint32_t v = gv[src];
-    if (val) val[b0 + i] = v;
-    if (cv) cv[b0 + i] = make_uint2(c, v);
+  const uint32_t* g = gc + (int64_t)r * cstride;
+  const uint32_t msk = bits < 32 ? (1u << bits) - 1u : ~0u;
+#pragma unroll
+  for (int k = 0; k < kUnpackPer; ++k) {
+    const int64_t i = ((int64_t)blockIdx.x * kUnpackPer + k) * 256 + threadIdx.x;
+    if (i >= n) break;
+    uint32_t c;
+    if (!gc) {
+      c = (uint32_t)col[b0 + i];
+    } else if (bits < 32) {   // two aligned words hold the entry (the sender pads one word)
+      const int64_t o = i * bits;
+      const uint64_t two = (uint64_t)g[(o >> 5) + 1] << 32 | g[o >> 5];
+      c = (uint32_t)(two >> (o & 31)) & msk;
+    } else {
+      c = g[i];
+    }
+    if (gc && col) col[b0 + i] = (int32_t)c;
+    if (gv) {
+      const uint32_t v = gv[(int64_t)r * gstride + i];
+      if (val) val[b0 + i] = v;
+      if (cv) cv[b0 + i] = make_uint2(c, v);
+    }
   }
+}
+
+// Column indices of an operand panel packed to `bits` (< 32) bits each for the
+// all-gather: entry i at bit i * bits of a little-endian word stream, one
+// thread per output word (no atomics), words past the entries zero.  Columns
+// < 2^bits (the caller's bits = ceil(log2 n)); 1M columns cross xGMI in 20 bits.
+__global__ __launch_bounds__(256) void bm_pack_bits(const uint32_t* __restrict__ src, int64_t n, int bits,
+                                                   uint32_t* __restrict__ dst, int64_t words) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= words) return;
+  const int64_t lo = w * 32;
+  const int64_t iend = min((lo + 32 + bits - 1) / bits, n);
+  uint64_t acc = 0;
+  for (int64_t i = lo / bits; i < iend; ++i) {
+    const int64_t o = i * bits - lo;   // < 32; negative: the entry began in the previous word
+    const uint64_t v = src[i];
+    acc |= o >= 0 ? v << o : v >> -o;
+  }
+  dst[w] = (uint32_t)acc;
 }
 
 }  // namespace
@@ -216,28 +238,32 @@ SPMM_EXPORT int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col,
   return 0;
 }
 
-// Interleaved (column, value bits) copy of B for the row-major numeric kernel.
-SPMM_EXPORT int spmm_spgemm_bm_interleave(const int32_t* col, const float* val, int64_t n, void* cv, void* stream) {
-  if (n <= 0) return 0;
-  const int64_t th = (n + 3) / 4;
-  hipLaunchKernelGGL(bm_interleave, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, (hipStream_t)stream, col,
-                     (const uint32_t*)val, n, (uint2*)cv);
+// Unpack an all-gathered operand payload: rank r's columns at gc + r *
+// cstride (packed to `bits` bits when bits < 32), its value bits at gv + r *
+// gstride (either may be null, see the kernel); base: device int64[world + 1]
+// output offsets.
+SPMM_EXPORT int spmm_spgemm_bm_unpack_gathered(const void* gc, const void* gv, int world, int64_t gstride,
+                                               int64_t cstride, int bits, const int64_t* base, int64_t max_n,
+                                               int32_t* col, float* val, void* cv, void* stream) {
+  if (world <= 0 || max_n <= 0) return 0;
+  if (world > 65535 || (max_n + 255) / 256 > (int64_t)UINT32_MAX || bits < 1 || bits > 32) return (int)hipErrorInvalidValue;
+  if (!gc && !col) return (int)hipErrorInvalidValue;
+  if (gc && bits < 32 && cstride < (max_n * bits + 31) / 32 + 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bm_unpack_gathered, dim3((unsigned)((max_n + 256 * kUnpackPer - 1) / (256 * kUnpackPer)), (unsigned)world), dim3(256), 0,
+                     (hipStream_t)stream, (const uint32_t*)gc, (const uint32_t*)gv, gstride, cstride, bits, base, col,
+                     (uint32_t*)val, (uint2*)cv);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
 
-// Unpack an all-gathered operand payload: rank r's columns at gc + r *
-// gstride, its value bits at gv + r * gstride (either may be null, see the
-// kernel); base: device int64[world + 1] output offsets.
-SPMM_EXPORT int spmm_spgemm_bm_unpack_gathered(const void* gc, const void* gv, int world, int64_t gstride,
-                                               const int64_t* base, int64_t max_n, int32_t* col, float* val, void* cv,
-                                               void* stream) {
-  if (world <= 0 || max_n <= 0) return 0;
-  if (world > 65535 || (max_n + 255) / 256 > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
-  if (!gc && !col) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_unpack_gathered, dim3((unsigned)((max_n + 255) / 256), (unsigned)world), dim3(256), 0,
-                     (hipStream_t)stream, (const uint32_t*)gc, (const uint32_t*)gv, gstride, base, col,
-                     (uint32_t*)val, (uint2*)cv);
+// Pack n column indices (each < 2^bits, 1 <= bits < 32) into `words` words
+// (>= (n * bits + 31) / 32 + 1: the unpacker reads two words an entry).
+SPMM_EXPORT int spmm_pack_bits(const int32_t* src, int64_t n, int bits, uint32_t* dst, int64_t words, void* stream) {
+  if (words <= 0) return 0;
+  if (n < 0 || bits < 1 || bits > 31 || words < (n * bits + 31) / 32 + 1 || (words + 255) / 256 > (int64_t)UINT32_MAX)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bm_pack_bits, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint32_t*)src, n, bits, dst, words);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -30,7 +30,6 @@ int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin, void* ws8,
 int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb, int nwin, int lgw,
                              const int64_t* pbase, void* ws8, void* out, const int64_t* cbase, int gc, int32_t* outc,
                              int64_t cap, int64_t cap_c, int32_t* err, void* stream);
-int spmm_spgemm_bm_interleave(const int32_t* col, const float* val, int64_t n, void* cv, void* stream);
 int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const uint32_t* ws, const int32_t* Bci,
                          int64_t m, int nwin, int lg, int32_t* ucnt, int32_t* err, void* stream);
 int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8, const int32_t* Bci,
@@ -155,10 +154,18 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   p->lg_c = sl < 48 ? 4 : (sl < 96 ? 5 : 6);
   p->nsub_c = nsub_c;
   p->lg_num = seg / nwin < 48 ? 4 : (seg / nwin < 96 ? 5 : 6);
-  p->count_rows = ws8_ok && amax >= 0 && amax <= 256;
-  p->rows = ws8_ok && (o->rows_mode == 2 || cfg == 0);
   p->det = o->det != 0;
   p->pipe = o->pipe != 0;
+  // the row kernels exist only in their pipelined forms (padded layouts, 32-bit buffer
+  // offsets, unordered sums); every other product takes the per-unit kernels
+  const bool pad = o->pad != 0 && o->use_ws8 != 0;
+  const int64_t ngc = (nwin + nsub_c - 1) / nsub_c;
+  const int64_t cap_bcv = bnnz + (kPadPairs - 1) * (int64_t)nwin * mb;
+  const int64_t cap_colp = bnnz + (kPadCols - 1) * ngc * mb;
+  p->count_rows = ws8_ok && amax >= 0 && amax <= 256 && pad && p->pipe && nsub_c == 2 && nwin >= 3 && annz > 0 &&
+                  cap_colp * 4 < ((int64_t)1 << 32) && m * nwin < ((int64_t)1 << 30);
+  p->rows = ws8_ok && (o->rows_mode == 2 || cfg == 0) && pad && o->cv != 0 && !p->det && p->pipe && annz > 0 &&
+            cap_bcv * 8 < ((int64_t)1 << 32);
   p->m = m;
   p->annz = annz;
   p->mb = mb;
@@ -166,14 +173,12 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   p->tot = tot;
   p->nunits = m * nwin;
   p->ngc = (nwin + nsub_c - 1) / nsub_c;
-  const bool pad = o->pad != 0 && o->use_ws8 != 0;
-  p->pad_num = pad && (p->rows || !p->det) && o->cv != 0 && bnnz + (kPadPairs - 1) * (int64_t)nwin * mb < ((int64_t)1 << 32);
-  p->pad_cnt = pad && p->count_rows && bnnz + (kPadCols - 1) * p->ngc * mb < ((int64_t)1 << 32);
+  p->pad_num = pad && (p->rows || !p->det) && o->cv != 0 && cap_bcv < ((int64_t)1 << 32);
+  p->pad_cnt = p->count_rows;   // (its conditions include the padded layout's)
   p->ws8 = o->use_ws8 != 0 && ws8_ok && (p->count_rows || p->rows || p->pad_num);
-  if (!p->ws8) p->pad_num = p->pad_cnt = 0;
-  p->plain_cv = p->ws8 && p->rows && !p->pad_num && o->cv != 0;   // unpadded interleaved pairs
-  p->cap_bcv = p->pad_num ? bnnz + (kPadPairs - 1) * (int64_t)nwin * mb : (p->plain_cv ? bnnz : 0);
-  p->cap_colp = p->pad_cnt && p->count_rows ? bnnz + (kPadCols - 1) * p->ngc * mb : 0;
+  if (!p->ws8) p->pad_num = p->pad_cnt = p->rows = p->count_rows = 0;
+  p->cap_bcv = p->pad_num ? cap_bcv : 0;
+  p->cap_colp = p->pad_cnt ? cap_colp : 0;
   p->ovf_cap = std::max<int64_t>(1, std::min<int64_t>(p->nunits, kOvfCap));
   int64_t off = 0;
   auto take = [&](int64_t bytes, bool on) -> int64_t {
@@ -265,7 +270,6 @@ SPMM_EXPORT int spmm_spgemm_bm_back(const SpmmBmPlan* p, const int64_t* Arp, con
                                     p->cap_bcv, 0, z, s));
   }
   if (p->ws8 && p->rows) {
-    if (p->plain_cv) BM_TRY(spmm_spgemm_bm_interleave(Bci, Bv, p->nnzb, bcv, s));
     return spmm_spgemm_bm_numeric_rows(p->cfg, Arp, Aci, Av, ws8, split, Bci, Bv, bcv, p->m, p->nwin, p->lg_num, uoff,
                                        cap, Cci, Cv, ovf, novf, p->ovf_cap, z, p->det, p->pad_num, p->cap_bcv,
                                        p->pipe, p->annz, s);

@@ -905,16 +905,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   if constexpr (MODE == 1) BM_WG_FLUSH();
 }
 
-// ---- row-major numeric kernel (nwin <= 8) ---------------------------------
-// A workgroup takes whole rows (row k*gridDim + perm(g)) and runs their
-// windows back to back, so the A row and all its window bounds are loaded
-// ONCE per row, one row ahead: the A entries of row k+1 and the row pointers
-// of row k+2 before row k's first B pass, the packed bounds and output
-// offsets of row k+1 before row k's last B pass.  They are copied into the
-// current-row registers right after that last pass has waited for its B
-// loads, when every one of them has landed (a copy of a register whose load
-// is still in flight would stall the wave for the whole memory latency).
-// Per window the staging is register arithmetic + one scan.
+// ---- row-major kernels (nwin <= 8) -----------------------------------------
+// A workgroup takes whole rows and runs their windows back to back, so the A
+// row and all its window bounds are loaded ONCE per row, rows ahead (see the
+// row pipeline in spgemm_bm_rows_pipe).
 // ws8[j] = {first index of B row j, 16-bit lengths of windows 0..7} (uint4 x 2);
 // ws8[2j + 1].y = first index of row j in the padded pair array (below).
 //
@@ -924,6 +918,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
 // 8L / 128: random segment gathers run at a fixed rate of LINES, and the
 // 1M config's ~13-pair segments gather 1.39x faster aligned (4.64 vs 3.35
 // TB/s useful, tools/probes/seg_gather.hip, profiles/r4/seg_gather.md).
+// (The unpipelined row kernels -- flat numeric, flat count, their
+// deterministic forms -- were removed in round 6: the planner sends every
+// product the pipelined ones cannot take to the per-unit kernels.)
 struct BmRowArgs {
   BmArgs a;
   const uint4* ws8;
@@ -941,417 +938,9 @@ __device__ __forceinline__ uint32_t bm_window_start(const uint4& wa, uint32_t wb
   return b;
 }
 
-// WIDE (padded pairs only): a lane loads TWO (column, value) pairs with one
-// 16-byte load -- half the lanes per chunk, half the load instructions; RR
-// product slots per lane filled by RR / 2 load rounds.
-template <int LGW, int NT, int PCAP, int R, int CCAP, bool CV, bool DET, bool WIDE = false>
-__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows(BmRowArgs ra) {
-  const BmArgs& p = ra.a;
-  constexpr int NW = NT / 64;
-  constexpr int NWORD = (1 << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
-  constexpr int RR = R;                    // product slots per lane
-  constexpr int PPL = WIDE ? 2 : 1;        // pairs per lane and load
-  constexpr int RL = RR / PPL;             // load rounds
-  static_assert(!WIDE || (CV && !DET && RR % 2 == 0), "wide loads: interleaved pairs, unordered mode");
-  constexpr int LCAP = DET ? 256 : 1;   // deterministic fix-up list (fits the 4-workgroup LDS budget)
-  static_assert(WPW % 64 == 0 && PCAP < 65536, "geometry");
-  static_assert(!DET || (CCAP << 6) <= (1 << kKeyBits), "DET keys fit 17 bits");
-
-  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
-  __shared__ __attribute__((aligned(16))) uint16_t pre16[NWORD];
-  __shared__ __attribute__((aligned(16))) unsigned long long items[PCAP];
-  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];   // chunk: {first B index, valid lanes}
-  __shared__ float dval[CCAP];                                 //        a(i, j)
-  __shared__ __attribute__((aligned(8))) uint2 dlist[LCAP];
-  __shared__ int wsum[2 * NW];
-  __shared__ int sdup, sfix, snl;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lgc = p.lg;                    // log2 pairs per chunk
-  const int lg = lgc - (WIDE ? 1 : 0);     // log2 lanes per chunk
-  const int Gc = 1 << lgc;
-  const int Gl = 1 << lg;
-  const int ngrp = NW << (6 - lg);
-  const int gid = (w << (6 - lg)) + (lane >> lg);
-  const int gl = lane & (Gl - 1);
-  const int nwin = p.nwin;
-  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
-  int vz;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-  BM_STAMP_DECL
-  if (*p.err & 8) return;   // ws8 lengths truncated: the host takes the per-unit kernels (uniform exit)
-
-  auto clear_bm = [&]() {
-    for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
-  };
-  clear_bm();
-  if (tid == 0) {
-    sdup = 0;
-    sfix = 0;
-    snl = 0;
-  }
-
-  // 32-bit row indices: the host takes this path only for m * nwin < 2^31
-  const int NG = (int)gridDim.x;
-  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
-  const int m = (int)p.m;
-
-  // row pipeline registers: rows me, me + NG, ...; row1 / row2 = the next two
-  // rows of this workgroup
-  int row = me, row1 = me + NG, row2 = me + 2 * NG;
-  int ca0 = 0, cna = 0;           // its A row (scalars after the copy)
-  float cav = 0.f;                // its A value (thread = entry)
-  uint4 cwa = make_uint4(0, 0, 0, 0);   // its packed window bounds
-  uint32_t cwb = 0;
-  int64_t cuo = 0;                // lane q: uoff[row * nwin + q], q <= nwin
-  int n1a = 0, n1b = 0;           // Arp of row + NG (vector, landed one row early)
-  int n2a = 0, n2b = 0;           // Arp of row + 2 NG (in flight)
-  int njj = 0;                    // A columns of row + NG
-  float nav = 0.f;
-  uint4 nwa = make_uint4(0, 0, 0, 0);
-  uint32_t nwb = 0;
-  int64_t nuo = 0;
-
-  auto ld_arp = [&](int r, int& a, int& b) {
-    if (r < m) {
-      a = (int)p.Arp[r + vz];
-      b = (int)p.Arp[r + 1 + vz];
-    }
-  };
-  auto ld_entries = [&](int r, int a, int b) {   // A entries of row r into njj / nav
-    if (r < m) {
-      const int a0 = __builtin_amdgcn_readfirstlane(a), na = __builtin_amdgcn_readfirstlane(b) - a0;
-      if (tid < na) {
-        njj = p.Aci[a0 + tid];
-        nav = p.Av[a0 + tid];
-      }
-    }
-  };
-  auto ld_bounds = [&](int r, int a, int b) {    // packed bounds + offsets of row r
-    if (r < m) {
-      const int na = __builtin_amdgcn_readfirstlane(b) - __builtin_amdgcn_readfirstlane(a);
-      if (tid < na) {
-        nwa = ra.ws8[2 * (int64_t)njj];
-        const uint4 x = ra.ws8[2 * (int64_t)njj + 1];
-        nwb = x.x;
-        if (ra.pad) nwa.x = x.y;   // the segment starts in the padded pair array
-      }
-      if (lane <= nwin) nuo = p.uoff[r * nwin + lane];
-    }
-  };
-  auto take_next = [&]() {   // next row -> current row (call only when its loads have landed)
-    ca0 = __builtin_amdgcn_readfirstlane(n1a);
-    cna = __builtin_amdgcn_readfirstlane(n1b) - ca0;
-    cav = nav;
-    cwa = nwa;
-    cwb = nwb;
-    cuo = nuo;
-    n1a = n2a;
-    n1b = n2b;
-  };
-  // prologue: row in the current registers, Arp of row1 loaded
-  ld_arp(row, n1a, n1b);
-  ld_entries(row, n1a, n1b);
-  ld_bounds(row, n1a, n1b);
-  ld_arp(row1, n2a, n2b);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  take_next();
-  __syncthreads();
-
-  int c[RR];
-  float v[RR];
-  while (row < m) {
-    const int na = cna;
-    row1 = row + NG;
-    row2 = row + 2 * NG;
-    uint32_t bq = cwa.x;   // first B index of window q of this thread's entry
-    for (int q = 0; q < nwin; ++q) {
-      const bool last = q == nwin - 1;
-      // ---- row pipeline hooks ------------------------------------------
-      if (q == 0) {
-        ld_entries(row1, n1a, n1b);
-        ld_arp(row2, n2a, n2b);
-      }
-      if (last) ld_bounds(row1, n1a, n1b);
-      // ---- staging from registers ---------------------------------------
-      const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
-      int len = 0, nch = 0;
-      if (tid < na && tid < NT) {
-        len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
-        nch = (len + Gc - 1) >> lgc;
-      }
-      const uint32_t b0 = bq;
-      bq += ra.pad ? (uint32_t)(((len + (1 << kPadLg) - 1) >> kPadLg) << kPadLg) : (uint32_t)len;
-      const int clo = q << LGW;
-      const int u = (int)(row * nwin + q);
-      // (both halves zero-extended: offsets pass 2^31 on the 1M product)
-      const int64_t off =
-          (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)cuo >> 32), q) << 32) |
-                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cuo, q));
-      const int want = __builtin_amdgcn_readlane((int)(uint32_t)cuo, q + 1) - (int)(uint32_t)off;
-      int pre, plen, TC, P;
-      bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-      const bool too_big = na > NT || P > PCAP || TC > CCAP || TC > RL * ngrp;
-      if (P == 0 || too_big) {   // uniform
-        if (too_big && P != 0 && tid == 0) {
-          const uint32_t at = atomicAdd(p.novf, 1u);
-          if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
-          else atomicOr(p.err, 4);
-        }
-        if (last) take_next();   // (rare: waits for the next row's loads here)
-        __syncthreads();         // wsum reads done before the next scan
-        continue;
-      }
-      for (int kk = 0; kk < nch; ++kk) {
-        const int rem = len - (kk << lgc);
-        desc[pre + kk] = make_uint2(b0 + ((uint32_t)kk << lgc), (uint32_t)(rem < Gc ? rem : Gc));
-        dval[pre + kk] = cav;
-      }
-      __syncthreads();
-      BM_STAMP(0);
-      // ---- pass 1 ----------------------------------------------------------
-      const int nr = (TC + ngrp - 1) / ngrp;
-      {
-        uint2 ds[RL];
-#pragma unroll
-        for (int d = 0; d < RL; ++d) {
-          const int t = gid + d * ngrp;
-          ds[d] = desc[t < TC ? t : TC - 1];
-        }
-        uint32_t f[RL];
-        uint32_t okm = 0;   // bit s: product slot s (round s / PPL, pair s % PPL) is in its segment
-#pragma unroll
-        for (int d = 0; d < RL; ++d) {
-          const int t = gid + d * ngrp;
-          const int nv = (int)ds[d].y - PPL * gl;
-          const bool ok = (t < TC) & (nv > 0);
-          okm |= (ok ? 1u : 0u) << (d * PPL);
-          if constexpr (WIDE) okm |= ((ok & (nv > 1)) ? 1u : 0u) << (d * PPL + 1);
-          f[d] = ds[d].x + (ok ? (uint32_t)(PPL * gl) : 0u);
-        }
-        int x[RR];
-        float b[RR];
-#pragma unroll
-        for (int d = 0; d < RL; ++d) {
-#pragma unroll
-          for (int h = 0; h < PPL; ++h) {
-            x[d * PPL + h] = 0;
-            b[d * PPL + h] = 0.f;
-          }
-          if (d < nr) {   // wave-uniform
-            if constexpr (WIDE) {   // one 16-byte load: two pairs (chunks start on 128-byte lines)
-              const uint4 e = *reinterpret_cast<const uint4*>(p.Bcv + f[d]);
-              x[2 * d] = (int)e.x;
-              b[2 * d] = __uint_as_float(e.y);
-              x[2 * d + 1] = (int)e.z;
-              b[2 * d + 1] = __uint_as_float(e.w);
-            } else if constexpr (CV) {   // one 8-byte load: a chunk's products share cache lines
-              const uint2 e = p.Bcv[f[d]];
-              x[d] = (int)e.x;
-              b[d] = __uint_as_float(e.y);
-            } else {
-              x[d] = p.Bci[f[d]];
-              b[d] = p.Bv[f[d]];
-            }
-          }
-        }
-        // A values while the B loads are in flight
-#pragma unroll
-        for (int d = 0; d < RL; ++d) {
-          const int t = gid + d * ngrp;
-          const float a = dval[t < TC ? t : TC - 1];
-#pragma unroll
-          for (int h = 0; h < PPL; ++h) v[d * PPL + h] = a;
-        }
-#pragma unroll
-        for (int d = 0; d < RR; ++d) {
-          c[d] = ((okm >> d) & 1u) ? x[d] - clo : -1;
-          v[d] *= b[d];
-        }
-      }
-      uint32_t dupm = 0;
-      {
-        uint32_t old[RR];
-#pragma unroll
-        for (int d = 0; d < RR; ++d) {
-          old[d] = 0u;
-          if (c[d] >= 0) old[d] = atomicOr(bm32 + (c[d] >> 5), 1u << (c[d] & 31));
-        }
-#pragma unroll
-        for (int d = 0; d < RR; ++d) dupm |= (c[d] >= 0 ? (old[d] >> (c[d] & 31)) & 1u : 0u) << d;
-      }
-      // this unit's B loads have landed, and with them every older load:
-      // the next row's registers are ready to be taken
-      if (last) take_next();
-      if (dupm) sdup = 1;
-      __syncthreads();
-      BM_STAMP(1);
-      // ---- rank prefix per 64-bit word ---------------------------------
-      // (groups: a lane takes SG adjacent words per step -- 16-byte reads, ONE
-      // wave scan of their sum, 16-bit prefixes stored SG at a time)
-      constexpr int SG = (kSweepG > 1 && WPW % (64 * kSweepG) == 0) ? kSweepG : 1;
-      constexpr bool PAIRS = SG > 1;
-      int run[WPT];   // groups: [SG * kk] = group prefix inside the wave, [SG * kk + i] = local prefix of word i
-      int wtot = 0;
-      if constexpr (PAIRS) {
-#pragma unroll
-        for (int kk = 0; kk < WPT / SG; ++kk) {
-          const ulonglong2* src = reinterpret_cast<const ulonglong2*>(&bm[w * WPW + kk * 64 * SG + SG * lane]);
-          int c[SG];
-#pragma unroll
-          for (int h = 0; h < SG / 2; ++h) {
-            const ulonglong2 x = src[h];
-            c[2 * h] = __popcll(x.x);
-            c[2 * h + 1] = __popcll(x.y);
-          }
-          int sum = 0;
-#pragma unroll
-          for (int i = 0; i < SG; ++i) {
-            if (i > 0) run[SG * kk + i] = sum;
-            sum += c[i];
-          }
-          const int incl = bm_wave_incl(sum);
-          run[SG * kk] = wtot + incl - sum;
-          wtot += __builtin_amdgcn_readlane(incl, 63);
-        }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < WPT; ++kk) {
-          const int cnt = __popcll(bm[w * WPW + kk * 64 + lane]);
-          const int incl = bm_wave_incl(cnt);
-          run[kk] = wtot + incl - cnt;
-          wtot += __builtin_amdgcn_readlane(incl, 63);
-        }
-      }
-      const int any_dup = sdup;
-      if (lane == 0) wsum[w] = wtot;
-      __syncthreads();
-      int base = 0, total = 0;
-#pragma unroll
-      for (int i = 0; i < NW; ++i) {
-        const int sw = wsum[i];
-        base += (i < w) ? sw : 0;
-        total += sw;
-      }
-      if constexpr (PAIRS) {
-#pragma unroll
-        for (int kk = 0; kk < WPT / SG; ++kk) {
-          const uint32_t g0 = (uint32_t)(base + run[SG * kk]);
-          uint32_t pk[SG / 2];
-#pragma unroll
-          for (int h = 0; h < SG / 2; ++h) {
-            const uint32_t lo = g0 + (h > 0 ? (uint32_t)run[SG * kk + 2 * h] : 0u);
-            const uint32_t hi = g0 + (uint32_t)run[SG * kk + 2 * h + 1];
-            pk[h] = (lo & 0xffffu) | (hi << 16);
-          }
-          uint16_t* dst = &pre16[w * WPW + kk * 64 * SG + SG * lane];
-          if constexpr (SG == 2) {
-            *reinterpret_cast<uint32_t*>(dst) = pk[0];
-          } else if constexpr (SG == 4) {
-            *reinterpret_cast<uint2*>(dst) = make_uint2(pk[0], pk[1]);
-          } else {
-            static_assert(SG == 8, "sweep group of 2, 4 or 8 words");
-            *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < WPT; ++kk) pre16[w * WPW + kk * 64 + lane] = (uint16_t)(base + run[kk]);
-      }
-      if (tid == 0) sdup = 0;
-      __syncthreads();
-      BM_STAMP(2);
-      // ---- pass 2 --------------------------------------------------------
-      auto rank = [&](int cc) {
-        const int wd = cc >> 6;
-        return (int)pre16[wd] + __popcll(bm[wd] & ((1ull << (cc & 63)) - 1ull));
-      };
-#pragma unroll
-      for (int d0 = 0; d0 < RR; d0 += 4) {
-        if (d0 >= nr * PPL) break;   // uniform: slots past the unit's chunks hold no product
-        int r[4];
-#pragma unroll
-        for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) r[dd] = rank(c[d0 + dd] >= 0 ? c[d0 + dd] : 0);
-#pragma unroll
-        for (int dd = 0; dd < 4 && d0 + dd < RR; ++dd) {
-          const int d = d0 + dd;
-          if (c[d] >= 0 && !((dupm >> d) & 1u))
-            items[r[dd]] = ((unsigned long long)__float_as_uint(v[d]) << 32) | (uint32_t)(c[d] + clo);
-        }
-      }
-      if (any_dup) {   // uniform
-        __syncthreads();
-        if constexpr (DET) {   // duplicates mark their slot; a second duplicate flags the unit
-          bool tri = false;
-#pragma unroll
-          for (int d = 0; d < RR; ++d)
-            if ((dupm >> d) & 1u) {
-              unsigned long long* it = &items[rank(c[d])];
-              tri |= (atomicOr(reinterpret_cast<uint32_t*>(it), kDupBit) & kDupBit) != 0u;
-              atomicAdd(reinterpret_cast<float*>(it) + 1, v[d]);
-            }
-          if (tri) sfix = 1;
-        } else {
-#pragma unroll
-          for (int d = 0; d < RR; ++d)
-            if ((dupm >> d) & 1u) atomicAdd(reinterpret_cast<float*>(&items[rank(c[d])]) + 1, v[d]);
-        }
-      }
-      __syncthreads();
-      bool skip = false;
-      if constexpr (DET) {
-        if (sfix) {   // uniform, rare: re-sum the slots of >= 3 products in Gustavson order
-#pragma unroll
-          for (int d = 0; d < RR; ++d) {
-            if (c[d] >= 0) {
-              const int rr = rank(c[d]);
-              if (reinterpret_cast<const uint32_t*>(&items[rr])[0] & kDupBit) {
-                const int at = atomicAdd(&snl, 1);
-                const uint32_t key = ((uint32_t)(gid + d * ngrp) << lg) | (uint32_t)gl;
-                if (at < LCAP) dlist[at] = make_uint2(((uint32_t)rr << kKeyBits) | key, __float_as_uint(v[d]));
-              }
-            }
-          }
-          __syncthreads();
-          const int nl = snl;
-          if (nl <= LCAP && w == 0) bm_det_sum(dlist, nl, items, lane);
-          skip = nl > LCAP;   // too many: the reload kernel redoes the unit
-          if (skip && tid == 0) {
-            const uint32_t at = atomicAdd(p.novf, 1u);
-            if ((int64_t)at < p.ovf_cap) p.ovf[at] = u;
-            else atomicOr(p.err, 4);
-          }
-          __syncthreads();
-          if (tid == 0) {
-            sfix = 0;
-            snl = 0;
-          }
-        }
-      }
-      BM_STAMP(3);
-      // ---- write-out -----------------------------------------------------
-      
-      int lim = skip ? 0 : total;
-      if (!skip && (want != total || off < 0 || off + total > p.cap)) {   // never write outside the unit or C
-        if (tid == 0) atomicOr(p.err, 2);
-        lim = (off < 0 || off + total > p.cap) ? 0 : (total < want ? total : want);
-      }
-      bm_write_unit<NT>(items, lim, p.Cci, p.Cv, off, DET ? kColMask : 0xFFFFFFFFu);
-      clear_bm();
-      __syncthreads();
-      BM_STAMP(4);
-      BM_STAMP_UNIT();
-    }
-    row += NG;
-  
-  }
-  BM_STAMP_FLUSH();
-}
-
 // ---- pipelined row-major numeric kernel (padded pairs, unordered sum) -------
-// The same unit work as spgemm_bm_rows<..., WIDE> in a software pipeline that
-// hides the B gathers: unit k+1 is staged (scan, descriptors) and its B loads
+// The per-unit kernel's work on whole rows (two padded pairs per 16-byte
+// lane load) in a software pipeline that hides the B gathers: unit k+1 is staged (scan, descriptors) and its B loads
 // are issued right after unit k's pass 2, BEFORE unit k's write-out, so the
 // gathers travel while unit k's slots are copied to C.  Unit k+1's pass 1
 // then finds its products landed (the flat kernel waited a full memory
@@ -1689,7 +1278,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
           row_block(next_row());
         }
         BM_STAMP(1);
-        // ---- rank prefix per 64-bit word (as spgemm_bm_rows) ------------
+        // ---- rank prefix per 64-bit word ---------------------------------
         int run[WPT];
         int wtot = 0;
         if constexpr (PAIRS) {
@@ -1825,243 +1414,9 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   BM_WG_FLUSH();
 }
 
-// ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
-// The count kernel of the same row pipeline: one window's bitmap (16 KB at
-// W = 2^17) per workgroup, so eight 256-thread workgroups share a CU and
-// hide each other's B-load latency (the 8-window, 128 KB-bitmap count kernel
-// runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
-// wave's own bitmap rows, clear of the same rows, one barrier.
-template <int LGW, int NSUB, int NT, int RR, int CCAP, bool PADC>
-#ifndef SPMM_BM_COUNT_WPS   // row count kernel: waves per SIMD its registers are sized for (8: <= 64 VGPRs)
-#define SPMM_BM_COUNT_WPS 8   // (64k: 8 = 1.547-1.551 ms with 2 spills, 7 = 1.547-1.565, 6 = 1.641)
-#endif
-__global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(BmRowArgs ra) {
-  const BmArgs& p = ra.a;
-  constexpr int NW = NT / 64;
-  constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
-  constexpr int WORDS_PER_WIN = NWORD / NSUB;
-  static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
-  // log2 columns per lane and load: padded columns are read 4 at a time
-  // (16-byte loads: the gathers are bound by their load-instruction count,
-  // 1M count 16.5 -> 15.3 ms vs 8-byte loads, PERF_LOG round 4), the host's
-  // lane groups halved to keep a chunk at one 128-byte line
-  constexpr bool WIDE = PADC;
-  constexpr int SH = PADC ? 2 : 0;
-  constexpr int CPL = 1 << SH;
-
-  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
-  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
-  __shared__ int wsum[2 * NW];
-  __shared__ int csum[NW];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lg = p.lg - (WIDE ? 1 : 0);
-  const int Gl = 1 << lg;
-  const int ngrp = NW << (6 - lg);
-  const int gid = (w << (6 - lg)) + (lane >> lg);
-  const int gl = lane & (Gl - 1);
-  const int nwin = p.nwin;
-  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
-  int vz;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-  if (*p.err & 8) return;   // ws8 lengths truncated: the host re-counts with spgemm_bm (uniform exit)
-
-  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
-
-  // 32-bit row / unit indices: the host takes this path only for m * nwin < 2^31
-  const int NG = (int)gridDim.x;
-  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
-  const int m = (int)p.m;
-  int row = me;
-  int cna = 0;
-  uint4 cwa = make_uint4(0, 0, 0, 0);
-  uint32_t cwb = 0;
-  int n1a = 0, n1b = 0, n2a = 0, n2b = 0, njj = 0;
-  uint4 nwa = make_uint4(0, 0, 0, 0);
-  uint32_t nwb = 0;
-  auto ld_arp = [&](int r, int& a, int& b) {
-    if (r < m) {
-      a = (int)p.Arp[r + vz];
-      b = (int)p.Arp[r + 1 + vz];
-    }
-  };
-  auto ld_entries = [&](int r) {
-    if (r < m) {
-      const int a0 = __builtin_amdgcn_readfirstlane(n1a), na = __builtin_amdgcn_readfirstlane(n1b) - a0;
-      if (tid < na) njj = p.Aci[a0 + tid];
-    }
-  };
-  auto ld_bounds = [&](int r) {
-    if (r < m) {
-      const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
-      if (tid < na) {
-        nwa = ra.ws8[2 * (int64_t)njj];
-        const uint4 x = ra.ws8[2 * (int64_t)njj + 1];
-        nwb = x.x;
-        if constexpr (PADC) nwa.x = x.z;   // the row's first column in the padded column array
-      }
-    }
-  };
-  auto take_next = [&]() {
-    cna = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
-    cwa = nwa;
-    cwb = nwb;
-    n1a = n2a;
-    n1b = n2b;
-  };
-  ld_arp(row, n1a, n1b);
-  ld_entries(row);
-  ld_bounds(row);
-  ld_arp(row + NG, n2a, n2b);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  take_next();
-  __syncthreads();
-
-  for (; row < m; row += NG) {
-    const int na = cna;
-    uint32_t bq = cwa.x;
-    for (int q = 0; q < nwin; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
-      const bool last = q + NSUB >= nwin;
-      if (q == 0) {
-        ld_entries(row + NG);
-        ld_arp(row + 2 * NG, n2a, n2b);
-      }
-      if (last) ld_bounds(row + NG);
-      const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
-      int len = 0, nch = 0;
-      if (tid < na && tid < NT) {
-        if constexpr (NSUB == 1) {
-          len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
-        } else if constexpr (NSUB == 2) {   // q even: windows q and q + 1 share one 32-bit word of lengths
-          len = (int)(wl & 0xffffu) + (int)(wl >> 16);   // (lengths past nwin are packed as 0)
-        } else {   // q a multiple of NSUB: the unit's lengths are whole 32-bit words of ws8
-          static_assert(NSUB == 4 || NSUB == 8, "count units of 1, 2, 4 or 8 windows");
-          const uint32_t wq[4] = {cwa.y, cwa.z, cwa.w, cwb};
-#pragma unroll
-          for (int k = 0; k < NSUB / 2; ++k) {
-            const uint32_t x = wq[(q >> 1) + k < 4 ? (q >> 1) + k : 3];
-            len += (int)(x & 0xffffu) + (int)(x >> 16);
-          }
-        }
-        nch = (len + (Gl << SH) - 1) >> (lg + SH);
-      }
-      const uint32_t b0 = bq;
-      bq += PADC ? (uint32_t)(((len + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg) : (uint32_t)len;
-      const int clo = q << LGW;
-      const int u = row * nwin + q;
-      int pre, plen, TC, P;
-      bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
-      for (int cb = 0; cb < TC; cb += CCAP) {
-        const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
-        const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
-        for (int kk = k0; kk < k1; ++kk) {
-          const int rem = len - (kk << (lg + SH));
-          desc[pre + kk - cb] =
-              make_uint2(b0 + ((uint32_t)kk << (lg + SH)), (uint32_t)(rem < (Gl << SH) ? rem : (Gl << SH)));
-        }
-        __syncthreads();
-        const int nr = (TCb + ngrp - 1) / ngrp;
-        for (int i0 = 0; i0 < nr; i0 += RR) {
-          uint2 ds[RR];
-#pragma unroll
-          for (int d = 0; d < RR; ++d) {
-            const int t = gid + (i0 + d) * ngrp;
-            ds[d] = desc[t < TCb ? t : TCb - 1];
-          }
-          if constexpr (PADC) {
-            // four columns per lane: one 16-byte load (aligned: chunks start on
-            // 32-column boundaries of the padded array); the later columns
-            // may be past the segment (padding)
-            static_assert(RR * CPL <= 32, "one bit per loaded column");
-            uint32_t x[RR][CPL];
-            uint32_t okb = 0;   // bit d * CPL + i: column i of round d is in its segment
-#pragma unroll
-            for (int d = 0; d < RR; ++d) {
-              const int t = gid + (i0 + d) * ngrp;
-              const int nv = (int)ds[d].y - CPL * gl;
-              const bool ok = (t < TCb) & (nv > 0);
-              okb |= (ok ? ((nv >= CPL) ? (1u << CPL) - 1u : (1u << nv) - 1u) : 0u) << (d * CPL);
-#pragma unroll
-              for (int i = 0; i < CPL; ++i) x[d][i] = 0u;
-              if (i0 + d < nr) {   // wave-uniform guard
-                const uint4 v = *reinterpret_cast<const uint4*>(p.Bci + ds[d].x + (ok ? (uint32_t)(CPL * gl) : 0u));
-                x[d][0] = v.x; x[d][1] = v.y; x[d][2] = v.z; x[d][3] = v.w;
-              }
-            }
-#pragma unroll
-            for (int d = 0; d < RR; ++d) {
-#pragma unroll
-              for (int i = 0; i < CPL; ++i) {
-                if ((okb >> (d * CPL + i)) & 1u) {
-                  const int cc = (int)x[d][i] - clo;
-                  atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
-                }
-              }
-            }
-          } else {
-            int x[RR];
-            uint32_t okm = 0;
-#pragma unroll
-            for (int d = 0; d < RR; ++d) {
-              const int t = gid + (i0 + d) * ngrp;
-              const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
-              okm |= (ok ? 1u : 0u) << d;
-              x[d] = 0;
-              if (i0 + d < nr) x[d] = p.Bci[ds[d].x + (ok ? (uint32_t)gl : 0u)];   // wave-uniform guard
-            }
-#pragma unroll
-            for (int d = 0; d < RR; ++d) {
-              if ((okm >> d) & 1u) {
-                const int cc = x[d] - clo;
-                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
-              }
-            }
-          }
-        }
-        __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
-      }
-      if (last) take_next();   // after this unit's B loads: every older load has landed
-      if (P == 0) {   // uniform: nothing was ORed
-        if constexpr (NSUB == 1) {
-          if (tid == 0) p.ucnt[u] = 0;
-        } else if (tid < NSUB && q + tid < nwin) {
-          p.ucnt[u + tid] = 0;
-        }
-        __syncthreads();   // wsum reads done before the next scan
-        continue;
-      }
-      // popcount of this wave's bitmap rows, clearing them as they are read
-      int cnt = 0;
-#pragma unroll
-      for (int kk = 0; kk < WPT; ++kk) {
-        const int wd = w * WPW + kk * 64 + lane;
-        cnt += __popcll(bm[wd]);
-        bm[wd] = 0ull;
-      }
-      cnt = bm_wave_sum(cnt);
-      if (lane == 0) csum[w] = cnt;
-      __syncthreads();
-      if constexpr (NSUB == 1) {
-        if (tid == 0) {
-          int t = 0;
-#pragma unroll
-          for (int i = 0; i < NW; ++i) t += csum[i];
-          p.ucnt[u] = t;
-        }
-      } else if (tid < NSUB && q + tid < nwin) {   // window tid of the unit: the waves whose blocks lie in it
-        constexpr int WAVES_PER_WIN = WORDS_PER_WIN / WPW;
-        int t = 0;
-#pragma unroll
-        for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[tid * WAVES_PER_WIN + i];
-        p.ucnt[u + tid] = t;
-      }
-    }
-  }
-}
-
 // ---- pipelined row-major count kernel (two-window units, padded columns) ---
-// spgemm_bm_rows_count<..., NSUB = 2, PADC> in the pipelined form of
+// Two-window count units (a B row's two-window column segment read once for
+// both) over the padded count columns, in the pipelined form of
 // spgemm_bm_rows_pipe: unit k+1's scan rides unit k's OR phase (its
 // per-wave sums are written before that phase's barrier), its descriptors
 // are written after it and its B loads issued BEFORE unit k's popcount and
@@ -2427,11 +1782,6 @@ struct BmRowKernel {
   static constexpr int NT = K.rows_nt;
   // register rounds (the row pipeline's registers cost rounds)
   static constexpr int R = K.rounds_fast > K.rows_r ? K.rows_r : K.rounds_fast;
-  static constexpr auto k = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, false>;
-  static constexpr auto kcv = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false>;
-  static constexpr auto kcvw = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, false, R % 2 == 0>;
-  static constexpr auto k_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), false, true>;
-  static constexpr auto kcv_det = spgemm_bm_rows<K.lgw, NT, K.pcap_fast, R, R * (NT / 16), true, true>;
   static constexpr int RP = R & ~1;   // the pipelined kernel loads two pairs per lane and round
   static constexpr auto kpipe = spgemm_bm_rows_pipe<K.lgw, NT, K.pcap_fast, RP, RP * (NT / 16)>;
 };
@@ -2454,24 +1804,9 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastN
   return launch_rows(kernel, ra, ra.a.m, s, nt);
 }
 
-// count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
-// per unit (32 KB, 4 per CU: a B row's column segment read once for both)
 #ifndef SPMM_BM_COUNT_RR   // B loads in flight per thread (diagnostic builds: tools/bm_variants.py)
 #define SPMM_BM_COUNT_RR 8
 #endif
-#ifndef SPMM_BM_COUNT_NT   // threads per count workgroup (the host gates A rows <= this)
-#define SPMM_BM_COUNT_NT 256
-#endif
-// workgroup size by bitmap bytes: 32 KB -> 256 threads (4 per CU), 64 KB -> 512 (2 per CU)
-constexpr int count_nt(int lgw, int nsub) {
-  return ((nsub << lgw) / 8) > (64 << 10) ? 1024 : ((nsub << lgw) / 8) > (32 << 10) ? 512 : SPMM_BM_COUNT_NT;
-}
-template <int C, int NSUB>
-struct BmRowCountKernel {
-  static constexpr int NT = count_nt(kCfgs[C].lgw, NSUB);
-  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, false>;
-  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR / 2, 256, true>;
-};
 // pipelined (two-window units, padded columns; 32 KB bitmap + 6 KB descriptors: 4 workgroups per CU)
 template <int C>
 struct BmRowCountPipe {
@@ -2479,38 +1814,30 @@ struct BmRowCountPipe {
   static constexpr auto k = spgemm_bm_rows_count_pipe<kCfgs[C].lgw, NT, SPMM_BM_COUNT_RR / 2, 768>;
 };
 
+// The pipelined row count kernel; its conditions (kRowCountOk) are the
+// planner's (csr_bitmap_plan.hip: count_rows), every other product counts on
+// the per-unit kernel.
 template <int C>
 int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s) {
-  using K1 = BmRowCountKernel<C, 1>;
-  using K2 = BmRowCountKernel<C, 2>;
   const int64_t colp_bytes = ra.a.cap * 4;
-  // (pipelined from two units per row up: with one, every unit is a row's last and the
-  // pipeline only adds work -- 65536^2 count 1.32 -> 1.36 ms step, PERF_LOG round 5)
-  if (ra.pad && pipe && nsub == 2 && ra.a.nwin >= 3 && K2::NT == BmRowCountPipe<C>::NT && annz > 0 &&
-      colp_bytes < (int64_t(1) << 32) && ra.a.m * ra.a.nwin < (int64_t(1) << 30))
-    return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz, ra.a.err + 3}, ra.a.m, s,
-                       BmRowCountPipe<C>::NT);
-  if (ra.pad)
-    return nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT);
-  return nsub == 2 ? launch_rows(K2::k, ra, s, K2::NT) : launch_rows(K1::k, ra, s, K1::NT);
+  if (!(ra.pad && pipe && nsub == 2 && ra.a.nwin >= 3 && annz > 0 && colp_bytes < (int64_t(1) << 32) &&
+        ra.a.m * ra.a.nwin < (int64_t(1) << 30)))
+    return (int)hipErrorInvalidValue;
+  return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz, ra.a.err + 3}, ra.a.m, s,
+                     BmRowCountPipe<C>::NT);
 }
 
-// det: the deterministic kernels (fixed summation order)
+// The pipelined row numeric kernel (2 pairs per lane and 16-byte loads on the
+// padded pairs, 32-bit buffer offsets), then the reload kernel over the
+// deferred units; same conditions as the planner's `rows`.
 template <int C>
 int bm_numeric_rows(BmRowArgs ra, int det, int64_t nbcv, int pipe, int64_t annz, hipStream_t s) {
   using K = BmRowKernel<C>;
-  // 2 pairs per lane and 16-byte loads on the padded pairs (1M numeric 52.8 ->
-  // 50.6 ms vs one 8-byte pair per lane, PERF_LOG round 4); pipelined when
-  // the padded pairs fit 32-bit buffer offsets
-  const bool wide = ra.a.Bcv && ra.pad && ra.a.lg >= 1;
-  const bool piped = wide && !det && pipe && annz > 0 && nbcv > 0 && nbcv * 8 < (int64_t(1) << 32);
-  const int rc = piped ? launch_rows(K::kpipe, BmPipeArgs{ra, (uint32_t)(nbcv * 8), annz, ra.a.err + 2}, ra.a.m, s, K::NT)
-               : det ? (ra.a.Bcv ? launch_rows(K::kcv_det, ra, s, K::NT) : launch_rows(K::k_det, ra, s, K::NT))
-                     : (wide ? launch_rows(K::kcvw, ra, s, K::NT)
-                             : (ra.a.Bcv ? launch_rows(K::kcv, ra, s, K::NT) : launch_rows(K::k, ra, s, K::NT)));
+  if (!(ra.a.Bcv && ra.pad && ra.a.lg >= 1 && !det && pipe && annz > 0 && nbcv > 0 && nbcv * 8 < (int64_t(1) << 32)))
+    return (int)hipErrorInvalidValue;
+  const int rc = launch_rows(K::kpipe, BmPipeArgs{ra, (uint32_t)(nbcv * 8), annz, ra.a.err + 2}, ra.a.m, s, K::NT);
   if (rc) return rc;
-  return det ? launch_bm(BmKernels<C>::reload_det, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s)
-             : launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
+  return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
 }
 
 template <int C>

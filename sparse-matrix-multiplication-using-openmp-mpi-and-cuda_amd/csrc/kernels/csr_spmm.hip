@@ -584,6 +584,145 @@ __global__ __launch_bounds__(NT, 4) void spmm_sweep(const int64_t* __restrict__ 
   }
 }
 
+// ---- row-group MFMA: the sweep's gather scheme, products on the matrix cores ----
+// A wave owns 16 consecutive rows; their entries are contiguous in A, taken in
+// chunks of RM_K = 32 (rows mixed inside a chunk).  Chunk c is one
+// v_mfma_f32_16x16x32_bf16 per 16-column output tile: K = the chunk's
+// entries, A operand [row][k] = the entry's value when entry k is in that row
+// (else 0: 1/16 useful, the matrix cores are ~30x faster than the gathers),
+// B operand [k][col] = the entry's gathered X row.  Lane (kg = lane / 16,
+// p = lane % 16) gathers 16 bytes (columns 8p .. 8p + 7) of entries 4i + kg,
+// i < 8, like the sweep (one load instruction: four X rows); the rows go
+// through an 8 KB per-wave LDS image (the swizzle of spmm_panel_mfma) and
+// come back transposed (ds_read_b64_tr_b16) as the B operand.  Software
+// pipeline, no workgroup barriers (every LDS byte is wave-private):
+//   iteration c: issue chunk c+2's column / value loads (one entry a lane),
+//   chunk c+1's gathers (columns landed one iteration ago, spread by
+//   ds_bpermute), build chunk c's A operand, then consume chunk c's gathers
+//   (issued one iteration ago) -> LDS -> 8 MFMAs.
+// D = 128, X 16-byte aligned (as spmm_sweep); fp32 accumulation.
+constexpr int RM_K = 32;
+
+template <bool OUT_BF16>
+// (ci / av / X without __restrict__: restrict read-only loads are free to sink
+// below the asm barriers that keep the software pipeline's order)
+__global__ __launch_bounds__(NT, 2) void spmm_rows_mfma(const int64_t* __restrict__ rp, const int32_t* ci,
+                                                        const unsigned short* av,
+                                                        const unsigned short* X, int64_t ldx, int64_t m,
+                                                        void* __restrict__ Yv, int64_t ldy) {
+  __shared__ __attribute__((aligned(16))) unsigned char xs_all[NT / 64][RM_K * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = ((int64_t)blockIdx.x * (NT / 64) + w) * 16;
+  if (r0 >= m) return;   // (whole wave; nothing below synchronises waves)
+  unsigned char* const Xs = xs_all[w];
+  const int mr = lane & 15, kg = lane >> 4, p = lane & 15;
+  const int64_t lo = rp[min(r0 + mr, m)], hi = rp[min(r0 + mr + 1, m)];   // lane's A-operand row (empty past m)
+  const int64_t e0 = __builtin_amdgcn_readfirstlane(rp[r0]);
+  const int64_t e1 = __builtin_amdgcn_readfirstlane(rp[min(r0 + 16, m)]);
+  v4f acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (e1 > e0) {
+    // one entry per lane (lanes 32..63 repeat 0..31): column and value of entry base + lane % 32
+    auto ld_ent = [&](int64_t base, int& c, unsigned& v) {
+      const int64_t e = base + (lane & 31);
+      const int64_t ec = e < e1 ? e : e1 - 1;   // (clamped: in bounds, masked below)
+      c = ci[ec];
+      const unsigned raw = av[ec];   // (unconditional: a load under a branch costs the loop its vmcnt counts)
+      v = e < e1 ? raw : 0u;
+    };
+    // chunk gathers: entry 4 i + kg of the chunk, 16 bytes at part p; past the
+    // entries: row 0 of X, zeroed when staged
+    auto gather = [&](int c, uint4 (&x)[8]) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int col = __shfl(c, 4 * i + kg, 64);
+        x[i] = *reinterpret_cast<const uint4*>(X + (int64_t)col * ldx + 8 * p);
+      }
+    };
+    // chunk `base`: its gathered X rows xc (landed) and its entries' values vc -> 8 MFMAs
+    auto consume = [&](int64_t base, const uint4 (&xc)[8], unsigned vc) {
+      // A operand: lane (row mr, k-group kg) holds k = 8 kg .. 8 kg + 7
+      uint32_t aw[4];
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const int64_t k0 = base + 8 * kg + j;
+        const unsigned v0 = (unsigned)__shfl((int)vc, 8 * kg + j, 64);
+        const unsigned v1 = (unsigned)__shfl((int)vc, 8 * kg + j + 1, 64);
+        const unsigned m0 = (k0 >= lo && k0 < hi) ? v0 : 0u;
+        const unsigned m1 = (k0 + 1 >= lo && k0 + 1 < hi) ? v1 : 0u;
+        aw[j / 2] = m0 | (m1 << 16);
+      }
+      const v8bf a = __builtin_bit_cast(v8bf, make_uint4(aw[0], aw[1], aw[2], aw[3]));
+      // the X rows -> the swizzled image (rows past the entries: zeros)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = 4 * i + kg;
+        const uint4 v = base + r < e1 ? xc[i] : make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(Xs + r * 256 + (((p >> 1) ^ xswz(r)) << 5) + (p & 1) * 16) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+      const int r0k = 8 * g + q, r1k = r0k + 4;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const unsigned char* p0 = Xs + r0k * 256 + ((t ^ xswz(r0k)) << 5) + pp * 8;
+        const unsigned char* p1 = Xs + r1k * 256 + ((t ^ xswz(r1k)) << 5) + pp * 8;
+        v4s blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p0));
+        v4s bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p1));
+        const v8s bs = __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(v8bf, bs), acc[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the image's reads before the next stores
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // Two chunks an iteration: their 16 gathers issue together, then the next
+    // iteration's entries, then the chunks are consumed in order.  No gather is
+    // in flight across the loop's back edge (hipcc copies loop-carried load
+    // registers and waits for them there); the other resident waves cover the
+    // start of each iteration's gathers, as in spmm_sweep's rounds.
+    int c0 = 0, c1 = 0;
+    unsigned v0 = 0, v1 = 0;
+    ld_ent(e0, c0, v0);
+    ld_ent(e0 + RM_K, c1, v1);
+#pragma unroll 1
+    for (int64_t base = e0; base < e1; base += 2 * RM_K) {
+      uint4 xA[8], xB[8];
+      gather(c0, xA);
+      gather(c1, xB);
+      int c0n, c1n;
+      unsigned v0n, v1n;
+      ld_ent(base + 2 * RM_K, c0n, v0n);
+      ld_ent(base + 3 * RM_K, c1n, v1n);
+      asm volatile("" ::: "memory");   // (every load above issues before the first chunk is consumed)
+      consume(base, xA, v0);
+      consume(base + RM_K, xB, v1);   // (past the entries: all-zero A)
+      c0 = c0n;
+      c1 = c1n;
+      v0 = v0n;
+      v1 = v1n;
+    }
+  }
+  // C/D map: col = lane & 15 of tile t, row = 4 (lane / 16) + i
+  const int64_t rb = r0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = rb + i;
+    if (row >= m) break;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int64_t col = 16 * t + (lane & 15);
+      if constexpr (OUT_BF16)
+        reinterpret_cast<unsigned short*>(Yv)[row * ldy + col] = f2bf(acc[t][i]);
+      else
+        reinterpret_cast<float*>(Yv)[row * ldy + col] = acc[t][i];
+    }
+  }
+}
+
 // ---- inspector: the panel plan on the device -------------------------------
 // (ops/spmm.py plan_panels; was a chain of torch sort / unique / bincount
 // launches, ~37 ms for the 65536^2 config.)  Per 64-row panel, one workgroup:
@@ -890,6 +1029,21 @@ SPMM_EXPORT int spmm_spmm_sweep(const int64_t* rp, const int32_t* ci, const void
   const int64_t g = waves / (NT / 64);
   hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(NT), 0, (hipStream_t)stream, rp, ci, (const unsigned short*)av,
                      (const unsigned short*)X, ldx, m, lgs, Y, ldy, err);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
+// Row-group MFMA SpMM (spmm_rows_mfma): D == 128, ldx a multiple of 8 and X
+// 16-byte aligned; no inspector.
+SPMM_EXPORT int spmm_spmm_rows_mfma(const int64_t* rp, const int32_t* ci, const void* av, const void* X, int64_t ldx,
+                                    int64_t m, int64_t D, void* Y, int64_t ldy, int out_bf16, void* stream) {
+  if (m <= 0) return 0;
+  if (D != 128 || ldx % 8 != 0 || ((uintptr_t)X & 15)) return (int)hipErrorInvalidValue;
+  const int64_t wg = (m + 16 * (NT / 64) - 1) / (16 * (NT / 64));
+  if (wg > (int64_t)UINT32_MAX) return (int)hipErrorInvalidValue;
+  auto k = out_bf16 ? spmm_rows_mfma<true> : spmm_rows_mfma<false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)wg), dim3(NT), 0, (hipStream_t)stream, rp, ci, (const unsigned short*)av,
+                     (const unsigned short*)X, ldx, m, Y, ldy);
   SPMM_LAUNCH_CHECK();
   return 0;
 }

@@ -114,6 +114,46 @@ class GatherStats:
 GATHER_STATS = GatherStats()
 
 
+def col_bits(n: int) -> int:
+    """Bits per column index of an n-column operand on the wire (32: sent raw)."""
+    b = max(1, (n - 1).bit_length())
+    return b if b < 30 else 32
+
+
+def packed_words(entries: int, bits: int) -> int:
+    """Words of one rank's column payload (packed: one spare word, the
+    unpacker reads two words an entry)."""
+    return entries if bits >= 32 else (entries * bits + 31) // 32 + 1
+
+
+def pack_cols(col: torch.Tensor, bits: int, out: torch.Tensor) -> None:
+    """This rank's columns -> its send buffer ``out`` (int32[packed_words]):
+    packed to ``bits`` bits each (csr_bitmap_layout.hip bm_pack_bits), or
+    copied and zero-padded when sent raw."""
+    from ..ops.spgemm import _native as _nat
+
+    n = col.numel()
+    if bits >= 32:
+        out[:n].copy_(col)
+        out[n:].zero_()
+        return
+    _nat.check(_nat.hip().spmm_pack_bits(_nat.ptr(col), n, bits, _nat.ptr(out), out.numel(),
+                                         _nat.stream_ptr(out.device)), "pack_bits")
+
+
+def unpack_gathered(gc, gv, W: int, gstride: int, cstride: int, bits: int, base: torch.Tensor, max_n: int,
+                    col: torch.Tensor, val=None, cv=None) -> None:
+    """[W, stride] gathered payloads -> contiguous columns / values
+    (csr_bitmap_layout.hip bm_unpack_gathered; see there)."""
+    from ..ops.spgemm import _native as _nat
+
+    P = _nat.ptr
+    _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(
+        P(gc) if gc is not None else None, P(gv) if gv is not None else None, W, gstride, cstride, bits, P(base),
+        max_n, P(col), P(val) if val is not None else None, P(cv) if cv is not None else None,
+        _nat.stream_ptr(col.device)), "spgemm_bm_unpack_gathered")
+
+
 def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], CSR]]:
     """Right operand of the row-block SpGEMM (every rank's B row panel), in
     stages so the gather overlaps the SpGEMM's setup.
@@ -161,15 +201,16 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
         return meta_B, OperandReady(lambda: CSR(m, panel.n, rowptr, empty_c, empty_v))
 
     if dev.type == "cuda" and panel.col.dtype == torch.int32 and panel.val.dtype == torch.float32:
-        from ..ops.spgemm import _native as _nat
-
-        cb = torch.zeros(emax, dtype=torch.int32, device=dev)
-        cb[:panel.nnz] = panel.col
+        # columns cross the links packed to ceil(log2 n) bits (1M columns: 20 of 32)
+        bits = col_bits(panel.n)
+        cw = packed_words(emax, bits)
+        cb = torch.empty(cw, dtype=torch.int32, device=dev)
+        pack_cols(panel.col, bits, cb)
         vb = torch.zeros(emax, dtype=torch.int32, device=dev)
         vb[:panel.nnz] = panel.val.view(torch.int32)
         rec = None
         if GATHER_STATS.enabled:   # bytes this rank receives: row counts + columns + values
-            rec = [W * (mmax * 8 + 2 * emax * 4), GATHER_STATS.mark(dev), None]
+            rec = [W * (mmax * 8 + (cw + emax) * 4), GATHER_STATS.mark(dev), None]
             GATHER_STATS.calls.append(rec)
         pay_c = comm.all_gather_async(cb)
         pay_v = comm.all_gather_async(vb)
@@ -177,16 +218,13 @@ def allgather_operand_async(panel: CSR, comm: Comm) -> Tuple[CSR, Callable[[], C
         got = {}
 
         def unpack(gc, gv, col, val, cv):
-            _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(
-                _nat.ptr(gc) if gc is not None else None, _nat.ptr(gv) if gv is not None else None, W,
-                emax, _nat.ptr(base), emax, _nat.ptr(col), _nat.ptr(val) if val is not None else None,
-                _nat.ptr(cv) if cv is not None else None, _nat.stream_ptr(dev)), "spgemm_bm_unpack_gathered")
+            unpack_gathered(gc, gv, W, emax, cw, bits, base, emax, col, val, cv)
 
         def cols() -> CSR:
             if "col" not in got:
                 g = pay_c()
-                if g.numel() != W * emax:
-                    raise RuntimeError(f"operand gather: {g.numel()} column words, expected {W * emax}")
+                if g.numel() != W * cw:
+                    raise RuntimeError(f"operand gather: {g.numel()} column words, expected {W * cw}")
                 col = torch.empty(nnz, dtype=torch.int32, device=dev)
                 unpack(g, None, col, None, None)
                 got["col"] = col
@@ -283,7 +321,8 @@ class RowblockGraph:
                packed bounds, padded count columns), count kernel, unit scan;
       graph 2: unpack the gathered values, padded pairs, numeric + reload.
 
-    ``run()`` = copy this rank's B panel (columns, value bits) into the send
+    ``run()`` = copy this rank's B panel (columns packed to ceil(log2 n) bits,
+    value bits) into the send
     buffers, start the two payload all-gathers (RCCL runs them in issue order
     on its own stream), make the compute stream wait for the columns and
     replay graph 1 -- the count kernel runs while the values cross xGMI --
@@ -332,14 +371,19 @@ class RowblockGraph:
         if not _agree(comm, plan is not None):
             raise ValueError("RowblockGraph: the product does not take the bitmap-rank path on every rank")
         self.plan, self.flops = plan, info.flops
-        self.cb = torch.zeros(emax, dtype=torch.int32, device=dev)
+        # send buffers: columns packed to ceil(log2 n) bits, value bits raw
+        self.bits = col_bits(B_panel.n)
+        self.cw = packed_words(emax, self.bits)
+        self.cb = torch.zeros(self.cw, dtype=torch.int32, device=dev)
         self.vb = torch.zeros(emax, dtype=torch.int32, device=dev)
-        self.gc = torch.empty(W * emax, dtype=torch.int32, device=dev)
+        self.gc = torch.empty(W * self.cw, dtype=torch.int32, device=dev)
         self.gv = torch.empty(W * emax, dtype=torch.int32, device=dev)
         self.base = torch.tensor([0] + list(itertools.accumulate(nnzs)), dtype=torch.int64, device=dev)
         self.bufs = SG.bitmap_buffers(plan, dev, cap=max(plan.raw.tot, 1))
         self.bufs["n"] = B_panel.n
-        self.gather_bytes = W * (2 * emax * 4)
+        self.gather_bytes = W * (self.cw + emax) * 4
+        if hasattr(comm, "bind_payloads"):   # (an emulated group: it builds the peers' payloads the same way)
+            comm.bind_payloads(self._col_payload, self._val_payload)
         # ---- one eager step (checks every launch and the kernels' error bits:
         # a product the row kernels cannot take, or with units beyond the reload
         # kernel, is not replayed), then the capture ---------------------------
@@ -367,15 +411,16 @@ class RowblockGraph:
         if not _agree(comm, err is None):
             raise ValueError(f"RowblockGraph: graph capture failed on a rank ({err})")
 
-    def _unpack(self, gc, gv) -> None:
-        from ..ops.spgemm import _native as _nat
+    def _col_payload(self, panel: CSR, out: torch.Tensor) -> None:
+        pack_cols(panel.col, self.bits, out)
 
-        W = self.comm.world
-        P = _nat.ptr
-        _nat.check(_nat.hip().spmm_spgemm_bm_unpack_gathered(
-            P(gc) if gc is not None else None, P(gv) if gv is not None else None, W, self.emax, P(self.base),
-            self.emax, P(self.B.col), P(self.B.val) if gv is not None else None, None, _nat.stream_ptr(self.A.device)),
-            "spgemm_bm_unpack_gathered")
+    def _val_payload(self, panel: CSR, out: torch.Tensor) -> None:
+        n = panel.nnz
+        out[:n].copy_(panel.val.view(torch.int32))
+
+    def _unpack(self, gc, gv) -> None:
+        unpack_gathered(gc, gv, self.comm.world, self.emax, self.cw, self.bits, self.base, self.emax, self.B.col,
+                        self.B.val if gv is not None else None)
 
     def _front(self) -> None:
         from ..ops import spgemm as SG
@@ -390,10 +435,8 @@ class RowblockGraph:
         SG.bitmap_back(self.A, self.B, self.plan, self.bufs, self.built)
 
     def _step(self, g1, g2) -> dict:
-        n = self.Bp.nnz
-        if n:
-            self.cb[:n].copy_(self.Bp.col)
-            self.vb[:n].copy_(self.Bp.val.view(torch.int32))
+        self._col_payload(self.Bp, self.cb)
+        self._val_payload(self.Bp, self.vb)
         rec = None
         if GATHER_STATS.enabled:
             rec = [self.gather_bytes, GATHER_STATS.mark(self.A.device), None]

@@ -86,9 +86,9 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     plan, inspector_ms, inspector_first_ms = None, None, None
     import time
 
-    if method not in ("auto", "mfma", "sweep", "rowwise"):
+    if method not in ("auto", "mfma", "panel", "sweep", "rowwise"):
         raise ValueError(f"unknown SpMM method {method!r}")
-    if comm.device.type == "cuda" and method in ("auto", "mfma"):
+    if comm.device.type == "cuda" and method in ("auto", "panel"):
         times = []
         for _ in range(2):   # first call: includes loading the kernels; second: the steady state
             torch.cuda.synchronize(comm.device)
@@ -100,7 +100,7 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
         inspector_first_ms = times[0]
     kernel_ms = {}
     if method == "auto":
-        method = "mfma" if plan is not None and cols % 128 == 0 and plan.reuse >= CONFIG.spmm_mfma_min_reuse else "rowwise"
+        method = "panel" if plan is not None and cols % 128 == 0 and plan.reuse >= CONFIG.spmm_mfma_min_reuse else "rowwise"
         if comm.device.type == "cuda":
             # executor choice at inspection time: time every kernel that can
             # take this operand (one local SpMM each, warm, 10 calls) and keep
@@ -110,8 +110,8 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
             # Timed on the real X (the step's all-gathered operand): an
             # all-zero X would flatter kernels whose cost depends on the data.
             Xfull = allgather_rows(Xp, comm, counts)
-            cands = (("mfma",) if plan is not None and cols % 128 == 0 else ()) + ("rowwise",) + (
-                ("sweep",) if cols == 128 and sweep_ok(A) else ())
+            cands = (("panel",) if plan is not None and cols % 128 == 0 else ()) + ("rowwise",) + (
+                ("sweep",) if cols == 128 and sweep_ok(A) else ()) + (("mfma",) if cols == 128 else ())
             for meth in cands:
                 spmm(A, Xfull, method=meth, plan=plan)
                 torch.cuda.synchronize(comm.device)
@@ -123,7 +123,7 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
             del Xfull
             # the slowest rank's view decides, so every rank runs the same kernel
             # (a kernel not available on some rank counts as infinitely slow there)
-            worst = {k: comm.allreduce_max(kernel_ms.get(k, float("inf"))) for k in ("mfma", "rowwise", "sweep")}
+            worst = {k: comm.allreduce_max(kernel_ms.get(k, float("inf"))) for k in ("mfma", "panel", "rowwise", "sweep")}
             method = min(worst, key=worst.get)
     step = lambda: rowblock_spmm(A, Xp, comm, counts, plan=plan, method=method)  # noqa: E731
     if not comm.is_dist and comm.device.type == "cuda":
@@ -134,7 +134,8 @@ def bench_setup(comm: Comm, n: int = 65536, density: float = 1e-3, cols: int = 1
     if comm.is_dist:
         nnz_a = sum(comm.gather_ints(nnz_a))
     flops = 2 * nnz_a * cols
-    kernel = {"mfma": "MFMA panel kernel (v_mfma_f32_16x16x32_bf16)", "sweep": "VALU row-owning sweep kernel",
+    kernel = {"mfma": "MFMA row-group kernel (v_mfma_f32_16x16x32_bf16)",
+              "panel": "MFMA panel kernel (v_mfma_f32_16x16x32_bf16)", "sweep": "VALU row-owning sweep kernel",
               "rowwise": "VALU row-gather kernel"}[method]
     extra = dict(nnz_A=nnz_a, spmm_method=method, spmm_kernel=kernel,
                  panel_reuse=(plan.reuse if plan is not None else None),

@@ -69,9 +69,9 @@ _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_v
 _native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
                      C_I64, C_I64, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_bm_interleave", c_vp, c_vp, C_I64, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, c_vp, C_I64, c_vp, c_vp, c_vp,
-                     c_vp)
+_native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, C_I64, C_INT, c_vp, C_I64, c_vp,
+                     c_vp, c_vp, c_vp)
+_native.register_hip("spmm_pack_bits", c_vp, C_I64, C_INT, c_vp, C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_count", C_INT, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_numeric", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp,
                      C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, c_vp, c_vp, c_vp)
@@ -329,6 +329,20 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
     nwg_h = np.maximum((na_h + epw - 1) // epw, 1)
     bad = torch.zeros(1, dtype=torch.int64, device=dev)   # rows whose counts disagree (device-side)
     nil = None
+    cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    sP = None
+    pending = []   # (event after its accumulation, buffers...) of batches not yet placed
+
+    def place_pending() -> None:
+        while pending:
+            ready, rt_off_p, dst_p, rt_nnz_p, scratch_p, nrt_p = pending.pop(0)
+            sP.wait_event(ready)
+            _native.check(lib.spmm_spgemm_long_place(P(rt_off_p), P(dst_p), P(rt_nnz_p), nrt_p, P(scratch_p),
+                                                     P(Cci), P(Cv), sP.cuda_stream), "long_place")
+            for t in (rt_off_p, dst_p, rt_nnz_p, scratch_p):
+                t.record_stream(sP)
+    if values and defer is None and cur is not None and stream == cur.cuda_stream and nrows > 0:
+        sP = _place_stream(dev)
     start, done = 0, 0
     while start < nrows:
         # batch = the longest run of rows from start whose products fit cap (at least one row)
@@ -397,6 +411,9 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         rt_cnt = T.reshape(-1)
         if LONG_STATS is not None:
             _long_stats(rt_cnt + D.reshape(-1) if direct else rt_cnt)
+        if pending:   # the previous batch's copy starts with this batch's accumulation
+            pending[-1] = (_mark_event(cur),) + pending[-1][1:]
+            place_pending()
         rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
         lists = torch.empty(2 * R * nch + 4, dtype=torch.int32, device=dev)   # the two kernels' item lists + counters
         _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
@@ -417,11 +434,23 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
             defer.append((rb, rt_off, rt_nnz, scratch))
         elif values:
             dst = (Crp[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
-            _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
-                                                     P(Cv), stream), "long_place")
+            if sP is not None:
+                # the copy into C waits for the NEXT batch's accumulation and runs beside it
+                # on the place stream (long_dense / long_rank are LDS-atomic bound, the copy
+                # HBM bound; beside the routing scatter, HBM bound too, it gained nothing);
+                # the batch's buffers stay allocated until that stream has read them
+                ready = torch.cuda.Event()
+                ready.record(cur)
+                pending.append((ready, rt_off, dst, rt_nnz, scratch, R * nch))
+            else:
+                _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
+                                                         P(Cv), stream), "long_place")
         del scratch
         done = int(csum_h[end - 1])
         start = end
+    if sP is not None:
+        place_pending()   # (the last batch: nothing left to run beside)
+        cur.wait_stream(sP)   # C's long rows are complete in stream order from here
     nbad = int(bad)
     if nbad:
         raise RuntimeError(f"spgemm long rows: routing histogram or numeric count disagrees with the product / "
@@ -712,8 +741,7 @@ class _BmOpts(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmOpts
 
 class _BmPlan(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmPlan
     _fields_ = ([(n, C.c_int32) for n in ("cfg", "lgw", "nwin", "nsub", "lg_count", "lg_c", "nsub_c", "lg_num",
-                                          "count_rows", "rows", "det", "pipe", "ws8", "pad_num", "pad_cnt",
-                                          "plain_cv")]
+                                          "count_rows", "rows", "det", "pipe", "ws8", "pad_num", "pad_cnt")]
                 + [(n, C.c_int64) for n in ("m", "annz", "mb", "nnzb", "tot", "nunits", "ngc", "cap_bcv", "cap_colp",
                                             "ovf_cap", "o_split", "o_ucnt", "o_ws8", "o_plen", "o_plenc", "o_pbase",
                                             "o_cbase", "o_colp", "o_bcv", "o_ovf", "o_scan", "ws_bytes")])
@@ -769,7 +797,7 @@ class BitmapPlan:
         if name in ("raw", "opts"):
             raise AttributeError(name)
         v = getattr(self.raw, name)
-        return bool(v) if name in ("count_rows", "rows", "det", "ws8", "pad_num", "pad_cnt", "plain_cv") else v
+        return bool(v) if name in ("count_rows", "rows", "det", "ws8", "pad_num", "pad_cnt") else v
 
 
 def _bitmap_plan(A: CSR, B: CSR, info: SpgemmInfo, pre: Optional[dict], use_ws8: bool = True) -> Optional[BitmapPlan]:
@@ -994,6 +1022,21 @@ def _det_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:
 PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper
 PIPE_CHUNK_PRODUCTS = 1 << 29      # staging per chunk (x 8 B = 4 GiB), two chunks in flight
 _SIDE = {}
+
+
+def _mark_event(stream) -> "torch.cuda.Event":
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
+
+
+def _place_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """The long-row placement stream of (device, thread) (see _long_rows)."""
+    key = (dev.index, threading.get_ident(), "place")
+    s = _SIDE.get(key)
+    if s is None:
+        s = _SIDE[key] = torch.cuda.Stream(dev)
+    return s
 
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":

@@ -1,21 +1,32 @@
 """CSR x dense SpMM: Y = A . X  (A bf16 CSR, X bf16 [n, D], fp32 accumulate).
 
-Two gfx950 kernels (``csrc/kernels/csr_spmm.hip``):
+gfx950 kernels (``csrc/kernels/csr_spmm.hip``):
 
-* ``mfma``    — panel kernel: an inspector (:func:`plan_panels`, run once per
-  matrix) lists each 64-row panel's sorted union of columns in chunks of 64;
-  the kernel gathers each chunk's X rows into LDS once, scatters the chunk's
-  entries into a dense 64x64 A tile and runs v_mfma_f32_16x16x32_bf16.
-  X rows shared by several rows of a panel are fetched once.
+* ``mfma``    — row-group MFMA kernel (D = 128; other multiples of 128 take
+  ``panel``): a wave owns 16 consecutive rows, takes their entries in chunks
+  of 32 with the sweep's 16-byte gathers (16 in flight a wave), transposes
+  the gathered X rows through LDS and multiplies with
+  v_mfma_f32_16x16x32_bf16 (K = the chunk's entries).  No inspector.
+* ``panel``   — panel MFMA kernel: an inspector (:func:`plan_panels`, run once
+  per matrix) lists each 64-row panel's sorted union of columns in chunks of
+  64; the kernel gathers each chunk's X rows into LDS once, scatters the
+  chunk's entries into a dense 64x64 A tile and runs the same MFMA.  X rows
+  shared by several rows of a panel are fetched once.
 * ``rowwise`` — VALU row-gather kernel, no inspector; one wave per row.
 * ``sweep``   — VALU row-owning sweep (D = 128): a resident grid of waves,
   each owning up to 16 rows staged in LDS, walks A's columns slice by slice
   with 16 independent 16-byte gathers in flight per wave (:func:`sweep_ok`
   checks once per operand that the rows fit).
 
-``auto`` picks ``mfma`` when the panel column reuse (nnz / union columns) is
-at least ``MFMA_MIN_REUSE`` — i.e. when the MFMA path moves fewer bytes —
-and ``rowwise`` otherwise.  CPU tensors use the OpenMP kernel.
+Both MFMA kernels multiply zero A slots into X rows of other rows of the
+group: a non-finite X value reaches every output row of its 16-row group
+(panel: 64-row panel) as NaN, where the VALU kernels keep it to the rows
+that use it.
+
+``auto`` picks ``panel`` when the panel column reuse (nnz / union columns) is
+at least ``MFMA_MIN_REUSE`` — i.e. when the panel path moves fewer bytes —
+and ``rowwise`` otherwise (``models.spmm.bench_setup`` times every
+candidate instead).  CPU tensors use the OpenMP kernel.
 """
 from __future__ import annotations
 
@@ -32,6 +43,8 @@ from .csr import CSR
 
 _native.register_hip("spmm_spmm_panel_mfma", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64,
                      c_vp, C.c_int64, C.c_int, c_vp)
+_native.register_hip("spmm_spmm_rows_mfma", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp,
+                     C.c_int64, C.c_int, c_vp)
 _native.register_hip("spmm_spmm_rowwise", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, c_vp,
                      C.c_int64, C.c_int, c_vp)
 _native.register_hip("spmm_spmm_sweep", c_vp, c_vp, c_vp, c_vp, C.c_int64, C.c_int64, C.c_int64, C.c_int64, c_vp,
@@ -199,10 +212,16 @@ def spmm(A: CSR, X: torch.Tensor, out_dtype=torch.float32, method: str = "auto",
     stream = _native.stream_ptr(dev)
     if method == "auto":
         if D % 128 == 0 and (plan is not None and plan.reuse >= MFMA_MIN_REUSE):
-            method = "mfma"
+            method = "panel"
         else:
             method = "rowwise"
+    if method == "mfma" and D != 128:
+        method = "panel"   # (the row-group kernel covers one 128-column block)
     if method == "mfma":
+        av = A.val.to(torch.bfloat16).contiguous()
+        _native.check(lib.spmm_spmm_rows_mfma(P(A.rowptr), P(A.col), P(av), P(X), D, A.m, D, P(Y), D, out_bf16,
+                                              stream), "spmm_rows_mfma")
+    elif method == "panel":
         if D % 128 != 0:
             raise ValueError("MFMA SpMM needs D % 128 == 0")
         plan = plan if plan is not None else plan_panels(A)

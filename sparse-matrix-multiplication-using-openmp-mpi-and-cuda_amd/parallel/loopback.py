@@ -245,22 +245,38 @@ class PanelComm(Comm):
     """Rank ``rank`` of ``world`` in ONE thread, for the row-block step's
     operand gathers only (``models.spgemm.RowblockGraph``: the panel sizes,
     row counts and the two payload gathers, plus agreements): the other ranks'
-    contributions are computed from ``panels`` (every rank's B row panel), so
-    rank r's whole step runs on one GPU with no peer threads.  ``gbps`` > 0
-    delivers each payload late, on a separate "link" stream after a
-    stream-ordered delay of (bytes this rank receives) / gbps, in RCCL's
-    issue order (columns, then values): ``tools/rank_emulate.py`` models a
+    contributions are computed from ``panels`` (every rank's B row panel) by
+    the payload builders the step binds (``bind_payloads``: packed columns,
+    value bits), so rank r's whole step runs on one GPU with no peer threads.
+    ``gbps`` > 0 delivers each payload late: a "wire" stream runs a
+    stream-ordered delay of (bytes this rank receives) / gbps per payload, in
+    RCCL's issue order (columns, then values), while a "link" stream writes the
+    payloads (the HBM traffic of the incoming data); a payload is delivered
+    when both are done.  ``prefill``: the payloads are written once, at the
+    first gather into each buffer, and later gathers only run the delay --
+    the panels' data must then not change -- i.e. the link model of a real
+    node, where the peers' RCCL kernels push the bytes into this GPU's memory
+    and none of this GPU's CUs copy them.  ``tools/rank_emulate.py`` models a
     rank of an N-GPU node with it; tests drive the W-rank branches with it."""
 
-    def __init__(self, rank: int, world: int, dev: torch.device, panels, gbps: float = 0.0, link_priority: int = 0):
+    def __init__(self, rank: int, world: int, dev: torch.device, panels, gbps: float = 0.0, link_priority: int = 0,
+                 prefill: bool = False):
         super().__init__(rank, world, rank, dev, "panels")
         if len(panels) != world:
             raise ValueError("PanelComm: one B panel per rank")
-        self.panels, self.gbps = panels, gbps
-        # (``link_priority`` -1: a high-priority stream, whose transfers the dispatcher puts
+        self.panels, self.gbps, self.prefill = panels, gbps, prefill
+        self._filled = set()
+        # (``link_priority`` -1: high-priority streams, whose work the dispatcher puts
         # ahead of the compute stream's large grids; tools/rank_emulate.py --link-priority)
         self.link = torch.cuda.Stream(dev, priority=link_priority) if dev.type == "cuda" else None
+        self.wire = torch.cuda.Stream(dev, priority=link_priority) if dev.type == "cuda" else None
         self._n = 0
+        self._payloads = None
+
+    def bind_payloads(self, cols, vals) -> None:
+        """``cols(panel, out)`` / ``vals(panel, out)`` write one rank's send
+        buffer of the column / value gather (the step's own builders)."""
+        self._payloads = (cols, vals)
 
     @property
     def device_collectives(self) -> bool:
@@ -281,23 +297,36 @@ class PanelComm(Comm):
         pass
 
     def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> Callable[[], None]:
-        values = self._n % 2 == 1   # RowblockGraph's order: columns, then value bits
+        if self._payloads is None:
+            raise RuntimeError("PanelComm: the step did not bind its payload builders")
+        which = self._n % 2   # RowblockGraph's order: columns, then value bits
         self._n += 1
-        emax = t.numel()
-        if out.numel() != self.world * emax or any(p.nnz > emax for p in self.panels):
-            raise ValueError(f"PanelComm: receive buffer of {out.numel()} for {self.world} panels of <= {emax}")
+        per = t.numel()
+        if out.numel() != self.world * per:
+            raise ValueError(f"PanelComm: receive buffer of {out.numel()} for {self.world} payloads of {per}")
         cur = torch.cuda.current_stream(self.device)
-        self.link.wait_stream(cur)   # (RCCL: a collective starts after the producer of its input)
-        recv_bytes = (self.world - 1) * t.numel() * t.element_size()
-        with torch.cuda.stream(self.link):
-            if self.gbps > 0:
-                from .. import _native
+        evs = []
+        if self.gbps > 0:
+            from .. import _native
 
+            self.wire.wait_stream(cur)   # (RCCL: a collective starts after the producer of its input)
+            recv_bytes = (self.world - 1) * per * t.element_size()
+            with torch.cuda.stream(self.wire):
                 _native.check(_native.hip().spmm_prim_spin(recv_bytes / (self.gbps * 1e3),
                                                            _native.stream_ptr(self.device)), "prim_spin")
-            for r, p in enumerate(self.panels):   # every panel's current columns / values
-                if p.nnz:
-                    out[r * emax:r * emax + p.nnz].copy_(p.val.view(torch.int32) if values else p.col)
-        ev = torch.cuda.Event()
-        ev.record(self.link)
-        return lambda: cur.wait_event(ev)
+            evs.append(torch.cuda.Event())
+            evs[-1].record(self.wire)
+        key = (out.data_ptr(), which)
+        if not (self.prefill and key in self._filled):
+            self._filled.add(key)
+            self.link.wait_stream(cur)
+            with torch.cuda.stream(self.link):
+                for r, p in enumerate(self.panels):   # every rank's payload from its panel's current data
+                    self._payloads[which](p, out[r * per:(r + 1) * per])
+            evs.append(torch.cuda.Event())
+            evs[-1].record(self.link)
+
+        def wait() -> None:
+            for e in evs:
+                cur.wait_event(e)
+        return wait

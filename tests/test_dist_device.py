@@ -374,6 +374,42 @@ def test_loopback_gpu_rowblock_graph(world):
     _graph_case(world)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_cols", [1, 2, 3, 1000, (1 << 20) + 1, 1 << 20, (1 << 29) - 7, 1 << 31])
+def test_packed_column_payload_roundtrip(n_cols):
+    """Column payloads packed to ceil(log2 n) bits (bm_pack_bits) and
+    unpacked from a [W, words] gather buffer with uneven, empty and
+    word-straddling panels equal the columns sent (30 bits and more: raw);
+    the kernels against plain torch."""
+    dev = torch.device("cuda")
+    bits = MS.col_bits(n_cols)
+    assert bits == 32 or (1 << bits) >= n_cols
+    g = torch.Generator().manual_seed(n_cols % 1000)
+    sizes = [0, 1, 37, 4096 + 3, 11]
+    emax = max(sizes)
+    cw = MS.packed_words(emax, bits)
+    cols = [torch.randint(0, n_cols, (k,), generator=g, dtype=torch.int64).to(torch.int32).to(dev) for k in sizes]
+    cols[-1][:] = n_cols - 1   # the largest column: every bit set
+    gc = torch.full((len(sizes) * cw,), -1, dtype=torch.int32, device=dev)
+    for r, c in enumerate(cols):
+        MS.pack_cols(c, bits, gc[r * cw:(r + 1) * cw])
+    base = torch.tensor([0] + list(__import__("itertools").accumulate(sizes)), dtype=torch.int64, device=dev)
+    out = torch.full((sum(sizes),), -5, dtype=torch.int32, device=dev)
+    MS.unpack_gathered(gc, None, len(sizes), emax, cw, bits, base, emax, out)
+    assert torch.equal(out, torch.cat(cols))
+
+
+def test_packed_words_bound():
+    """The packed payload never exceeds the raw one and always holds the
+    unpacker's second word (CPU: arithmetic only)."""
+    for n in (1, 2, 5, 1 << 20, 1 << 24, (1 << 30) + 1):
+        b = MS.col_bits(n)
+        for e in (0, 1, 31, 32, 33, 1000003):
+            w = MS.packed_words(e, b)
+            assert w >= (e if b == 32 else (e * b + 31) // 32 + 1)
+            assert b == 32 or w <= e + 1
+
+
 def test_all_gather_into_gloo_and_loopback():
     """``Comm.all_gather_into`` (the persistent-buffer gather the graph step
     uses) on the loopback backend at W = 3 (CPU)."""

@@ -93,7 +93,7 @@ def test_distributed_spmm_gloo(tmp_path, world):
 # ----------------------------------------------------------------- GPU ----
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method", ["rowwise", "mfma"])
+@pytest.mark.parametrize("method", ["rowwise", "mfma", "panel"])
 @pytest.mark.parametrize("m,n,D,d", [(1000, 800, 128, 0.02), (333, 4096, 256, 0.01), (64, 64, 128, 0.5),
                                      (4097, 300, 128, 0.05)])
 def test_spmm_gpu(method, m, n, D, d):
@@ -108,14 +108,19 @@ def test_spmm_gpu(method, m, n, D, d):
 
 
 @pytest.mark.gpu
-def test_spmm_mfma_exact_small_integers():
-    """Exact integer data catches any fragment-layout / transpose mistake."""
+@pytest.mark.parametrize("method", ["mfma", "panel"])
+@pytest.mark.parametrize("m,n,d", [(130, 200, 0.1), (4099, 3000, 0.02), (40, 100, 0.0), (17, 64, 1.0)])
+def test_spmm_mfma_exact_small_integers(method, m, n, d):
+    """Exact integer data catches any fragment-layout / transpose mistake:
+    row groups past m, empty rows / matrix, rows longer than a chunk, chunks
+    straddling rows (row-group kernel), fp32 and bf16 outputs."""
     dev = torch.device("cuda")
-    m, n, D = 130, 200, 128
-    A = gen_csr.uniform_csr(m, n, 0.1, seed=9, device=dev, values="small_int", dtype=torch.bfloat16)
+    D = 128
+    A = gen_csr.uniform_csr(m, n, d, seed=9, device=dev, values="small_int", dtype=torch.bfloat16)
     X = (torch.arange(n * D, device=dev).view(n, D) % 11 - 5).to(torch.bfloat16)
-    Y = SM.spmm(A, X, method="mfma")
-    assert torch.equal(Y, ref(A, X))
+    R = ref(A, X)
+    assert torch.equal(SM.spmm(A, X, method=method), R)
+    assert torch.equal(SM.spmm(A, X, method=method, out_dtype=torch.bfloat16).float(), R.to(torch.bfloat16).float())
 
 
 @pytest.mark.gpu
@@ -180,11 +185,12 @@ def test_spmm_graph_replay_matches_eager():
     A = gen_csr.uniform_csr(3000, 2500, 0.01, seed=41, device=dev, dtype=torch.bfloat16)
     X = (torch.rand((2500, 128), device=dev) * 2 - 1).to(torch.bfloat16)
     plan = plan_panels(A)
-    g = SpmmGraph(A, X, method="mfma", plan=plan)
-    assert torch.equal(g.run(), spmm(A, X, method="mfma", plan=plan))
-    X2 = (torch.rand((2500, 128), device=dev) * 2 - 1).to(torch.bfloat16)
-    g.X.copy_(X2)
-    assert torch.equal(g.run(), spmm(A, X2, method="mfma", plan=plan))
+    for method in ("panel", "mfma"):
+        g = SpmmGraph(A, X, method=method, plan=plan)
+        assert torch.equal(g.run(), spmm(A, X, method=method, plan=plan))
+        X2 = (torch.rand((2500, 128), device=dev) * 2 - 1).to(torch.bfloat16)
+        g.X.copy_(X2)
+        assert torch.equal(g.run(), spmm(A, X2, method=method, plan=plan))
 
 
 def _plan_chunks(P):
@@ -234,7 +240,7 @@ dev = torch.device("cuda")
 for (m, n, d) in [(4096, 3000, 0.01), (300, 200, 0.9), (70, 65, 1.0)]:
     A = gen_csr.uniform_csr(m, n, d, seed=3, device=dev, dtype=torch.bfloat16)
     X = (torch.randn(n, 256, device=dev) * 0.5).to(torch.bfloat16)
-    Y = SM.spmm(A, X, method="mfma")
+    Y = SM.spmm(A, X, method="panel")
     R = A.to_dense(torch.float32) @ X.float()
     err = float((Y - R).abs().max()) / max(1.0, float(R.abs().max()))
     assert err < 1e-3, (m, n, d, err)

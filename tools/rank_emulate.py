@@ -6,17 +6,21 @@ rank's B row panel) and times:
 * ``local_ms``: the local product against the full B (``spgemm(A_panel, B)``,
   eager, or ``--graph``: a SpgemmGraph replay) -- the step without the gather;
 * ``step_ms[gbps]`` (``--gather-gbps 0,300,...``): the whole rank-r step of
-  ``bench.py`` at N ranks, i.e. ``models.spgemm.RowblockGraph.run`` (copy of
-  the own panel into the send buffers, column gather, graph 1 = unpack +
+  ``bench.py`` at N ranks, i.e. ``models.spgemm.RowblockGraph.run`` (pack
+  of the own panel into the send buffers, column gather, graph 1 = unpack +
   B layouts + count kernel, value gather, graph 2 = unpack + padded pairs +
-  numeric), through ``parallel.loopback.PanelComm``: the gathered payloads
-  are copied into the receive buffers on a separate "link" stream after a
-  stream-ordered delay of (bytes this rank receives) / gbps, in RCCL's issue
-  order (columns, then values, one after the other), so the columns / values
-  become readable exactly when a link of that rate would deliver them and
-  the count kernel overlaps the value transfer as on the real node.  Not
-  modelled: the CUs and HBM bandwidth RCCL's own kernels take while they
-  run.  0 = delay-free (the copies only).
+  numeric), through ``parallel.loopback.PanelComm``: every rank's payload is
+  built from its panel on a "link" stream while a "wire" stream runs a
+  stream-ordered delay of (bytes this rank receives) / gbps per payload, in
+  RCCL's issue order (columns, then values); a payload is readable when
+  both are done, i.e. when a link of that rate would deliver it, and the
+  count kernel overlaps the value transfer as on the real node.  Not
+  modelled: the CUs RCCL's own kernels take while they run.  0 = delay-free
+  (the payload writes only).
+* ``step_ms_link[gbps]``: the same step with the payloads written once
+  (``PanelComm(prefill=True)``): the link delay alone, as on a node where
+  the peers push the bytes and this GPU's CUs copy none of them (the
+  ``step_ms`` model charges this GPU for writing all N payloads every step).
 
     python tools/rank_emulate.py --world 8 [--rank 0] [--gather-gbps 0,150,300]
 """
@@ -83,15 +87,21 @@ def main() -> None:
     if a.gather_gbps:
         panels = [uniform_csr(a.n, a.n, a.density, seed=a.seed + 1, device=dev, rows=p) for p in pan]
         steps = {}
+        link = {}
+        keep = []   # (graphs stay alive until the end: see tests/test_dist_device.py _graph_case_panels)
         for g in [float(x) for x in a.gather_gbps.split(",")]:
-            comm = PanelComm(a.rank, a.world, dev, panels, g, link_priority=a.link_priority)
-            rg = MS.RowblockGraph(A, panels[a.rank], comm)
-            steps[str(g)] = round(timed(rg.run, a.steps), 3)
-            C = rg.result()
-            rec.setdefault("step_nnz_C", C.nnz)
-            del rg, C, comm
-            torch.cuda.empty_cache()
+            for prefill, d in ((False, steps), (True, link)):
+                comm = PanelComm(a.rank, a.world, dev, panels, g, link_priority=a.link_priority, prefill=prefill)
+                rg = MS.RowblockGraph(A, panels[a.rank], comm)
+                d[str(g)] = round(timed(rg.run, a.steps), 3)
+                C = rg.result()
+                rec.setdefault("step_nnz_C", C.nnz)
+                if C.nnz != rec["step_nnz_C"]:
+                    raise RuntimeError("emulated steps disagree on nnz(C)")
+                keep.append(rg)
+                del C
         rec["step_ms"] = steps
+        rec["step_ms_link"] = link
     print(json.dumps(rec), flush=True)
 
 
