@@ -156,14 +156,13 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   p->lg_num = seg / nwin < 48 ? 4 : (seg / nwin < 96 ? 5 : 6);
   p->det = o->det != 0;
   p->pipe = o->pipe != 0;
-  // the row kernels exist only in their pipelined forms (padded layouts, 32-bit buffer
-  // offsets, unordered sums); every other product takes the per-unit kernels
+  // the row numeric kernel exists only in its pipelined form (padded pairs, 32-bit buffer
+  // offsets, unordered sums); every other product takes the per-unit numeric kernels
   const bool pad = o->pad != 0 && o->use_ws8 != 0;
   const int64_t ngc = (nwin + nsub_c - 1) / nsub_c;
   const int64_t cap_bcv = bnnz + (kPadPairs - 1) * (int64_t)nwin * mb;
   const int64_t cap_colp = bnnz + (kPadCols - 1) * ngc * mb;
-  p->count_rows = ws8_ok && amax >= 0 && amax <= 256 && pad && p->pipe && nsub_c == 2 && nwin >= 3 && annz > 0 &&
-                  cap_colp * 4 < ((int64_t)1 << 32) && m * nwin < ((int64_t)1 << 30);
+  p->count_rows = ws8_ok && amax >= 0 && amax <= 256;
   p->rows = ws8_ok && (o->rows_mode == 2 || cfg == 0) && pad && o->cv != 0 && !p->det && p->pipe && annz > 0 &&
             cap_bcv * 8 < ((int64_t)1 << 32);
   p->m = m;
@@ -174,7 +173,7 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   p->nunits = m * nwin;
   p->ngc = (nwin + nsub_c - 1) / nsub_c;
   p->pad_num = pad && (p->rows || !p->det) && o->cv != 0 && cap_bcv < ((int64_t)1 << 32);
-  p->pad_cnt = p->count_rows;   // (its conditions include the padded layout's)
+  p->pad_cnt = pad && p->count_rows && cap_colp < ((int64_t)1 << 32);
   p->ws8 = o->use_ws8 != 0 && ws8_ok && (p->count_rows || p->rows || p->pad_num);
   if (!p->ws8) p->pad_num = p->pad_cnt = p->rows = p->count_rows = 0;
   p->cap_bcv = p->pad_num ? cap_bcv : 0;
@@ -210,7 +209,7 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
 
 // Layouts + count kernel + unit offsets.  Bv may be null (B's values still in flight:
 // the padded pairs are then built by spmm_spgemm_bm_back).  uoff: nunits + 1 entries;
-// z: int32[4] {error bits, deferred units, numeric row ticket, count row ticket} (zeroed here).  *pairs_built: whether the padded
+// z: int32[4] {error bits, deferred units, numeric row ticket, 0} (zeroed here).  *pairs_built: whether the padded
 // pairs exist after this call (pass it to spmm_spgemm_bm_back).
 SPMM_EXPORT int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const int64_t* Brp,
                                      const int32_t* Bci, const float* Bv, void* ws, int64_t* uoff, int32_t* z,

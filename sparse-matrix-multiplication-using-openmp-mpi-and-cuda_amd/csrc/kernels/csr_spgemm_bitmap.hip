@@ -45,9 +45,9 @@ using namespace spmm_bitmap;
 #define SPMM_BM_PRIO_HI() __builtin_amdgcn_s_setprio(3)
 #define SPMM_BM_PRIO_LO() __builtin_amdgcn_s_setprio(0)
 
-// Work schedule (diagnostic builds only): ticket rows (bit 0: the pipelined numeric row
-// kernel, the default; bit 1: the pipelined count kernel) or static ones (me, me + NG, ...).
-// 1M step: static 58.5 ms, numeric tickets 54.7 ms, both 56.2-56.8 ms (PERF_LOG round 6).
+// Row schedule of the pipelined numeric row kernel: ticket rows (1, the default) or static
+// rows me, me + NG, ... (0, diagnostic builds).  1M step: static 58.5 ms, tickets 54.7 ms
+// (PERF_LOG round 6).
 #ifndef SPMM_BM_TICKETS
 #define SPMM_BM_TICKETS 1
 #endif
@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   const auto rtk = __builtin_amdgcn_make_buffer_rsrc(pa.ticket, 0, 4, 0x00020000);
   int id1 = me, id2 = me + NG, id3 = me + 2 * NG;   // rows in the "1" / "2" / "3" pipeline registers
   auto next_row = [&]() {   // row k + 4 in row k's last unit
-    if constexpr (!(SPMM_BM_TICKETS & 1)) return id3 + NG;
+    if constexpr (!SPMM_BM_TICKETS) return id3 + NG;
     return kl < 2 ? me + (kl + 4) * NG : __builtin_amdgcn_readfirstlane(s_tk[kl & 1]);
   };
 
@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
       const int64_t off = soff;
       int lim = 0;
       int tk = 0;
-      if constexpr (LAST && (SPMM_BM_TICKETS & 1))
+      if constexpr (LAST && SPMM_BM_TICKETS)
         if (tid == 0) tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rtk, tkz, 0, 0);   // (to LDS at the unit's end)
       BM_STAMP(4);   // (the previous unit's write-out)
       if (sskip) {   // uniform
@@ -1401,7 +1401,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
       BM_STAMP(0);
       BM_STAMP_UNIT();
       write_out(off, lim);
-      if constexpr (LAST && (SPMM_BM_TICKETS & 1)) {
+      if constexpr (LAST && SPMM_BM_TICKETS) {
         if (tid == 0) s_tk[kl & 1] = 6 * NG + tk;   // (read in row kl + 2's last unit, barriers between)
         ++kl;
       }
@@ -1414,9 +1414,243 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   BM_WG_FLUSH();
 }
 
+// ---- row-major count kernel (nwin <= 8, A rows <= NT entries) -------------
+// The count kernel of the same row pipeline: one window's bitmap (16 KB at
+// W = 2^17) per workgroup, so eight 256-thread workgroups share a CU and
+// hide each other's B-load latency (the 8-window, 128 KB-bitmap count kernel
+// runs one workgroup per CU).  Every unit: ORs (no return), popcount of the
+// wave's own bitmap rows, clear of the same rows, one barrier.
+template <int LGW, int NSUB, int NT, int RR, int CCAP, bool PADC>
+#ifndef SPMM_BM_COUNT_WPS   // row count kernel: waves per SIMD its registers are sized for (8: <= 64 VGPRs)
+#define SPMM_BM_COUNT_WPS 8   // (64k: 8 = 1.547-1.551 ms with 2 spills, 7 = 1.547-1.565, 6 = 1.641)
+#endif
+__global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(BmRowArgs ra) {
+  const BmArgs& p = ra.a;
+  constexpr int NW = NT / 64;
+  constexpr int NWORD = (NSUB << LGW) / 64, WPW = NWORD / NW, WPT = WPW / 64;
+  constexpr int WORDS_PER_WIN = NWORD / NSUB;
+  static_assert(WPW % 64 == 0 && WORDS_PER_WIN % WPW == 0, "a wave's bitmap block inside one window");
+  // log2 columns per lane and load: padded columns are read 4 at a time
+  // (16-byte loads: the gathers are bound by their load-instruction count,
+  // 1M count 16.5 -> 15.3 ms vs 8-byte loads, PERF_LOG round 4), the host's
+  // lane groups halved to keep a chunk at one 128-byte line
+  constexpr bool WIDE = PADC;
+  constexpr int SH = PADC ? 2 : 0;
+  constexpr int CPL = 1 << SH;
+
+  __shared__ __attribute__((aligned(16))) unsigned long long bm[NWORD];
+  __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
+  __shared__ int wsum[2 * NW];
+  __shared__ int csum[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lg = p.lg - (WIDE ? 1 : 0);
+  const int Gl = 1 << lg;
+  const int ngrp = NW << (6 - lg);
+  const int gid = (w << (6 - lg)) + (lane >> lg);
+  const int gl = lane & (Gl - 1);
+  const int nwin = p.nwin;
+  uint32_t* const bm32 = reinterpret_cast<uint32_t*>(bm);
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+  if (*p.err & 8) return;   // ws8 lengths truncated: the host re-counts with spgemm_bm (uniform exit)
+
+  for (int i = tid; i < NWORD / 2; i += NT) reinterpret_cast<uint4*>(bm)[i] = make_uint4(0, 0, 0, 0);
+
+  // 32-bit row / unit indices: the host takes this path only for m * nwin < 2^31
+  const int NG = (int)gridDim.x;
+  const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+  const int m = (int)p.m;
+  int row = me;
+  int cna = 0;
+  uint4 cwa = make_uint4(0, 0, 0, 0);
+  uint32_t cwb = 0;
+  int n1a = 0, n1b = 0, n2a = 0, n2b = 0, njj = 0;
+  uint4 nwa = make_uint4(0, 0, 0, 0);
+  uint32_t nwb = 0;
+  auto ld_arp = [&](int r, int& a, int& b) {
+    if (r < m) {
+      a = (int)p.Arp[r + vz];
+      b = (int)p.Arp[r + 1 + vz];
+    }
+  };
+  auto ld_entries = [&](int r) {
+    if (r < m) {
+      const int a0 = __builtin_amdgcn_readfirstlane(n1a), na = __builtin_amdgcn_readfirstlane(n1b) - a0;
+      if (tid < na) njj = p.Aci[a0 + tid];
+    }
+  };
+  auto ld_bounds = [&](int r) {
+    if (r < m) {
+      const int na = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
+      if (tid < na) {
+        nwa = ra.ws8[2 * (int64_t)njj];
+        const uint4 x = ra.ws8[2 * (int64_t)njj + 1];
+        nwb = x.x;
+        if constexpr (PADC) nwa.x = x.z;   // the row's first column in the padded column array
+      }
+    }
+  };
+  auto take_next = [&]() {
+    cna = __builtin_amdgcn_readfirstlane(n1b) - __builtin_amdgcn_readfirstlane(n1a);
+    cwa = nwa;
+    cwb = nwb;
+    n1a = n2a;
+    n1b = n2b;
+  };
+  ld_arp(row, n1a, n1b);
+  ld_entries(row);
+  ld_bounds(row);
+  ld_arp(row + NG, n2a, n2b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  take_next();
+  __syncthreads();
+
+  for (; row < m; row += NG) {
+    const int na = cna;
+    uint32_t bq = cwa.x;
+    for (int q = 0; q < nwin; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
+      const bool last = q + NSUB >= nwin;
+      if (q == 0) {
+        ld_entries(row + NG);
+        ld_arp(row + 2 * NG, n2a, n2b);
+      }
+      if (last) ld_bounds(row + NG);
+      const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
+      int len = 0, nch = 0;
+      if (tid < na && tid < NT) {
+        if constexpr (NSUB == 1) {
+          len = (int)((wl >> (16 * (q & 1))) & 0xffffu);
+        } else if constexpr (NSUB == 2) {   // q even: windows q and q + 1 share one 32-bit word of lengths
+          len = (int)(wl & 0xffffu) + (int)(wl >> 16);   // (lengths past nwin are packed as 0)
+        } else {   // q a multiple of NSUB: the unit's lengths are whole 32-bit words of ws8
+          static_assert(NSUB == 4 || NSUB == 8, "count units of 1, 2, 4 or 8 windows");
+          const uint32_t wq[4] = {cwa.y, cwa.z, cwa.w, cwb};
+#pragma unroll
+          for (int k = 0; k < NSUB / 2; ++k) {
+            const uint32_t x = wq[(q >> 1) + k < 4 ? (q >> 1) + k : 3];
+            len += (int)(x & 0xffffu) + (int)(x >> 16);
+          }
+        }
+        nch = (len + (Gl << SH) - 1) >> (lg + SH);
+      }
+      const uint32_t b0 = bq;
+      bq += PADC ? (uint32_t)(((len + (1 << kPadCLg) - 1) >> kPadCLg) << kPadCLg) : (uint32_t)len;
+      const int clo = q << LGW;
+      const int u = row * nwin + q;
+      int pre, plen, TC, P;
+      bm_scan2<NT>(nch, len, wsum, pre, plen, TC, P);
+      for (int cb = 0; cb < TC; cb += CCAP) {
+        const int TCb = TC - cb < CCAP ? TC - cb : CCAP;
+        const int k0 = max(cb - pre, 0), k1 = min(cb + CCAP - pre, nch);
+        for (int kk = k0; kk < k1; ++kk) {
+          const int rem = len - (kk << (lg + SH));
+          desc[pre + kk - cb] =
+              make_uint2(b0 + ((uint32_t)kk << (lg + SH)), (uint32_t)(rem < (Gl << SH) ? rem : (Gl << SH)));
+        }
+        __syncthreads();
+        const int nr = (TCb + ngrp - 1) / ngrp;
+        for (int i0 = 0; i0 < nr; i0 += RR) {
+          uint2 ds[RR];
+#pragma unroll
+          for (int d = 0; d < RR; ++d) {
+            const int t = gid + (i0 + d) * ngrp;
+            ds[d] = desc[t < TCb ? t : TCb - 1];
+          }
+          if constexpr (PADC) {
+            // four columns per lane: one 16-byte load (aligned: chunks start on
+            // 32-column boundaries of the padded array); the later columns
+            // may be past the segment (padding)
+            static_assert(RR * CPL <= 32, "one bit per loaded column");
+            uint32_t x[RR][CPL];
+            uint32_t okb = 0;   // bit d * CPL + i: column i of round d is in its segment
+#pragma unroll
+            for (int d = 0; d < RR; ++d) {
+              const int t = gid + (i0 + d) * ngrp;
+              const int nv = (int)ds[d].y - CPL * gl;
+              const bool ok = (t < TCb) & (nv > 0);
+              okb |= (ok ? ((nv >= CPL) ? (1u << CPL) - 1u : (1u << nv) - 1u) : 0u) << (d * CPL);
+#pragma unroll
+              for (int i = 0; i < CPL; ++i) x[d][i] = 0u;
+              if (i0 + d < nr) {   // wave-uniform guard
+                const uint4 v = *reinterpret_cast<const uint4*>(p.Bci + ds[d].x + (ok ? (uint32_t)(CPL * gl) : 0u));
+                x[d][0] = v.x; x[d][1] = v.y; x[d][2] = v.z; x[d][3] = v.w;
+              }
+            }
+#pragma unroll
+            for (int d = 0; d < RR; ++d) {
+#pragma unroll
+              for (int i = 0; i < CPL; ++i) {
+                if ((okb >> (d * CPL + i)) & 1u) {
+                  const int cc = (int)x[d][i] - clo;
+                  atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+                }
+              }
+            }
+          } else {
+            int x[RR];
+            uint32_t okm = 0;
+#pragma unroll
+            for (int d = 0; d < RR; ++d) {
+              const int t = gid + (i0 + d) * ngrp;
+              const bool ok = (t < TCb) & ((uint32_t)gl < ds[d].y);
+              okm |= (ok ? 1u : 0u) << d;
+              x[d] = 0;
+              if (i0 + d < nr) x[d] = p.Bci[ds[d].x + (ok ? (uint32_t)gl : 0u)];   // wave-uniform guard
+            }
+#pragma unroll
+            for (int d = 0; d < RR; ++d) {
+              if ((okm >> d) & 1u) {
+                const int cc = x[d] - clo;
+                atomicOr(bm32 + (cc >> 5), 1u << (cc & 31));
+              }
+            }
+          }
+        }
+        __syncthreads();   // descriptors consumed before they are rewritten; every OR in place
+      }
+      if (last) take_next();   // after this unit's B loads: every older load has landed
+      if (P == 0) {   // uniform: nothing was ORed
+        if constexpr (NSUB == 1) {
+          if (tid == 0) p.ucnt[u] = 0;
+        } else if (tid < NSUB && q + tid < nwin) {
+          p.ucnt[u + tid] = 0;
+        }
+        __syncthreads();   // wsum reads done before the next scan
+        continue;
+      }
+      // popcount of this wave's bitmap rows, clearing them as they are read
+      int cnt = 0;
+#pragma unroll
+      for (int kk = 0; kk < WPT; ++kk) {
+        const int wd = w * WPW + kk * 64 + lane;
+        cnt += __popcll(bm[wd]);
+        bm[wd] = 0ull;
+      }
+      cnt = bm_wave_sum(cnt);
+      if (lane == 0) csum[w] = cnt;
+      __syncthreads();
+      if constexpr (NSUB == 1) {
+        if (tid == 0) {
+          int t = 0;
+#pragma unroll
+          for (int i = 0; i < NW; ++i) t += csum[i];
+          p.ucnt[u] = t;
+        }
+      } else if (tid < NSUB && q + tid < nwin) {   // window tid of the unit: the waves whose blocks lie in it
+        constexpr int WAVES_PER_WIN = WORDS_PER_WIN / WPW;
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[tid * WAVES_PER_WIN + i];
+        p.ucnt[u + tid] = t;
+      }
+    }
+  }
+}
+
 // ---- pipelined row-major count kernel (two-window units, padded columns) ---
-// Two-window count units (a B row's two-window column segment read once for
-// both) over the padded count columns, in the pipelined form of
+// spgemm_bm_rows_count<..., NSUB = 2, PADC> in the pipelined form of
 // spgemm_bm_rows_pipe: unit k+1's scan rides unit k's OR phase (its
 // per-wave sums are written before that phase's barrier), its descriptors
 // are written after it and its B loads issued BEFORE unit k's popcount and
@@ -1431,7 +1665,6 @@ struct BmCountPipeArgs {
   BmRowArgs r;
   uint32_t colp_bytes;   // bytes of the padded column array (< 2^32: checked by the host)
   int64_t annz;          // nnz(A) > 0
-  int32_t* ticket;       // row ticket counter, zero at launch
 };
 
 template <int LGW, int NT, int RR, int CCAP>
@@ -1450,7 +1683,6 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   __shared__ __attribute__((aligned(16))) uint2 desc[CCAP];
   __shared__ int wscan[2 * NW];
   __shared__ int csum[NW];
-  __shared__ int s_tk[2];   // row tickets (as spgemm_bm_rows_pipe)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1474,16 +1706,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   const int m = (int)p.m;
   const int annz = (int)pa.annz;
   const int ngc = (nwin + 1) / 2;   // units per row
-  // row schedule: six static rows, then tickets (as spgemm_bm_rows_pipe)
-  int kl = 0;
-  int tkz;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(tkz));
-  const auto rtk = __builtin_amdgcn_make_buffer_rsrc(pa.ticket, 0, 4, 0x00020000);
+  // static row schedule (me, me + NG, ...): ticket rows as in spgemm_bm_rows_pipe measured
+  // slower here (1M 55.8 vs 54.1 ms, 65536^2 1.86 vs 1.36 ms, PERF_LOG round 6)
   int id1 = me, id2 = me + NG, id3 = me + 2 * NG;
-  auto next_row = [&]() {
-    if constexpr (!(SPMM_BM_TICKETS & 2)) return id3 + NG;
-    return kl < 2 ? me + (kl + 4) * NG : __builtin_amdgcn_readfirstlane(s_tk[kl & 1]);
-  };
+  auto next_row = [&]() { return id3 + NG; };
 
   // ---- row pipeline (as spgemm_bm_rows_pipe) --------------------------------
   auto arp2 = [&](int r, int& a, int& b) {   // (low words: nnz(A) < 2^31)
@@ -1636,9 +1862,6 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
   auto unit = [&](auto last_tag, int row, int g) {
     constexpr bool LAST = decltype(last_tag)::value;
     const int u = su, q0 = sq, TC = sTC, nr = snr, clo = sclo, P = sP;
-    int tk = 0;
-    if constexpr (LAST && (SPMM_BM_TICKETS & 2))
-      if (tid == 0) tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rtk, tkz, 0, 0);   // (to LDS at the unit's end)
     if constexpr (LAST) {   // the next row into the staging registers; the row inputs move along
       take_row();
       row_block(next_row());
@@ -1689,10 +1912,6 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_count_pipe(BmCountPipeAr
     for (int i = 0; i < WAVES_PER_WIN; ++i) t += csum[(lane & 1) * WAVES_PER_WIN + i];
     const bool wr = w == 0 && lane < NSUB && q0 + lane < nwin;
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, rsu, wr ? (u + lane) * 4 : -1, 0, 0);
-    if constexpr (LAST && (SPMM_BM_TICKETS & 2)) {
-      if (tid == 0) s_tk[kl & 1] = 6 * NG + tk;   // (read in row kl + 2's last unit, barriers between)
-      ++kl;
-    }
     BM_STAMP(6);
   };
   for (int row = me; row < m; row = cid) {   // (cid: the next row, taken by the row's last unit)
@@ -1804,9 +2023,24 @@ int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastN
   return launch_rows(kernel, ra, ra.a.m, s, nt);
 }
 
+// count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
+// per unit (32 KB, 4 per CU: a B row's column segment read once for both)
 #ifndef SPMM_BM_COUNT_RR   // B loads in flight per thread (diagnostic builds: tools/bm_variants.py)
 #define SPMM_BM_COUNT_RR 8
 #endif
+#ifndef SPMM_BM_COUNT_NT   // threads per count workgroup (the host gates A rows <= this)
+#define SPMM_BM_COUNT_NT 256
+#endif
+// workgroup size by bitmap bytes: 32 KB -> 256 threads (4 per CU), 64 KB -> 512 (2 per CU)
+constexpr int count_nt(int lgw, int nsub) {
+  return ((nsub << lgw) / 8) > (64 << 10) ? 1024 : ((nsub << lgw) / 8) > (32 << 10) ? 512 : SPMM_BM_COUNT_NT;
+}
+template <int C, int NSUB>
+struct BmRowCountKernel {
+  static constexpr int NT = count_nt(kCfgs[C].lgw, NSUB);
+  static constexpr auto k = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR, 256, false>;
+  static constexpr auto kp = spgemm_bm_rows_count<kCfgs[C].lgw, NSUB, NT, SPMM_BM_COUNT_RR / 2, 256, true>;
+};
 // pipelined (two-window units, padded columns; 32 KB bitmap + 6 KB descriptors: 4 workgroups per CU)
 template <int C>
 struct BmRowCountPipe {
@@ -1814,17 +2048,20 @@ struct BmRowCountPipe {
   static constexpr auto k = spgemm_bm_rows_count_pipe<kCfgs[C].lgw, NT, SPMM_BM_COUNT_RR / 2, 768>;
 };
 
-// The pipelined row count kernel; its conditions (kRowCountOk) are the
-// planner's (csr_bitmap_plan.hip: count_rows), every other product counts on
-// the per-unit kernel.
 template <int C>
 int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s) {
+  using K1 = BmRowCountKernel<C, 1>;
+  using K2 = BmRowCountKernel<C, 2>;
   const int64_t colp_bytes = ra.a.cap * 4;
-  if (!(ra.pad && pipe && nsub == 2 && ra.a.nwin >= 3 && annz > 0 && colp_bytes < (int64_t(1) << 32) &&
-        ra.a.m * ra.a.nwin < (int64_t(1) << 30)))
-    return (int)hipErrorInvalidValue;
-  return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz, ra.a.err + 3}, ra.a.m, s,
-                     BmRowCountPipe<C>::NT);
+  // (pipelined from two units per row up: with one, every unit is a row's last and the
+  // pipeline only adds work -- 65536^2 count 1.32 -> 1.36 ms step, PERF_LOG round 5)
+  if (ra.pad && pipe && nsub == 2 && ra.a.nwin >= 3 && K2::NT == BmRowCountPipe<C>::NT && annz > 0 &&
+      colp_bytes < (int64_t(1) << 32) && ra.a.m * ra.a.nwin < (int64_t(1) << 30))
+    return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz}, ra.a.m, s,
+                       BmRowCountPipe<C>::NT);
+  if (ra.pad)
+    return nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT);
+  return nsub == 2 ? launch_rows(K2::k, ra, s, K2::NT) : launch_rows(K1::k, ra, s, K1::NT);
 }
 
 // The pipelined row numeric kernel (2 pairs per lane and 16-byte loads on the
@@ -1969,7 +2206,7 @@ SPMM_EXPORT int spmm_spgemm_bm_numeric_rows(int cfg, const int64_t* Arp, const i
 // is set (ws8 lengths truncated); the host then uses spmm_spgemm_bm_count.
 // pad: Bci is the padded column array of spmm_spgemm_bm_pad_pairs (gc = nsub).
 // pipe: the pipelined kernel (pad, nsub 2, nnzb * 4 < 2^32, annz = nnz(A) > 0; err then
-// int32[4]: err[3] is its row-ticket counter, zero at launch).
+// int32[4]).
 SPMM_EXPORT int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8,
                                           const int32_t* Bci, int64_t m, int nwin, int lg, int nsub, int32_t* ucnt,
                                           int32_t* err, int64_t nnzb, int pad, int pipe, int64_t annz, void* stream) {

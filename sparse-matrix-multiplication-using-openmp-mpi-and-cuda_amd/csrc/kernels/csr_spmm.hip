@@ -602,11 +602,18 @@ __global__ __launch_bounds__(NT, 4) void spmm_sweep(const int64_t* __restrict__ 
 //   (issued one iteration ago) -> LDS -> 8 MFMAs.
 // D = 128, X 16-byte aligned (as spmm_sweep); fp32 accumulation.
 constexpr int RM_K = 32;
+#ifndef SPMM_RM_CPI   // row-group MFMA SpMM: chunks (of 32 entries, 8 gathers a lane) in flight per wave
+#define SPMM_RM_CPI 3
+#endif
+#ifndef SPMM_RM_WPC   // ... and the workgroups per CU its registers are sized for
+#define SPMM_RM_WPC 2
+#endif
+constexpr int RM_CPI = SPMM_RM_CPI;
 
 template <bool OUT_BF16>
 // (ci / av / X without __restrict__: restrict read-only loads are free to sink
 // below the asm barriers that keep the software pipeline's order)
-__global__ __launch_bounds__(NT, 2) void spmm_rows_mfma(const int64_t* __restrict__ rp, const int32_t* ci,
+__global__ __launch_bounds__(NT, SPMM_RM_WPC) void spmm_rows_mfma(const int64_t* __restrict__ rp, const int32_t* ci,
                                                         const unsigned short* av,
                                                         const unsigned short* X, int64_t ldx, int64_t m,
                                                         void* __restrict__ Yv, int64_t ldy) {
@@ -661,9 +668,8 @@ __global__ __launch_bounds__(NT, 2) void spmm_rows_mfma(const int64_t* __restric
         const uint4 v = base + r < e1 ? xc[i] : make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(Xs + r * 256 + (((p >> 1) ^ xswz(r)) << 5) + (p & 1) * 16) = v;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // (no fence: one wave's LDS instructions execute in order, so the transposing reads
+      // below see the stores above, and the next chunk's stores follow these reads)
       const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
       const int r0k = 8 * g + q, r1k = r0k + 4;
 #pragma unroll
@@ -675,35 +681,33 @@ __global__ __launch_bounds__(NT, 2) void spmm_rows_mfma(const int64_t* __restric
         const v8s bs = __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(v8bf, bs), acc[t], 0, 0, 0);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the image's reads before the next stores
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    // Two chunks an iteration: their 16 gathers issue together, then the next
-    // iteration's entries, then the chunks are consumed in order.  No gather is
-    // in flight across the loop's back edge (hipcc copies loop-carried load
-    // registers and waits for them there); the other resident waves cover the
-    // start of each iteration's gathers, as in spmm_sweep's rounds.
-    int c0 = 0, c1 = 0;
-    unsigned v0 = 0, v1 = 0;
-    ld_ent(e0, c0, v0);
-    ld_ent(e0 + RM_K, c1, v1);
+    // RM_CPI chunks an iteration: their 8 RM_CPI gathers issue together, then
+    // the next iteration's entries, then the chunks are consumed in order.  No
+    // gather is in flight across the loop's back edge (hipcc copies loop-carried
+    // load registers and waits for them there); the other resident waves cover
+    // the start of each iteration's gathers, as in spmm_sweep's rounds.
+    int cc[RM_CPI];
+    unsigned vv[RM_CPI];
+#pragma unroll
+    for (int q = 0; q < RM_CPI; ++q) ld_ent(e0 + q * RM_K, cc[q], vv[q]);
 #pragma unroll 1
-    for (int64_t base = e0; base < e1; base += 2 * RM_K) {
-      uint4 xA[8], xB[8];
-      gather(c0, xA);
-      gather(c1, xB);
-      int c0n, c1n;
-      unsigned v0n, v1n;
-      ld_ent(base + 2 * RM_K, c0n, v0n);
-      ld_ent(base + 3 * RM_K, c1n, v1n);
+    for (int64_t base = e0; base < e1; base += RM_CPI * RM_K) {
+      uint4 x[RM_CPI][8];
+#pragma unroll
+      for (int q = 0; q < RM_CPI; ++q) gather(cc[q], x[q]);
+      int cn[RM_CPI];
+      unsigned vn[RM_CPI];
+#pragma unroll
+      for (int q = 0; q < RM_CPI; ++q) ld_ent(base + (RM_CPI + q) * RM_K, cn[q], vn[q]);
       asm volatile("" ::: "memory");   // (every load above issues before the first chunk is consumed)
-      consume(base, xA, v0);
-      consume(base + RM_K, xB, v1);   // (past the entries: all-zero A)
-      c0 = c0n;
-      c1 = c1n;
-      v0 = v0n;
-      v1 = v1n;
+#pragma unroll
+      for (int q = 0; q < RM_CPI; ++q) consume(base + q * RM_K, x[q], vv[q]);   // (past the entries: zero A)
+#pragma unroll
+      for (int q = 0; q < RM_CPI; ++q) {
+        cc[q] = cn[q];
+        vv[q] = vn[q];
+      }
     }
   }
   // C/D map: col = lane & 15 of tile t, row = 4 (lane / 16) + i

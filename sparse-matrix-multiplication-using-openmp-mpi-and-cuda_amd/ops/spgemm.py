@@ -329,20 +329,6 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
     nwg_h = np.maximum((na_h + epw - 1) // epw, 1)
     bad = torch.zeros(1, dtype=torch.int64, device=dev)   # rows whose counts disagree (device-side)
     nil = None
-    cur = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
-    sP = None
-    pending = []   # (event after its accumulation, buffers...) of batches not yet placed
-
-    def place_pending() -> None:
-        while pending:
-            ready, rt_off_p, dst_p, rt_nnz_p, scratch_p, nrt_p = pending.pop(0)
-            sP.wait_event(ready)
-            _native.check(lib.spmm_spgemm_long_place(P(rt_off_p), P(dst_p), P(rt_nnz_p), nrt_p, P(scratch_p),
-                                                     P(Cci), P(Cv), sP.cuda_stream), "long_place")
-            for t in (rt_off_p, dst_p, rt_nnz_p, scratch_p):
-                t.record_stream(sP)
-    if values and defer is None and cur is not None and stream == cur.cuda_stream and nrows > 0:
-        sP = _place_stream(dev)
     start, done = 0, 0
     while start < nrows:
         # batch = the longest run of rows from start whose products fit cap (at least one row)
@@ -411,9 +397,6 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         rt_cnt = T.reshape(-1)
         if LONG_STATS is not None:
             _long_stats(rt_cnt + D.reshape(-1) if direct else rt_cnt)
-        if pending:   # the previous batch's copy starts with this batch's accumulation
-            pending[-1] = (_mark_event(cur),) + pending[-1][1:]
-            place_pending()
         rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
         lists = torch.empty(2 * R * nch + 4, dtype=torch.int32, device=dev)   # the two kernels' item lists + counters
         _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
@@ -434,23 +417,11 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
             defer.append((rb, rt_off, rt_nnz, scratch))
         elif values:
             dst = (Crp[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
-            if sP is not None:
-                # the copy into C waits for the NEXT batch's accumulation and runs beside it
-                # on the place stream (long_dense / long_rank are LDS-atomic bound, the copy
-                # HBM bound; beside the routing scatter, HBM bound too, it gained nothing);
-                # the batch's buffers stay allocated until that stream has read them
-                ready = torch.cuda.Event()
-                ready.record(cur)
-                pending.append((ready, rt_off, dst, rt_nnz, scratch, R * nch))
-            else:
-                _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
-                                                         P(Cv), stream), "long_place")
+            _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
+                                                     P(Cv), stream), "long_place")
         del scratch
         done = int(csum_h[end - 1])
         start = end
-    if sP is not None:
-        place_pending()   # (the last batch: nothing left to run beside)
-        cur.wait_stream(sP)   # C's long rows are complete in stream order from here
     nbad = int(bad)
     if nbad:
         raise RuntimeError(f"spgemm long rows: routing histogram or numeric count disagrees with the product / "
@@ -818,7 +789,7 @@ def bitmap_buffers(plan: BitmapPlan, dev: torch.device, cap: Optional[int] = Non
     use them are graph-capturable as they are."""
     raw = plan.raw
     out = dict(ws=torch.empty(max(raw.ws_bytes, 1), dtype=torch.uint8, device=dev),
-               # err, deferred count, numeric / count row tickets (zeroed by the front)
+               # err, deferred count, numeric row ticket, spare (zeroed by the front)
                z=torch.empty(4, dtype=torch.int32, device=dev),
                uoff=torch.empty(raw.nunits + 1, dtype=torch.int64, device=dev), nunits=raw.nunits, ws8=bool(raw.ws8))
     if cap is not None:
@@ -1022,21 +993,6 @@ def _det_cpu(A: CSR, B: CSR, info: SpgemmInfo) -> CSR:
 PIPE_MIN_PRODUCTS = 1 << 26        # smaller products: one compaction after all rows is cheaper
 PIPE_CHUNK_PRODUCTS = 1 << 29      # staging per chunk (x 8 B = 4 GiB), two chunks in flight
 _SIDE = {}
-
-
-def _mark_event(stream) -> "torch.cuda.Event":
-    ev = torch.cuda.Event()
-    ev.record(stream)
-    return ev
-
-
-def _place_stream(dev: torch.device) -> "torch.cuda.Stream":
-    """The long-row placement stream of (device, thread) (see _long_rows)."""
-    key = (dev.index, threading.get_ident(), "place")
-    s = _SIDE.get(key)
-    if s is None:
-        s = _SIDE[key] = torch.cuda.Stream(dev)
-    return s
 
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
