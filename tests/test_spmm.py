@@ -109,11 +109,13 @@ def test_spmm_gpu(method, m, n, D, d):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("method", ["mfma", "panel"])
-@pytest.mark.parametrize("m,n,d", [(130, 200, 0.1), (4099, 3000, 0.02), (40, 100, 0.0), (17, 64, 1.0)])
+@pytest.mark.parametrize("m,n,d", [(130, 200, 0.1), (4099, 3000, 0.02), (40, 100, 0.0), (17, 64, 1.0),
+                                   (48, 4096, 0.025)])
 def test_spmm_mfma_exact_small_integers(method, m, n, d):
     """Exact integer data catches any fragment-layout / transpose mistake:
     row groups past m, empty rows / matrix, rows longer than a chunk, chunks
-    straddling rows (row-group kernel), fp32 and bf16 outputs."""
+    straddling rows (row-group kernel; 48 x 4096 @ 2.5 %: ~1600 entries per
+    16 rows), fp32 and bf16 outputs."""
     dev = torch.device("cuda")
     D = 128
     A = gen_csr.uniform_csr(m, n, d, seed=9, device=dev, values="small_int", dtype=torch.bfloat16)
@@ -121,6 +123,37 @@ def test_spmm_mfma_exact_small_integers(method, m, n, d):
     R = ref(A, X)
     assert torch.equal(SM.spmm(A, X, method=method), R)
     assert torch.equal(SM.spmm(A, X, method=method, out_dtype=torch.bfloat16).float(), R.to(torch.bfloat16).float())
+
+
+@pytest.mark.gpu
+def test_spmm_mfma_row_kernel_segments():
+    """The row-group kernel on rows whose entries all sit in one half of the
+    columns, empty rows between them, rows crossing the middle, and the same
+    matrix with its columns NOT sorted inside the rows (CSR allows it): exact
+    on integers."""
+    dev = torch.device("cuda")
+    m, n, D = 37, 1000, 128
+    g = torch.Generator().manual_seed(11)
+    rows, cols = [], []
+    for r in range(m):
+        kind = r % 4
+        if kind == 3:
+            continue   # empty row
+        lo, hi = {0: (0, 512), 1: (512, 1000), 2: (400, 700)}[kind]
+        c = torch.randperm(hi - lo, generator=g)[:min(40, hi - lo)] + lo
+        rows.append(torch.full((c.numel(),), r))
+        cols.append(c)
+    rows, cols = torch.cat(rows), torch.cat(cols)
+    vals = torch.randint(-3, 4, (rows.numel(),), generator=g).float()
+    A = CS.from_coo(rows, cols, vals, m, n).to(dev)
+    A = CS.CSR(A.m, A.n, A.rowptr, A.col, A.val.to(torch.bfloat16))
+    X = (torch.arange(n * D, device=dev).view(n, D) % 11 - 5).to(torch.bfloat16)
+    assert torch.equal(SM.spmm(A, X, method="mfma"), ref(A, X))
+    # columns NOT sorted inside the rows
+    perm = torch.cat([torch.randperm(int(b - a), generator=g) + int(a)
+                      for a, b in zip(A.rowptr[:-1].tolist(), A.rowptr[1:].tolist())]).to(dev)
+    U = CS.CSR(A.m, A.n, A.rowptr, A.col[perm].contiguous(), A.val[perm].contiguous())
+    assert torch.equal(SM.spmm(U, X, method="mfma"), ref(A, X))
 
 
 @pytest.mark.gpu
