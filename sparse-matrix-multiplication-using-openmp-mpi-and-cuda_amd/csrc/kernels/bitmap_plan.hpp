@@ -25,4 +25,18 @@ struct SpmmBmPlan {
   int64_t o_split, o_ucnt, o_ws8, o_plen, o_plenc, o_pbase, o_cbase, o_colp, o_bcv, o_ovf, o_scan, ws_bytes;
 };
 
+// B as it lands from the row-block all-gathers (models/spgemm.py RowblockGraph), read in
+// place by the layout kernels instead of being unpacked into contiguous arrays first.
+// Panel r (B rows rbase[r] .. rbase[r + 1], entries ebase[r] .. ebase[r + 1]) has its
+// columns at gc + r * cstride (packed to `bits` bits when bits < 32) and its value bits at
+// gv + r * vstride.  gc == nullptr: B is contiguous (the plain arrays).
+struct SpmmBmGathered {
+  const uint32_t* gc;
+  const uint32_t* gv;
+  const int64_t* ebase;   // device [W + 1]
+  const int64_t* rbase;   // device [W + 1]
+  int64_t cstride, vstride;
+  int32_t W, bits;
+};
+
 }

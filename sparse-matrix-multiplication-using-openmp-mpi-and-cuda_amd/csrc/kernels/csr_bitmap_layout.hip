@@ -6,11 +6,41 @@
 // bytes per lane), and the pack / unpack of an all-gathered operand payload
 // (models/spgemm.py).
 #include "bitmap_common.hpp"
+#include "bitmap_plan.hpp"
 #include "common.hpp"
 
 using namespace spmm_bitmap;
 
 namespace {
+
+// B entry access for the layout kernels: the contiguous arrays, or the gathered
+// panels in place (SpmmBmGathered).  begin(j) fixes the panel of row j (a loop
+// over the W panel bounds); col(e) / val(e) then take B's global entry index.
+struct BView {
+  const int32_t* col;
+  const uint32_t* val;
+  SpmmBmGathered g;
+  const uint32_t* pc = nullptr;   // row's panel: its column / value words, its first entry
+  const uint32_t* pv = nullptr;
+  int64_t e0 = 0;
+  __device__ void begin(int64_t j) {
+    if (!g.gc) return;
+    int r = 0;
+    while (r + 1 < g.W && g.rbase[r + 1] <= j) ++r;
+    pc = g.gc + (int64_t)r * g.cstride;
+    pv = g.gv ? g.gv + (int64_t)r * g.vstride : nullptr;
+    e0 = g.ebase[r];
+  }
+  __device__ uint32_t c(int64_t e) const {
+    if (!g.gc) return (uint32_t)col[e];
+    const int64_t i = e - e0;
+    if (g.bits >= 32) return pc[i];
+    const int64_t o = i * g.bits;   // two aligned words hold the entry (the sender pads one word)
+    const uint64_t two = (uint64_t)pc[(o >> 5) + 1] << 32 | pc[o >> 5];
+    return (uint32_t)(two >> (o & 31)) & ((1u << g.bits) - 1u);
+  }
+  __device__ uint32_t v(int64_t e) const { return g.gc ? pv[e - e0] : val[e]; }
+};
 
 // ws8[j] from ws (nwin <= 8): first index + 16-bit window lengths; err bit 3
 // if a window segment of some B row is 65536 entries or longer.  plen (if
@@ -46,15 +76,15 @@ __global__ __launch_bounds__(256) void bm_pack_ws8(const uint32_t* __restrict__ 
 // row base pbase[j] + the padded start of each window (padding slots are left
 // as they are: the kernels never read a padded slot as a product), and stores
 // the base in ws8[2j + 1].y.
-__global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__ ws, const int32_t* __restrict__ col,
-                                                    const uint32_t* __restrict__ val, int64_t mb, int nwin, int lgw,
-                                                    const int64_t* __restrict__ pbase, uint4* __restrict__ ws8,
+__global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__ ws, BView B, int64_t mb, int nwin,
+                                                    int lgw, const int64_t* __restrict__ pbase, uint4* __restrict__ ws8,
                                                     uint2* __restrict__ out, const int64_t* __restrict__ cbase,
                                                     int gc, int32_t* __restrict__ outc, int64_t cap, int64_t cap_c,
                                                     int32_t* __restrict__ err) {
   const int lane = threadIdx.x & 63;
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (j >= mb) return;
+  B.begin(j);
   const uint32_t* wr = ws + j * (nwin + 1);
   const uint32_t w = lane <= nwin ? wr[lane] : 0u;   // lane q: first index of window q (q = nwin: row end)
   const int64_t base = out ? pbase[j] : 0, cb = outc ? cbase[j] : 0;
@@ -85,12 +115,12 @@ __global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__
   for (uint32_t e0 = r0; e0 < r1; e0 += 64) {
     const uint32_t e = e0 + lane;
     const bool ok = e < r1;
-    const uint32_t c = ok ? (uint32_t)col[e] : 0u;
+    const uint32_t c = ok ? B.c(e) : 0u;
     const int q = (int)(c >> lgw);
     if (out) {
       const int64_t d = base + (uint32_t)(e + (uint32_t)__shfl((int)dp, q));
       if (ok) {
-        if (d < cap) out[d] = make_uint2(c, val[e]);
+        if (d < cap) out[d] = make_uint2(c, B.v(e));
         else atomicOr(err, 32);   // (a layout bug, never a write out of bounds)
       }
     }
@@ -106,8 +136,7 @@ __global__ __launch_bounds__(256) void bm_pad_pairs(const uint32_t* __restrict__
 
 // ws[j * (nwin + 1) + q] = first index of B row j whose column >= q * 2^lgw
 // (q = 0: row start, q = nwin: row end).  One thread per (row, q).
-__global__ __launch_bounds__(256) void bm_window_splits(const int64_t* __restrict__ Brp,
-                                                        const int32_t* __restrict__ Bci, int64_t mb, int lgw,
+__global__ __launch_bounds__(256) void bm_window_splits(const int64_t* __restrict__ Brp, BView B, int64_t mb, int lgw,
                                                         int nwin, uint32_t* __restrict__ ws) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t nw1 = nwin + 1;
@@ -120,10 +149,11 @@ __global__ __launch_bounds__(256) void bm_window_splits(const int64_t* __restric
   } else if (q == nwin) {
     lo = hi;
   } else {
+    B.begin(j);
     const int64_t bound = (int64_t)q << lgw;
     while (lo < hi) {
       const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)Bci[mid] < bound) lo = mid + 1; else hi = mid;
+      if ((int64_t)B.c(mid) < bound) lo = mid + 1; else hi = mid;
     }
   }
   ws[t] = (uint32_t)lo;
@@ -193,13 +223,27 @@ __global__ __launch_bounds__(256) void bm_pack_bits(const uint32_t* __restrict__
 
 }  // namespace
 
+namespace {
+// (a null or column-less gathered view: the contiguous arrays)
+BView bview(const int32_t* col, const void* val, const SpmmBmGathered* g) {
+  BView v{col, (const uint32_t*)val, SpmmBmGathered{}};
+  if (g && g->gc) v.g = *g;
+  return v;
+}
+bool bview_ok(const SpmmBmGathered* g, bool values) {
+  return !g || !g->gc || (g->W >= 1 && g->bits >= 1 && g->bits <= 32 && g->ebase && g->rbase && (!values || g->gv));
+}
+}  // namespace
+
+// g (may be null): B read in place from its gathered panels (SpmmBmGathered), Bci unused.
 SPMM_EXPORT int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin,
-                                      uint32_t* ws, void* stream) {
+                                      uint32_t* ws, const SpmmBmGathered* g, void* stream) {
   if (mb <= 0) return 0;
   const int64_t n = mb * (nwin + 1);
-  if (nwin < 1 || lgw < 6 || lgw > 30 || n > (int64_t)UINT32_MAX - 255) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_window_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Brp, Bci,
-                     mb, lgw, nwin, ws);
+  if (nwin < 1 || lgw < 6 || lgw > 30 || n > (int64_t)UINT32_MAX - 255 || !bview_ok(g, false))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bm_window_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Brp,
+                     bview(Bci, nullptr, g), mb, lgw, nwin, ws);
   SPMM_LAUNCH_CHECK();
   return 0;
 }
@@ -227,12 +271,13 @@ SPMM_EXPORT int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin
 SPMM_EXPORT int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb,
                                          int nwin, int lgw, const int64_t* pbase, void* ws8, void* out, const int64_t* cbase,
                                          int gc, int32_t* outc, int64_t cap, int64_t cap_c, int32_t* err,
-                                         void* stream) {
+                                         const SpmmBmGathered* g, void* stream) {
   if (mb <= 0) return 0;
-  if (nwin < 1 || nwin > 8 || gc < 1 || gc > 8 || lgw < 1 || lgw > 30 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX)
+  if (nwin < 1 || nwin > 8 || gc < 1 || gc > 8 || lgw < 1 || lgw > 30 || (mb * 64 + 255) / 256 > (int64_t)UINT32_MAX ||
+      !bview_ok(g, out != nullptr))
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bm_pad_pairs, dim3((unsigned)((mb * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws, col,
-                     (const uint32_t*)val, mb, nwin, lgw, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc, cap, cap_c,
+  hipLaunchKernelGGL(bm_pad_pairs, dim3((unsigned)((mb * 64 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
+                     bview(col, val, g), mb, nwin, lgw, pbase, (uint4*)ws8, (uint2*)out, cbase, gc, outc, cap, cap_c,
                      err);
   SPMM_LAUNCH_CHECK();
   return 0;

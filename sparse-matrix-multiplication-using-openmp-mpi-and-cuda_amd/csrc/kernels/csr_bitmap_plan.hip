@@ -24,12 +24,12 @@
 extern "C" {
 int spmm_spgemm_bm_config(int cfg, int* lgw, int* nsub_count, int* pcap_fast, int* rounds_fast, int* reload_rows);
 int spmm_spgemm_bm_splits(const int64_t* Brp, const int32_t* Bci, int64_t mb, int lgw, int nwin, uint32_t* ws,
-                          void* stream);
+                          const SpmmBmGathered* g, void* stream);
 int spmm_spgemm_bm_pack_ws8(const uint32_t* ws, int64_t mb, int nwin, void* ws8, int32_t* err, int64_t* plen,
                             int64_t* plen_c, int gc, void* stream);
 int spmm_spgemm_bm_pad_pairs(const uint32_t* ws, const int32_t* col, const float* val, int64_t mb, int nwin, int lgw,
                              const int64_t* pbase, void* ws8, void* out, const int64_t* cbase, int gc, int32_t* outc,
-                             int64_t cap, int64_t cap_c, int32_t* err, void* stream);
+                             int64_t cap, int64_t cap_c, int32_t* err, const SpmmBmGathered* g, void* stream);
 int spmm_spgemm_bm_count(int cfg, const int64_t* Arp, const int32_t* Aci, const uint32_t* ws, const int32_t* Bci,
                          int64_t m, int nwin, int lg, int32_t* ucnt, int32_t* err, void* stream);
 int spmm_spgemm_bm_count_rows(int cfg, const int64_t* Arp, const int32_t* Aci, const void* ws8, const int32_t* Bci,
@@ -201,6 +201,14 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   return 0;
 }
 
+// Whether the plan's kernels read B only through the layouts built by the splits / pad
+// passes (so B may stay in its gathered panels): pipelined row count on the padded count
+// columns, pipelined row numeric + the reload kernel on the padded pairs.
+SPMM_EXPORT int spmm_spgemm_bm_gathered_ok(const SpmmBmPlan* p) {
+  return p->ws8 && p->count_rows && p->pad_cnt && p->rows && p->pad_num && p->pipe && !p->det && p->nsub_c == 2 &&
+         p->nwin >= 2;
+}
+
 #define BM_TRY(x)               \
   do {                          \
     const int _rc = (x);        \
@@ -208,14 +216,19 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   } while (0)
 
 // Layouts + count kernel + unit offsets.  Bv may be null (B's values still in flight:
-// the padded pairs are then built by spmm_spgemm_bm_back).  uoff: nunits + 1 entries;
+// the padded pairs are then built by spmm_spgemm_bm_back).  g (may be null): B read in
+// place from its all-gathered panels (SpmmBmGathered; Bci / Bv unused): only for plans
+// whose kernels read B through the padded layouts alone (spmm_spgemm_bm_gathered_ok).
+// uoff: nunits + 1 entries;
 // z: int32[4] {error bits, deferred units, numeric row ticket, 0} (zeroed here).  *pairs_built: whether the padded
 // pairs exist after this call (pass it to spmm_spgemm_bm_back).
 SPMM_EXPORT int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const int64_t* Brp,
                                      const int32_t* Bci, const float* Bv, void* ws, int64_t* uoff, int32_t* z,
-                                     int* pairs_built, void* stream) {
+                                     int* pairs_built, const SpmmBmGathered* g, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   *pairs_built = 0;
+  const bool gath = g != nullptr && g->gc != nullptr;
+  if (gath && !spmm_spgemm_bm_gathered_ok(p)) return (int)hipErrorInvalidValue;
   if (hipMemsetAsync(z, 0, 16, s) != hipSuccess || hipMemsetAsync(uoff, 0, 8, s) != hipSuccess)
     return (int)hipErrorUnknown;
   uint32_t* split = at<uint32_t>(ws, p->o_split);
@@ -228,16 +241,16 @@ SPMM_EXPORT int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, co
   int32_t* colp = at<int32_t>(ws, p->o_colp);
   void* bcv = at<void>(ws, p->o_bcv);
   void* scan = at<void>(ws, p->o_scan);
-  BM_TRY(spmm_spgemm_bm_splits(Brp, Bci, p->mb, p->lgw, p->nwin, split, s));
+  BM_TRY(spmm_spgemm_bm_splits(Brp, Bci, p->mb, p->lgw, p->nwin, split, g, s));
   if (p->ws8) BM_TRY(spmm_spgemm_bm_pack_ws8(split, p->mb, p->nwin, ws8, z, plen, plenc, p->nsub_c, s));
   if (p->ws8 && p->count_rows) {
     if (colp != nullptr) {
       BM_TRY(spmm_prim_scan(plenc, 8, p->mb, cbase, 0, scan, s));
-      const bool both = p->pad_num && Bv != nullptr;   // values here: both layouts in one pass
+      const bool both = p->pad_num && (gath ? g->gv != nullptr : Bv != nullptr);   // values here: both layouts, one pass
       if (both) BM_TRY(spmm_prim_scan(plen, 8, p->mb, pbase, 0, scan, s));
       BM_TRY(spmm_spgemm_bm_pad_pairs(split, Bci, both ? Bv : nullptr, p->mb, p->nwin, p->lgw, both ? pbase : nullptr,
                                       ws8, both ? bcv : nullptr, cbase, p->nsub_c, colp, both ? p->cap_bcv : 0,
-                                      p->cap_colp, z, s));
+                                      p->cap_colp, z, g, s));
       *pairs_built = both ? 1 : 0;
     }
     BM_TRY(spmm_spgemm_bm_count_rows(p->cfg, Arp, Aci, ws8, colp != nullptr ? colp : Bci, p->m, p->nwin, p->lg_c,
@@ -253,8 +266,10 @@ SPMM_EXPORT int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, co
 SPMM_EXPORT int spmm_spgemm_bm_back(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const float* Av,
                                     const int32_t* Bci, const float* Bv, int pairs_built, void* ws,
                                     const int64_t* uoff, int32_t* z, int64_t cap, int32_t* Cci, float* Cv,
-                                    void* stream) {
+                                    const SpmmBmGathered* g, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (g != nullptr && g->gc != nullptr && (!spmm_spgemm_bm_gathered_ok(p) || g->gv == nullptr))
+    return (int)hipErrorInvalidValue;
   uint32_t* split = at<uint32_t>(ws, p->o_split);
   void* ws8 = at<void>(ws, p->o_ws8);
   int64_t* plen = at<int64_t>(ws, p->o_plen);
@@ -266,7 +281,7 @@ SPMM_EXPORT int spmm_spgemm_bm_back(const SpmmBmPlan* p, const int64_t* Arp, con
   if (p->pad_num && !pairs_built) {
     BM_TRY(spmm_prim_scan(plen, 8, p->mb, pbase, 0, scan, s));
     BM_TRY(spmm_spgemm_bm_pad_pairs(split, Bci, Bv, p->mb, p->nwin, p->lgw, pbase, ws8, bcv, nullptr, 1, nullptr,
-                                    p->cap_bcv, 0, z, s));
+                                    p->cap_bcv, 0, z, g, s));
   }
   if (p->ws8 && p->rows) {
     return spmm_spgemm_bm_numeric_rows(p->cfg, Arp, Aci, Av, ws8, split, Bci, Bv, bcv, p->m, p->nwin, p->lg_num, uoff,

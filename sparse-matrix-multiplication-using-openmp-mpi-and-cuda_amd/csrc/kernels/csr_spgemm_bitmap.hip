@@ -293,7 +293,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   constexpr int RR = MODE == 1 ? R : (MODE == 0 ? 16 : 8);   // product slots per lane
   constexpr int PPL = WIDE ? 2 : 1;   // pairs per lane and load
   constexpr int RL = RR / PPL;        // load rounds
-  static_assert(!WIDE || (MODE == 1 && CV && !DET && RR % 2 == 0), "wide loads: fast numeric, interleaved pairs");
+  static_assert(!WIDE || (MODE != 0 && CV && !DET && RR % 2 == 0), "wide loads: numeric / reload, padded pairs");
   // deterministic fix-up list: the fast kernel defers a unit that overflows
   // it to the reload kernel, whose list is larger (it has one CU's LDS)
   constexpr int LCAP = !DET ? 1 : (MODE == 2 ? 1024 : 64);
@@ -685,7 +685,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         SPMM_BM_PRIO_LO();
         dupm = or_all();
       } else {
-        for (int i0 = 0; i0 < nr; i0 += RR) {
+        for (int i0 = 0; i0 < nr; i0 += RL) {
           fetch(i0, nr, TC, clo);
           or_all();
         }
@@ -813,7 +813,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
         for (int i = tid; i < total; i += NT) items[i] = 0ull;
         __syncthreads();
         bool tri = false;
-        for (int i0 = 0; i0 < nr; i0 += RR) {
+        for (int i0 = 0; i0 < nr; i0 += RL) {
           fetch(i0, nr, TC, clo);
           // the value adds: one compare-swap try each, ds_add_f32 for the lanes that lost (the
           // reload's adds land on distinct slots almost always: ~3x fewer LDS cycles than
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
           if constexpr (MODE == 1) {
             append(0);
           } else {
-            for (int i0 = 0; i0 < nr; i0 += RR) {   // the products again (B re-read)
+            for (int i0 = 0; i0 < nr; i0 += RL) {   // the products again (B re-read)
               fetch(i0, nr, TC, clo);
               append(i0);
             }
@@ -1971,6 +1971,10 @@ struct BmKernels {
                                               K.rounds_fast * (kFastNT / 16), 1, false, kWide, kWide>;
   static constexpr int kReloadNT = reload_nt(K.lgw);
   static constexpr auto reload = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2>;
+  // the reload kernel on the padded pairs (two a lane; the row numeric kernel's deferred
+  // units): reads B only through ws8 + the pairs, so B's plain arrays need not exist
+  static constexpr auto reload_wide = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2, false, true,
+                                                true>;
   static constexpr auto fast_det = spgemm_bm<K.lgw, 1, kFastNT, K.pcap_fast, K.rounds_fast,
                                              K.rounds_fast * (kFastNT / 16), 1, true>;
   static constexpr auto reload_det = spgemm_bm<K.lgw, 1, kReloadNT, reload_pcap(K.lgw), 8, kReloadCcap, 2, true>;
@@ -2074,7 +2078,9 @@ int bm_numeric_rows(BmRowArgs ra, int det, int64_t nbcv, int pipe, int64_t annz,
     return (int)hipErrorInvalidValue;
   const int rc = launch_rows(K::kpipe, BmPipeArgs{ra, (uint32_t)(nbcv * 8), annz, ra.a.err + 2}, ra.a.m, s, K::NT);
   if (rc) return rc;
-  return launch_bm(BmKernels<C>::reload, BmKernels<C>::kReloadNT, int64_t(1) << 30, ra.a, s);
+  BmArgs ar = ra.a;   // (the padded pairs and their bounds: ws8)
+  ar.ws8 = ra.ws8;
+  return launch_bm(BmKernels<C>::reload_wide, BmKernels<C>::kReloadNT, int64_t(1) << 30, ar, s);
 }
 
 template <int C>

@@ -55,10 +55,10 @@ int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t annz, int64
                              int64_t tot, int64_t nonempty, int64_t amax, double mean_seg, SpmmBmPlan* p);
 int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const int64_t* Brp,
                          const int32_t* Bci, const float* Bv, void* ws, int64_t* uoff, int32_t* z, int* pairs_built,
-                         void* stream);
+                         const SpmmBmGathered* g, void* stream);
 int spmm_spgemm_bm_back(const SpmmBmPlan* p, const int64_t* Arp, const int32_t* Aci, const float* Av,
                         const int32_t* Bci, const float* Bv, int pairs_built, void* ws, const int64_t* uoff,
-                        int32_t* z, int64_t cap, int32_t* Cci, float* Cv, void* stream);
+                        int32_t* z, int64_t cap, int32_t* Cci, float* Cv, const SpmmBmGathered* g, void* stream);
 }
 
 namespace a4 {
@@ -152,7 +152,7 @@ bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
     DevBuf<int64_t> uoff((size_t)p.nunits + 1, s);
     int built = 0;
     A4_HIP((hipError_t)spmm_spgemm_bm_front(&p, A.rp.get(), A.ci.get(), B.rp.get(), B.ci.get(), B.v.get(), ws.get(),
-                                            uoff.get(), z.get(), &built, s));
+                                            uoff.get(), z.get(), &built, nullptr, s));
     const int64_t nnz = down(uoff.get() + p.nunits, 1, s)[0];   // the one sizing read-back
     const int e0 = down(z.get(), 1, s)[0];
     A4_CHECK((e0 & 32) == 0, "spgemm bitmap: padded B layout overflow");
@@ -168,7 +168,7 @@ bool bitmap_product(const DCsr& A, const DCsr& B, const Plan& pl, hipStream_t s,
     C.ci = DevBuf<int32_t>((size_t)std::max<int64_t>(nnz, 1), s);
     C.v = DevBuf<float>((size_t)std::max<int64_t>(nnz, 1), s);
     A4_HIP((hipError_t)spmm_spgemm_bm_back(&p, A.rp.get(), A.ci.get(), A.v.get(), B.ci.get(), B.v.get(), built,
-                                           ws.get(), uoff.get(), z.get(), nnz, C.ci.get(), C.v.get(), s));
+                                           ws.get(), uoff.get(), z.get(), nnz, C.ci.get(), C.v.get(), nullptr, s));
     const int e = down(z.get(), 1, s)[0];
     A4_CHECK((e & 2) == 0, "spgemm bitmap: numeric and count kernels disagree");
     // a unit beyond the reload kernel's budget (bits 0 / 2), or, deterministic, a unit no

@@ -317,9 +317,15 @@ class RowblockGraph:
     columns and values, the plan's workspace, C at its product-count bound.
     Two HIP graphs are captured on a side stream:
 
-      graph 1: unpack the gathered columns, B's column layouts (window splits,
-               packed bounds, padded count columns), count kernel, unit scan;
-      graph 2: unpack the gathered values, padded pairs, numeric + reload.
+      graph 1: B's column layouts (window splits, packed bounds, padded count
+               columns), count kernel, unit scan;
+      graph 2: padded pairs, numeric + reload.
+
+    The layout passes read B in place from the gathered [world, stride]
+    buffers (columns unpacked from their 20-bit packing on the fly) when the
+    plan's kernels read B only through its padded layouts (the 1M config:
+    ``ops.spgemm.bitmap_gathered_ok``); otherwise graph 1 / graph 2 first
+    unpack the gathered columns / values into B's arrays.
 
     ``run()`` = copy this rank's B panel (columns packed to ceil(log2 n) bits,
     value bits) into the send
@@ -384,6 +390,18 @@ class RowblockGraph:
         self.gather_bytes = W * (self.cw + emax) * 4
         if hasattr(comm, "bind_payloads"):   # (an emulated group: it builds the peers' payloads the same way)
             comm.bind_payloads(self._col_payload, self._val_payload)
+        # B read in place from the gathered panels by the layout passes when the plan's kernels
+        # read B only through its padded layouts (the 1M config): no unpack passes, and B's
+        # column / value arrays are never formed
+        self.gview = None
+        if SG.bitmap_gathered_ok(plan):
+            P = SG._native.ptr
+            self.rbase = torch.tensor([0] + list(itertools.accumulate(ms)), dtype=torch.int64, device=dev)
+            mk = lambda gv: SG.BmGathered(gc=P(self.gc), gv=gv, ebase=P(self.base), rbase=P(self.rbase),  # noqa: E731
+                                          cstride=self.cw, vstride=emax, W=W, bits=self.bits)
+            self.gview = (mk(None), mk(P(self.gv)))   # (front: columns only; back: columns and values)
+            self.B = CSR(m, B_panel.n, rowptr, torch.zeros(0, dtype=torch.int32, device=dev),
+                         torch.zeros(0, dtype=torch.float32, device=dev))
         # ---- one eager step (checks every launch and the kernels' error bits:
         # a product the row kernels cannot take, or with units beyond the reload
         # kernel, is not replayed), then the capture ---------------------------
@@ -425,12 +443,18 @@ class RowblockGraph:
     def _front(self) -> None:
         from ..ops import spgemm as SG
 
+        if self.gview is not None:
+            self.built = SG.bitmap_front(self.A, self.B, self.plan, self.bufs, values=False, gathered=self.gview[0])
+            return
         self._unpack(self.gc, None)
         self.built = SG.bitmap_front(self.A, self.B, self.plan, self.bufs, values=False)
 
     def _back(self) -> None:
         from ..ops import spgemm as SG
 
+        if self.gview is not None:
+            SG.bitmap_back(self.A, self.B, self.plan, self.bufs, self.built, gathered=self.gview[1])
+            return
         self._unpack(None, self.gv)
         SG.bitmap_back(self.A, self.B, self.plan, self.bufs, self.built)
 

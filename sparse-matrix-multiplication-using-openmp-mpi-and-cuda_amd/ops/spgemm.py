@@ -67,8 +67,8 @@ _native.register_hip("spmm_spgemm_bm_count_rows", C_INT, c_vp, c_vp, c_vp, c_vp,
 _native.register_hip("spmm_spgemm_bm_numeric_rows", C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
                      C_INT, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp, C_I64, c_vp, C_INT, C_INT, C_I64, C_INT, C_I64, c_vp)
 _native.register_hip("spmm_spgemm_bm_pad_pairs", c_vp, c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp,
-                     C_I64, C_I64, c_vp, c_vp)
-_native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp)
+                     C_I64, C_I64, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_splits", c_vp, c_vp, C_I64, C_INT, C_INT, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_unpack_gathered", c_vp, c_vp, C_INT, C_I64, C_I64, C_INT, c_vp, C_I64, c_vp,
                      c_vp, c_vp, c_vp)
 _native.register_hip("spmm_pack_bits", c_vp, C_I64, C_INT, c_vp, C_I64, c_vp)
@@ -721,9 +721,19 @@ class _BmPlan(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmPlan
 _native.register_hip("spmm_spgemm_bm_choose", c_vp, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64)
 _native.register_hip("spmm_spgemm_bm_make_plan", c_vp, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64, C_I64,
                      C.c_double, c_vp)
-_native.register_hip("spmm_spgemm_bm_front", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_front", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_bm_back", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_INT, c_vp, c_vp, c_vp, C_I64,
-                     c_vp, c_vp, c_vp)
+                     c_vp, c_vp, c_vp, c_vp)
+_native.register_hip("spmm_spgemm_bm_gathered_ok", c_vp)
+
+
+class BmGathered(C.Structure):   # csrc/kernels/bitmap_plan.hpp SpmmBmGathered
+    """B read in place from its all-gathered panels by the layout kernels
+    (models.spgemm.RowblockGraph): panel r's columns at gc + r * cstride
+    (packed to ``bits`` < 32, or raw), its value bits at gv + r * vstride;
+    ebase / rbase: device int64 [W + 1] entry / row bounds of the panels."""
+    _fields_ = [("gc", c_vp), ("gv", c_vp), ("ebase", c_vp), ("rbase", c_vp), ("cstride", C.c_int64),
+                ("vstride", C.c_int64), ("W", C.c_int32), ("bits", C.c_int32)]
 
 
 def _bm_opts(use_ws8: bool = True) -> _BmOpts:
@@ -798,27 +808,40 @@ def bitmap_buffers(plan: BitmapPlan, dev: torch.device, cap: Optional[int] = Non
     return out
 
 
-def bitmap_front(A: CSR, B: CSR, plan: BitmapPlan, bufs: dict, values: bool) -> int:
+def bitmap_gathered_ok(plan: BitmapPlan) -> bool:
+    """Whether the plan's kernels read B only through its padded layouts, so
+    the layout passes may read B in place from gathered panels (BmGathered)."""
+    return bool(_native.hip().spmm_spgemm_bm_gathered_ok(C.byref(plan.raw)))
+
+
+def bitmap_front(A: CSR, B: CSR, plan: BitmapPlan, bufs: dict, values: bool, gathered=None) -> int:
     """B layouts + count kernel + unit-offset scan (csr_bitmap_plan.hip front)
     on the current stream; ``values``: B's values are readable (else only its
     columns: the padded pairs are then built by :func:`bitmap_back`).
-    Returns whether the padded pairs were built."""
+    ``gathered``: a :class:`BmGathered` view B's layouts are read from (B's own
+    column / value arrays are then not read).  Returns whether the padded
+    pairs were built."""
     P = _native.ptr
     built = C.c_int(0)
+    use_vals = values and gathered is None
     _native.check(_native.hip().spmm_spgemm_bm_front(
-        C.byref(plan.raw), P(A.rowptr), P(A.col), P(B.rowptr), P(B.col), P(B.val) if values else None,
-        P(bufs["ws"]), P(bufs["uoff"]), P(bufs["z"]), C.byref(built), _native.stream_ptr(A.device)),
+        C.byref(plan.raw), P(A.rowptr), P(A.col), P(B.rowptr), None if gathered is not None else P(B.col),
+        P(B.val) if use_vals else None, P(bufs["ws"]), P(bufs["uoff"]), P(bufs["z"]), C.byref(built),
+        C.byref(gathered) if gathered is not None else None, _native.stream_ptr(A.device)),
         "spgemm_bm_front")
     return built.value
 
 
-def bitmap_back(A: CSR, B: CSR, plan: BitmapPlan, bufs: dict, built: int) -> None:
+def bitmap_back(A: CSR, B: CSR, plan: BitmapPlan, bufs: dict, built: int, gathered=None) -> None:
     """Padded pairs (unless built by the front) + numeric and reload kernels
-    into ``bufs["Cci"] / ["Cv"]`` (csr_bitmap_plan.hip back)."""
+    into ``bufs["Cci"] / ["Cv"]`` (csr_bitmap_plan.hip back); ``gathered``: as
+    :func:`bitmap_front`."""
     P = _native.ptr
+    g = gathered is not None
     _native.check(_native.hip().spmm_spgemm_bm_back(
-        C.byref(plan.raw), P(A.rowptr), P(A.col), P(A.val), P(B.col), P(B.val), built, P(bufs["ws"]),
-        P(bufs["uoff"]), P(bufs["z"]), bufs["cap"], P(bufs["Cci"]), P(bufs["Cv"]), _native.stream_ptr(A.device)),
+        C.byref(plan.raw), P(A.rowptr), P(A.col), P(A.val), None if g else P(B.col), None if g else P(B.val), built,
+        P(bufs["ws"]), P(bufs["uoff"]), P(bufs["z"]), bufs["cap"], P(bufs["Cci"]), P(bufs["Cv"]),
+        C.byref(gathered) if g else None, _native.stream_ptr(A.device)),
         "spgemm_bm_back")
 
 

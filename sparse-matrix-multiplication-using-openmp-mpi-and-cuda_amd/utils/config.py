@@ -47,7 +47,8 @@ class Config:
     # row-major numeric kernel of the bitmap path (a row's windows back to back, <= 8 windows):
     # "auto" = for the widest-window configurations (0, 3), "on", "off" (per-unit kernel)
     spgemm_bitmap_rows: str = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_ROWS", "auto", str))
-    # row-major numeric kernel reads an interleaved (column, value) copy of B (1) or the two arrays (0)
+    # B's (column, value) pairs for the numeric kernels (1), or the two arrays (0: per-unit kernels
+    # only -- the row kernel reads the padded pairs)
     spgemm_bitmap_cv: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_CV", 1, int))
     # ... with every (row, window) segment of those pairs starting on a 128-byte line (1) or packed (0)
     spgemm_bitmap_pad: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_PAD", 1, int))
@@ -55,8 +56,8 @@ class Config:
     # engine) on the bitmap-rank path: 0 = off, 1 = on (other GPU paths stay unordered), 2 = strict
     # (a product no deterministic GPU kernel covers runs on the CPU engine)
     # row-major bitmap numeric and count kernels: software-pipelined (the next unit's B gathers
-    # issued before this unit's write-out / popcount, buffer-descriptor addressing) = 1, flat
-    # kernels = 0 (PERF_LOG round 5)
+    # issued before this unit's write-out / popcount, buffer-descriptor addressing) = 1; 0 = the
+    # per-unit numeric kernel and the flat row count kernel (PERF_LOG rounds 5-6)
     spgemm_bitmap_pipe: int = field(default_factory=lambda: _env("SPMM_SPGEMM_BITMAP_PIPE", 1, int))
     spgemm_deterministic: int = field(default_factory=lambda: _env("SPMM_SPGEMM_DETERMINISTIC", 0, int))
     spgemm_global_ws_gb: float = field(default_factory=lambda: _env("SPMM_GLOBAL_WS_GB", 8.0, float))

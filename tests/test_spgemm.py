@@ -612,14 +612,15 @@ def test_spgemm_gpu_bitmap_count_units(monkeypatch, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows,pad,pipe", [("on", 1, 1), ("on", 0, 1), ("on", 1, 0), ("off", 1, 1)])
-def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows, pad, pipe):
+@pytest.mark.parametrize("rows,pad,pipe,cv", [("on", 1, 1, 1), ("on", 0, 1, 1), ("on", 1, 0, 1), ("off", 1, 1, 1),
+                                          ("on", 1, 1, 0)])
+def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows, pad, pipe, cv):
     """The two numeric paths of the widest-window configuration on a product
     with 5 windows per row (ragged last window): the pipelined row kernels
     (B's pairs with every window segment padded to a 128-byte line) and the
     per-unit kernels, which take every product the row kernels cannot (no
-    padded layout, SPMM_SPGEMM_BITMAP_PIPE=0, rows off); all equal the
-    binned path."""
+    padded layout, SPMM_SPGEMM_BITMAP_PIPE=0, no (column, value) pairs, rows
+    off); all equal the binned path."""
     from spmm_amd.utils.config import CONFIG
 
     dev = torch.device("cuda")
@@ -628,8 +629,9 @@ def test_spgemm_gpu_bitmap_row_kernels(monkeypatch, rows, pad, pipe):
     monkeypatch.setattr(CONFIG, "spgemm_bitmap_rows", rows)
     monkeypatch.setattr(CONFIG, "spgemm_bitmap_pad", pad)
     monkeypatch.setattr(CONFIG, "spgemm_bitmap_pipe", pipe)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap_cv", cv)
     info = _bitmap_vs_binned(monkeypatch, A, B, 0)
-    assert info.rows_per_bin_num.get("bitmap_rows", 0) == (1 if (rows, pad, pipe) == ("on", 1, 1) else 0)
+    assert info.rows_per_bin_num.get("bitmap_rows", 0) == (1 if (rows, pad, pipe, cv) == ("on", 1, 1, 1) else 0)
 
 
 @pytest.mark.gpu
