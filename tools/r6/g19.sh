@@ -3,7 +3,7 @@
 # rank 0 of 8 emulation, kernel stats of the 1M and 64k graph steps
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/r6g19; mkdir -p $O
+O=$R/gpurun_out/${OUT:-r6g19}; mkdir -p $O
 cd $R
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 echo "gpu suite: $(tail -1 $O/pytest_gpu.log)"
