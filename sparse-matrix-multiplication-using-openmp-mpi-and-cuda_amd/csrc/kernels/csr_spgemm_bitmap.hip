@@ -277,6 +277,7 @@ struct BmArgs {
                            // bit 1: count / numeric disagree (kernel invariant)
                            // bit 2: deferred list full (host falls back)
   const uint4* ws8 = nullptr;   // per-unit WIDE numeric: packed window bounds + padded pair bases
+  int32_t chunk = 0;            // numeric: 0 = persistent grid, else `chunk` consecutive units a workgroup
 };
 
 // CV: B read as interleaved (column, value bits) pairs (p.Bcv): one 8-byte load
@@ -356,6 +357,11 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   // workgroup g takes unit k * gridDim + perm(g), perm putting consecutive
   // units (the windows of one row: same A row, neighbouring B lines) on one
   // XCD (blocks b and b + 8 share one; speed only).  Reload: the deferred list.
+  // Chunked numeric (p.chunk > 0): workgroup g takes units g * chunk .. + chunk
+  // and exits, and the grid is ~16x the resident slots, so the dispatcher
+  // hands the freed slots new workgroups: the workgroups of a CU are served
+  // unequally, and a persistent grid's fixed share leaves a 16 % tail
+  // (65536^2, PERF_LOG round 6).
   const int64_t nsw = MODE == 0 ? (nwin + NSUB - 1) / NSUB : nwin;   // units per row
   int64_t nunits = MODE == 2 ? (int64_t)__hip_atomic_load(p.novf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                              : p.m * nsw;
@@ -363,6 +369,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
   const int64_t NG = gridDim.x;
   const int64_t me = (MODE != 2 && NG % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (NG / 8) + blockIdx.x / 8
                                                 : (int64_t)blockIdx.x;
+  const int64_t CU = MODE == 1 ? p.chunk : 0;
+  const int64_t SU = CU > 0 ? 1 : NG;   // unit stride of this workgroup's sequence
+  const int64_t u_first = CU > 0 ? (int64_t)blockIdx.x * CU : me;
+  const int64_t u_lim = CU > 0 ? min(nunits, u_first + CU) : nunits;
 
   // ---- software pipeline over this workgroup's units ----------------------
   // Three units ahead, every load issued unconditionally at the top of an
@@ -375,26 +385,26 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
     int slot, u, row, qi;   // qi: unit index inside its row
   };
   auto first_head = [&](int64_t slot) {
-    Head h{(int)(slot < nunits ? slot : nunits), 0, 0, 0};
-    if (slot < nunits) {
+    Head h{(int)(slot < u_lim ? slot : u_lim), 0, 0, 0};
+    if (slot < u_lim) {
       h.u = MODE == 2 ? p.ovf[slot] : (int)slot;
       h.row = (int)(h.u / nsw);
       h.qi = (int)(h.u - (int64_t)h.row * nsw);
     }
     return h;
   };
-  const int step_q = (int)(NG % nsw), step_row = (int)(NG / nsw);
+  const int step_q = (int)(SU % nsw), step_row = (int)(SU / nsw);
   auto next_head = [&](const Head& h) {
     if constexpr (MODE == 2) {
       return first_head((int64_t)h.slot + NG);
     } else {
       Head n{h.slot, h.u, h.row, h.qi};
-      if ((int64_t)h.slot + NG >= nunits) {
-        n.slot = (int)nunits;
+      if ((int64_t)h.slot + SU >= u_lim) {
+        n.slot = (int)u_lim;
         return n;
       }
-      n.slot = (int)(h.slot + NG);
-      n.u = (int)(h.u + NG);
+      n.slot = (int)(h.slot + SU);
+      n.u = (int)(h.u + SU);
       n.row = h.row + step_row;
       n.qi = h.qi + step_q;
       if (n.qi >= nsw) {
@@ -404,10 +414,10 @@ __global__ __launch_bounds__(NT, 4) void spgemm_bm(BmArgs p) {
       return n;
     }
   };
-  auto live = [&](const Head& h) { return (int64_t)h.slot < nunits; };
+  auto live = [&](const Head& h) { return (int64_t)h.slot < u_lim; };
   auto q0_of = [&](const Head& h) { return h.qi * (MODE == 0 ? NSUB : 1); };
   auto q1_of = [&](const Head& h) { return MODE == 0 ? min(h.qi * NSUB + NSUB, nwin) : h.qi + 1; };
-  Head h0 = first_head(me);
+  Head h0 = first_head(u_first);
   Head h1 = next_head(h0), h2 = next_head(h1), h3 = next_head(h2);
   // row start / length of A (vector registers; nnz(A) < 2^31, checked by the host)
   int ra0 = 0, rb0 = 0, ra1 = 0, rb1 = 0, ra2 = 0, rb2 = 0, ra3 = 0, rb3 = 0;
@@ -1462,7 +1472,12 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   const int NG = (int)gridDim.x;
   const int me = (NG % 8 == 0) ? (int)(blockIdx.x % 8) * (NG / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
   const int m = (int)p.m;
-  int row = me;
+  // chunked grid (ra.a.chunk > 0): rows b * chunk .. + chunk a workgroup, as the per-unit
+  // numeric kernel's chunked schedule; else persistent (me, me + NG, ...)
+  const int CR = ra.a.chunk;
+  const int S = CR > 0 ? 1 : NG;
+  int row = CR > 0 ? (int)blockIdx.x * CR : me;
+  const int lim = CR > 0 ? min(m, row + CR) : m;
   int cna = 0;
   uint4 cwa = make_uint4(0, 0, 0, 0);
   uint32_t cwb = 0;
@@ -1502,21 +1517,21 @@ __global__ __launch_bounds__(NT, SPMM_BM_COUNT_WPS) void spgemm_bm_rows_count(Bm
   ld_arp(row, n1a, n1b);
   ld_entries(row);
   ld_bounds(row);
-  ld_arp(row + NG, n2a, n2b);
+  ld_arp(row + S, n2a, n2b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   take_next();
   __syncthreads();
 
-  for (; row < m; row += NG) {
+  for (; row < lim; row += S) {
     const int na = cna;
     uint32_t bq = cwa.x;
     for (int q = 0; q < nwin; q += NSUB) {   // a unit: windows [q, q + NSUB) of the row
       const bool last = q + NSUB >= nwin;
       if (q == 0) {
-        ld_entries(row + NG);
-        ld_arp(row + 2 * NG, n2a, n2b);
+        ld_entries(row + S);
+        ld_arp(row + 2 * S, n2a, n2b);
       }
-      if (last) ld_bounds(row + NG);
+      if (last) ld_bounds(row + S);
       const uint32_t wl = q < 2 ? cwa.y : q < 4 ? cwa.z : q < 6 ? cwa.w : cwb;
       int len = 0, nch = 0;
       if (tid < na && tid < NT) {
@@ -2026,6 +2041,14 @@ template <typename Kern>
 int launch_rows(Kern kernel, const BmRowArgs& ra, hipStream_t s, int nt = kFastNT) {
   return launch_rows(kernel, ra, ra.a.m, s, nt);
 }
+// a grid of exactly g workgroups (chunked schedules)
+template <typename Kern>
+int launch_rows_grid(Kern kernel, const BmRowArgs& ra, int64_t g, hipStream_t s, int nt) {
+  if (g < 1 || g > (int64_t)INT32_MAX) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(nt), 0, s, ra);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
 
 // count: one window (16 KB at W = 2^17, 8 workgroups per CU) or two windows
 // per unit (32 KB, 4 per CU: a B row's column segment read once for both)
@@ -2052,6 +2075,10 @@ struct BmRowCountPipe {
   static constexpr auto k = spgemm_bm_rows_count_pipe<kCfgs[C].lgw, NT, SPMM_BM_COUNT_RR / 2, 768>;
 };
 
+#ifndef SPMM_BM_ROWCOUNT_CHUNK   // flat row count kernel: rows a workgroup (0: persistent grid)
+#define SPMM_BM_ROWCOUNT_CHUNK 4
+#endif
+
 template <int C>
 int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s) {
   using K1 = BmRowCountKernel<C, 1>;
@@ -2063,6 +2090,14 @@ int bm_count_rows(BmRowArgs ra, int nsub, int pipe, int64_t annz, hipStream_t s)
       colp_bytes < (int64_t(1) << 32) && ra.a.m * ra.a.nwin < (int64_t(1) << 30))
     return launch_rows(BmRowCountPipe<C>::k, BmCountPipeArgs{ra, (uint32_t)colp_bytes, annz}, ra.a.m, s,
                        BmRowCountPipe<C>::NT);
+  constexpr int CR = SPMM_BM_ROWCOUNT_CHUNK;
+  if (CR > 0) {   // chunked grid: CR rows a workgroup (spgemm_bm_rows_count)
+    ra.a.chunk = CR;
+    const int64_t g = (ra.a.m + CR - 1) / CR;
+    if (ra.pad)
+      return nsub == 2 ? launch_rows_grid(K2::kp, ra, g, s, K2::NT) : launch_rows_grid(K1::kp, ra, g, s, K1::NT);
+    return nsub == 2 ? launch_rows_grid(K2::k, ra, g, s, K2::NT) : launch_rows_grid(K1::k, ra, g, s, K1::NT);
+  }
   if (ra.pad)
     return nsub == 2 ? launch_rows(K2::kp, ra, s, K2::NT) : launch_rows(K1::kp, ra, s, K1::NT);
   return nsub == 2 ? launch_rows(K2::k, ra, s, K2::NT) : launch_rows(K1::k, ra, s, K1::NT);
@@ -2083,12 +2118,30 @@ int bm_numeric_rows(BmRowArgs ra, int det, int64_t nbcv, int pipe, int64_t annz,
   return launch_bm(BmKernels<C>::reload_wide, BmKernels<C>::kReloadNT, int64_t(1) << 30, ar, s);
 }
 
+#ifndef SPMM_BM_UNIT_CHUNK   // per-unit fast numeric: units a workgroup (0: persistent grid)
+#define SPMM_BM_UNIT_CHUNK 8
+#endif
+
+// the fast numeric kernel on a grid of `chunk`-unit workgroups (see spgemm_bm's unit schedule)
+template <typename K>
+int launch_bm_chunked(K kernel, int nt, int64_t work, BmArgs a, int chunk, hipStream_t s) {
+  const int64_t g = (work + chunk - 1) / chunk;
+  if (g > (int64_t)INT32_MAX) return (int)hipErrorInvalidValue;
+  a.chunk = chunk;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)(g < 1 ? 1 : g)), dim3(nt), 0, s, a);
+  SPMM_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int C>
 int bm_numeric(int64_t work, const BmArgs& a, int det, hipStream_t s) {
   using K = BmKernels<C>;
   const bool wide = K::kWide && a.ws8 != nullptr && a.Bcv != nullptr && a.lg >= 1;   // padded pairs given
+  constexpr int CH = SPMM_BM_UNIT_CHUNK;
   const int rc = det ? launch_bm(K::fast_det, kFastNT, work, a, s)
-                     : (wide ? launch_bm(K::fast_wide, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s));
+               : CH > 0 ? (wide ? launch_bm_chunked(K::fast_wide, kFastNT, work, a, CH, s)
+                                : launch_bm_chunked(K::fast, kFastNT, work, a, CH, s))
+                        : (wide ? launch_bm(K::fast_wide, kFastNT, work, a, s) : launch_bm(K::fast, kFastNT, work, a, s));
   if (rc) return rc;
   return det ? launch_bm(K::reload_det, K::kReloadNT, int64_t(1) << 30, a, s)
              : launch_bm(K::reload, K::kReloadNT, int64_t(1) << 30, a, s);
