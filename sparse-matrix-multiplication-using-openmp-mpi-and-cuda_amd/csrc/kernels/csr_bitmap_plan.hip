@@ -163,7 +163,8 @@ SPMM_EXPORT int spmm_spgemm_bm_make_plan(const SpmmBmOpts* o, int64_t m, int64_t
   const int64_t cap_bcv = bnnz + (kPadPairs - 1) * (int64_t)nwin * mb;
   const int64_t cap_colp = bnnz + (kPadCols - 1) * ngc * mb;
   p->count_rows = ws8_ok && amax >= 0 && amax <= 256;
-  p->rows = ws8_ok && (o->rows_mode == 2 || cfg == 0) && pad && o->cv != 0 && !p->det && p->pipe && annz > 0 &&
+  // (cfg 2 keeps the per-unit kernels unless forced: not measured on the row kernel)
+  p->rows = ws8_ok && (o->rows_mode == 2 || cfg <= 1) && pad && o->cv != 0 && !p->det && p->pipe && annz > 0 &&
             cap_bcv * 8 < ((int64_t)1 << 32);
   p->m = m;
   p->annz = annz;
@@ -209,6 +210,18 @@ SPMM_EXPORT int spmm_spgemm_bm_gathered_ok(const SpmmBmPlan* p) {
          p->nwin >= 2;
 }
 
+// The front's reset of z (int32[4]) and uoff[0], as a kernel: a 16-byte hipMemsetAsync captured
+// into the row-block step's first graph wrote device-address-like garbage into z on replay
+// (ROCm 7.x; tools/r6/diag_rows_graph4.py): deferred count and row ticket garbage, so the
+// numeric kernel took rows past the matrix.  Vector stores, one lane each.
+namespace {
+__global__ __launch_bounds__(64) void bm_front_reset(int32_t* __restrict__ z, int64_t* __restrict__ uoff) {
+  const int t = threadIdx.x;
+  if (t < 4) z[t] = 0;
+  if (t == 4) uoff[t - 4] = 0;
+}
+}  // namespace
+
 #define BM_TRY(x)               \
   do {                          \
     const int _rc = (x);        \
@@ -229,8 +242,8 @@ SPMM_EXPORT int spmm_spgemm_bm_front(const SpmmBmPlan* p, const int64_t* Arp, co
   *pairs_built = 0;
   const bool gath = g != nullptr && g->gc != nullptr;
   if (gath && !spmm_spgemm_bm_gathered_ok(p)) return (int)hipErrorInvalidValue;
-  if (hipMemsetAsync(z, 0, 16, s) != hipSuccess || hipMemsetAsync(uoff, 0, 8, s) != hipSuccess)
-    return (int)hipErrorUnknown;
+  hipLaunchKernelGGL(bm_front_reset, dim3(1), dim3(64), 0, s, z, uoff);
+  if (hipGetLastError() != hipSuccess) return (int)hipErrorUnknown;
   uint32_t* split = at<uint32_t>(ws, p->o_split);
   int32_t* ucnt = at<int32_t>(ws, p->o_ucnt);
   void* ws8 = at<void>(ws, p->o_ws8);

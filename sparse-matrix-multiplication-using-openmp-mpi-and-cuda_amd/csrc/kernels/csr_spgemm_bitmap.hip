@@ -972,8 +972,8 @@ struct BmPipeArgs {
 };
 
 
-template <int LGW, int NT, int PCAP, int R, int CCAP>
-__global__ __launch_bounds__(NT, 4) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
+template <int LGW, int NT, int PCAP, int R, int CCAP, int WPE = 4>
+__global__ __launch_bounds__(NT, WPE) void spgemm_bm_rows_pipe(BmPipeArgs pa) {
   const BmRowArgs& ra = pa.r;
   const BmArgs& p = ra.a;
   constexpr int NW = NT / 64;
@@ -1960,8 +1960,18 @@ struct BmCfg {
 #ifndef SPMM_BM_CFG1_R   // register rounds of cfg 1's per-unit fast kernel (the 65536^2 config)
 #define SPMM_BM_CFG1_R 14   // 65536^2: 16 rounds spill 5 VGPRs; 14 = 1.64 -> 1.56 ms (384 of 131072 units deferred), 13: 1.61-1.67, 12: 1.82
 #endif
+// cfg 1's pipelined row kernel (65536^2): the per-unit kernel's 14 rounds, so its units fit as
+// they did there (at 10 rounds 74k of 131k units were deferred: 3.45 ms a step); 14 rounds and
+// four 4096-entry write-out rounds need 158 VGPRs, so 3 waves per SIMD (at 4: 49 spill ops).
+// 65536^2 step 1.202-1.205 vs 1.250-1.253 ms on the per-unit kernel (12 rounds: 1.56; r6g27)
+#ifndef SPMM_BM_CFG1_ROWS_R
+#define SPMM_BM_CFG1_ROWS_R 14
+#endif
+#ifndef SPMM_BM_CFG1_ROWS_WPE
+#define SPMM_BM_CFG1_ROWS_WPE 3
+#endif
 constexpr BmCfg kCfgs[] = {{17, 8, 2048, 12, 256, SPMM_BM_ROWS_R},
-                           {15, 2, 3840, SPMM_BM_CFG1_R, 256, SPMM_BM_ROWS_R},
+                           {15, 2, 3840, SPMM_BM_CFG1_R, 256, SPMM_BM_CFG1_ROWS_R},
                            {16, 4, 3072, 16, 256, SPMM_BM_ROWS_R}};
 constexpr int kNumCfgs = 3;
 constexpr int kFastNT = 256, kReloadCcap = 2048;
@@ -2021,7 +2031,7 @@ struct BmRowKernel {
   // register rounds (the row pipeline's registers cost rounds)
   static constexpr int R = K.rounds_fast > K.rows_r ? K.rows_r : K.rounds_fast;
   static constexpr int RP = R & ~1;   // the pipelined kernel loads two pairs per lane and round
-  static constexpr auto kpipe = spgemm_bm_rows_pipe<K.lgw, NT, K.pcap_fast, RP, RP * (NT / 16)>;
+  static constexpr auto kpipe = spgemm_bm_rows_pipe<K.lgw, NT, K.pcap_fast, RP, RP * (NT / 16), C == 1 ? SPMM_BM_CFG1_ROWS_WPE : 4>;
 };
 
 

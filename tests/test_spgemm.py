@@ -349,17 +349,24 @@ def test_rowblock_spgemm_rccl_one_rank(monkeypatch):
         # unpacked first for the count kernel, values + pairs before the numeric)
         assert "bitmap_units" in info.rows_per_bin_num
         # the host-sync-free step: RCCL gathers between two captured graphs,
-        # replayed after in-place value changes of both operands
-        g = MS.RowblockGraph(prob.A, prob.B, comm)
-        va, vb = prob.A.val.clone(), prob.B.val.clone()
-        for s in (1.0, -0.5, 2.0):
-            prob.A.val.copy_(va * s)
-            prob.B.val.copy_(vb * (s + 1.0))
-            g.run()
-            C1 = g.result()
-            C2 = SG.spgemm(prob.A, prob.B)
-            assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
-            assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5)
+        # replayed after in-place value changes of both operands; cfg 1 and cfg 0 on
+        # the row kernel with more rows than its static schedule (row tickets: the
+        # first graph's reset of the ticket / deferred words must hold on replay)
+        for n, d in ((65536, 1e-3), (262144, 1e-4)):
+            prob = MS.UniformProblem.build(n, d, comm, seed=7)
+            g = MS.RowblockGraph(prob.A, prob.B, comm)
+            assert g.gview is not None and g.plan.raw.rows
+            va, vb = prob.A.val.clone(), prob.B.val.clone()
+            for s in (1.0, -0.5, 2.0):
+                prob.A.val.copy_(va * s)
+                prob.B.val.copy_(vb * (s + 1.0))
+                g.run()
+                C1 = g.result()
+                C2 = SG.spgemm(prob.A, prob.B)
+                assert torch.equal(C1.rowptr, C2.rowptr) and torch.equal(C1.col, C2.col)
+                assert torch.allclose(C1.val, C2.val, atol=1e-5, rtol=1e-5), (n, s)
+            torch.cuda.synchronize()
+            del g
     finally:
         comm.close()
 
