@@ -1963,7 +1963,8 @@ struct BmCfg {
 // cfg 1's pipelined row kernel (65536^2): the per-unit kernel's 14 rounds, so its units fit as
 // they did there (at 10 rounds 74k of 131k units were deferred: 3.45 ms a step); 14 rounds and
 // four 4096-entry write-out rounds need 158 VGPRs, so 3 waves per SIMD (at 4: 49 spill ops).
-// 65536^2 step 1.202-1.205 vs 1.250-1.253 ms on the per-unit kernel (12 rounds: 1.56; r6g27)
+// 65536^2 step 1.202-1.205 vs 1.250-1.253 ms on the per-unit kernel (12 rounds: 1.56; r6g27;
+// 512 threads at 8 / 10 rounds, 4 waves per SIMD: 1.40 / 1.46, r6g35)
 #ifndef SPMM_BM_CFG1_ROWS_R
 #define SPMM_BM_CFG1_ROWS_R 14
 #endif
