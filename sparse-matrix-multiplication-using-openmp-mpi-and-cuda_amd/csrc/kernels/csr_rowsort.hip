@@ -15,6 +15,8 @@
 //   rs_unpack    keys back into the row
 #include "common.hpp"
 
+#include <algorithm>
+
 extern "C" {
 int spmm_prim_scan(const void* in, int in_bytes, int64_t n, int64_t* out, int inclusive, void* ws, void* stream);
 size_t spmm_prim_scan_ws(int64_t n);
@@ -29,9 +31,11 @@ constexpr int kRsLds = 16384;   // 128 KB of LDS
 constexpr int kRsNt = 1024;
 
 __global__ __launch_bounds__(256) void rs_lens(const int64_t* __restrict__ rp, const int64_t* __restrict__ rows,
-                                               int64_t nrows, int64_t* __restrict__ len) {
+                                               int64_t nrows, int64_t* __restrict__ len,
+                                               unsigned long long* __restrict__ cnt) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i < nrows) len[i] = rp[rows[i] + 1] - rp[rows[i]];
+  if (i == 0) cnt[i] = 0;
 }
 
 // radix: key = (i << 31) | column, value = value bits; otherwise key = column << 32 | bits
@@ -102,32 +106,57 @@ __global__ __launch_bounds__(256) void rs_sort_wave(const int64_t* __restrict__ 
   if (lane < len) key[s + lane] = x;
 }
 
-__global__ __launch_bounds__(kRsNt) void rs_sort_lds(const int64_t* __restrict__ toff, uint64_t* __restrict__ key) {
+// the listed rows of 65..kRsLds entries, appended to mid[0 .. *cnt) (any order; *cnt zeroed by rs_lens)
+__global__ __launch_bounds__(256) void rs_select_mid(const int64_t* __restrict__ toff, int64_t nrows,
+                                                     int32_t* __restrict__ mid, unsigned long long* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t len = 0;
+  if (i < nrows) len = toff[i + 1] - toff[i];
+  const bool hit = len > 64 && len <= kRsLds;
+  const unsigned long long b = __ballot(hit);
+  if (!b) return;
+  const int lane = threadIdx.x & 63, first = __ffsll((long long)b) - 1;
+  unsigned long long base = 0;
+  if (lane == first) base = atomicAdd(cnt, (unsigned long long)__popcll(b));
+  base = __shfl(base, first);
+  if (hit) mid[base + __popcll(b & ((1ull << lane) - 1ull))] = (int32_t)i;
+}
+
+// One 1024-thread workgroup per row of mid (a grid of at most one workgroup per CU looping over
+// the list: the 128 KB of LDS admits one per CU, so a workgroup per listed row -- most of them
+// short -- spent a slot on every row just to exit)
+__global__ __launch_bounds__(kRsNt) void rs_sort_lds(const int64_t* __restrict__ toff, const int32_t* __restrict__ mid,
+                                                     const unsigned long long* __restrict__ cnt,
+                                                     uint64_t* __restrict__ key) {
   __shared__ uint64_t sh[kRsLds];
   const int tid = threadIdx.x;
-  const int64_t s = toff[blockIdx.x];
-  const int len = (int)(toff[blockIdx.x + 1] - s);
-  if (len <= 64 || len > kRsLds) return;   // (workgroup-uniform)
-  int n = 128;
-  while (n < len) n <<= 1;
-  for (int i = tid; i < n; i += kRsNt) sh[i] = i < len ? key[s + i] : ~0ull;
-  __syncthreads();
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < n; i += kRsNt) {
-        const int p = i ^ j;
-        if (p > i) {
-          const uint64_t a = sh[i], b = sh[p];
-          if ((a > b) == ((i & k) == 0)) {
-            sh[i] = b;
-            sh[p] = a;
+  const int64_t nmid = (int64_t)*cnt;
+  for (int64_t r = blockIdx.x; r < nmid; r += gridDim.x) {
+    const int64_t row = mid[r];
+    const int64_t s = toff[row];
+    const int len = (int)(toff[row + 1] - s);
+    int n = 128;
+    while (n < len) n <<= 1;
+    for (int i = tid; i < n; i += kRsNt) sh[i] = i < len ? key[s + i] : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= n; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < n; i += kRsNt) {
+          const int p = i ^ j;
+          if (p > i) {
+            const uint64_t a = sh[i], b = sh[p];
+            if ((a > b) == ((i & k) == 0)) {
+              sh[i] = b;
+              sh[p] = a;
+            }
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
+    for (int i = tid; i < len; i += kRsNt) key[s + i] = sh[i];
+    __syncthreads();   // the row's LDS reads done before the next row's loads
   }
-  for (int i = tid; i < len; i += kRsNt) key[s + i] = sh[i];
 }
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -228,7 +257,7 @@ SPMM_EXPORT int spmm_rows_with_flag(const int32_t* flags, int64_t m, int mask, i
 // Workspace bytes of spmm_csr_sort_rows for nrows listed rows holding total entries.
 SPMM_EXPORT size_t spmm_csr_sort_rows_ws(int64_t nrows, int64_t total, int64_t maxlen) {
   size_t b = align256((size_t)(nrows + 1) * 8) * 2 + align256(spmm_prim_scan_ws(nrows + 1)) +
-             align256((size_t)total * 8);
+             align256((size_t)total * 8) + align256((size_t)nrows * 4) + 256;
   if (maxlen > kRsLds) b += align256((size_t)total * 8) + align256(spmm_prim_sort_ws(total));
   return b;
 }
@@ -250,8 +279,12 @@ SPMM_EXPORT int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64
   p += align256(spmm_prim_scan_ws(nrows + 1));
   uint64_t* key = (uint64_t*)p;
   p += align256((size_t)total * 8);
+  int32_t* mid = (int32_t*)p;   // rows for the LDS sort, and their count
+  p += align256((size_t)nrows * 4);
+  unsigned long long* nmid = (unsigned long long*)p;
+  p += 256;
   const bool radix = maxlen > kRsLds;
-  hipLaunchKernelGGL(rs_lens, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, rp, rows, nrows, len);
+  hipLaunchKernelGGL(rs_lens, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, rp, rows, nrows, len, nmid);
   SPMM_LAUNCH_CHECK();
   (void)hipMemsetAsync(len + nrows, 0, 8, s);
   int rc = spmm_prim_scan(len, 8, nrows + 1, toff, 0, scan_ws, s);   // exclusive: toff[nrows] = total
@@ -274,7 +307,14 @@ SPMM_EXPORT int spmm_csr_sort_rows(const int64_t* rp, const int64_t* rows, int64
     hipLaunchKernelGGL(rs_sort_wave, gw, dim3(256), 0, s, toff, nrows, key);
     SPMM_LAUNCH_CHECK();
     if (maxlen > 64) {
-      hipLaunchKernelGGL(rs_sort_lds, dim3((unsigned)nrows), dim3(kRsNt), 0, s, toff, key);
+      hipLaunchKernelGGL(rs_select_mid, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, toff, nrows, mid, nmid);
+      SPMM_LAUNCH_CHECK();
+      int dev = 0, ncu = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+      hipLaunchKernelGGL(rs_sort_lds, dim3((unsigned)std::min<int64_t>(nrows, ncu)), dim3(kRsNt), 0, s, toff, mid,
+                         nmid, key);
       SPMM_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(rs_unpack<false>, gw, dim3(256), 0, s, rp, rows, nrows, toff, key, nullptr, ci, (uint32_t*)v);
