@@ -167,8 +167,8 @@ def run_rmat(comm, args):
     if stream:
         nnz = [0]
 
-        def consume(_lo, _hi, C):   # C's row panel is complete here; count it and let it go
-            nnz[0] += C.nnz
+        def consume(_lo, _hi, C):   # count C's row panel and let it go (its last copies may still be running:
+            nnz[0] += C.nnz         # every write ends inside the step's closing synchronise)
 
         def consume_check(_lo, _hi, C):   # setup run only (untimed): observe every panel
             check["panels"] += 1
@@ -177,7 +177,7 @@ def run_rmat(comm, args):
             consume(_lo, _hi, C)
 
         prob.step(comm, info, consume_check)
-        step = lambda: prob.step(comm, None, consume)  # noqa: E731
+        step = lambda: prob.step(comm, None, consume, overlap=True)  # noqa: E731
     else:
         C = prob.step(comm, info)
         check.update(panels=1, sum_val=float(C.val.double().sum()), sum_col=int(C.col.long().sum()))
@@ -359,6 +359,12 @@ def main() -> None:
     from spmm_amd.parallel import comm as CM
 
     comm = CM.init(backend=args.backend, device="auto")
+    if comm.device.type == "cuda" and args.workload == "rmat":
+        # the pipelined one-pass's side stream, created before any other stream of this process
+        # (HIP hands streams hardware queues round-robin: a late one can share the main queue)
+        from spmm_amd.ops import spgemm as _SG
+
+        _SG._side_stream(comm.device)
     if comm.world != args.gpus:
         print(f"[bench] process group has {comm.world} rank(s), --gpus {args.gpus}", file=sys.stderr, flush=True)
         sys.exit(2)

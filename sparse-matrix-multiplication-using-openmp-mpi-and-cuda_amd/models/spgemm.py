@@ -576,14 +576,21 @@ def stream_panels(nprod: torch.Tensor, budget: int) -> List[Tuple[int, int]]:
 
 
 def streamed_spgemm(A: CSR, B: CSR, consume: Callable[[int, int, CSR], None], budget: Optional[int] = None,
-                    info: Optional[SpgemmInfo] = None) -> SpgemmInfo:
+                    info: Optional[SpgemmInfo] = None, overlap: bool = False) -> SpgemmInfo:
     """C = A . B produced in row panels and handed to ``consume(lo, hi,
     C[lo:hi])`` one at a time, so C never has to be resident: R-MAT scale-24
     A.A^T has ~10^12 intermediate products and a C of several TB, more than
     8 x 288 GB of HBM.  Every panel is a complete SpGEMM of A's rows lo..hi
     against all of B (nothing is skipped); only C's lifetime is bounded.  The
     reference bounds its device footprint the same way, with rounds of <= 500
-    output tiles copied back to the host (sparse_matrix_mult.cu:181-270)."""
+    output tiles copied back to the host (sparse_matrix_mult.cu:181-270).
+
+    ``overlap``: a panel is handed to ``consume`` while its last copies (the
+    compaction and the long-row placement, on the side stream) may still be
+    writing its column / value arrays -- its row pointer and nnz are final --
+    so the next panel's planning and kernels overlap them; a consumer that
+    reads C's arrays first calls ``ops.spgemm.wait_ready(C)``.  Every product
+    and every write still happens (a device synchronise covers them all)."""
     info = info if info is not None else SpgemmInfo()
     from ..ops.spgemm import row_nprod
 
@@ -594,7 +601,13 @@ def streamed_spgemm(A: CSR, B: CSR, consume: Callable[[int, int, CSR], None], bu
         lo, hi = todo.pop()
         pi = SpgemmInfo()
         try:
-            C = spgemm(A.row_slice(lo, hi), B, pi)
+            if overlap:
+                from ..ops.spgemm import deferred_placement
+
+                with deferred_placement():
+                    C = spgemm(A.row_slice(lo, hi), B, pi)
+            else:
+                C = spgemm(A.row_slice(lo, hi), B, pi)
         except torch.OutOfMemoryError:
             # the budget was a forecast: split the panel and go on with a
             # smaller budget (a single row that does not fit is a real limit)
@@ -840,13 +853,14 @@ class RmatProblem:
         return allgather_operand(self.At, comm)
 
     def step(self, comm: Comm, info: Optional[SpgemmInfo] = None,
-             consume: Optional[Callable[[int, int, CSR], None]] = None) -> Optional[CSR]:
+             consume: Optional[Callable[[int, int, CSR], None]] = None, overlap: bool = False) -> Optional[CSR]:
         """One product: C_r = A_r . A^T with A^T all-gathered inside the step.
         Resident (returns C_r, the gather overlapping the row planning) or,
-        with ``consume``, streamed in row panels (returns None)."""
+        with ``consume``, streamed in row panels (returns None; ``overlap``:
+        see :func:`streamed_spgemm`)."""
         if consume is None:
             return rowblock_spgemm(self.A, self.At, comm, info)
-        streamed_spgemm(self.A, self.right_operand(comm), consume, info=info)
+        streamed_spgemm(self.A, self.right_operand(comm), consume, info=info, overlap=overlap)
         return None
 
 

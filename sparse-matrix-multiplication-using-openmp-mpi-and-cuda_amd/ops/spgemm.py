@@ -599,13 +599,39 @@ def onepass(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None)
     Cci = torch.empty(nnz, dtype=torch.int32, device=dev)
     Cv = torch.empty(nnz, dtype=torch.float32, device=dev)
     P = _native.ptr
-    stream = _native.stream_ptr(dev)
-    _native.check(_native.hip().spmm_spgemm_compact(P(ub), P(rowptr), m, P(Uci), P(Uv), P(Cci), P(Cv), stream),
-                  "spgemm_compact")
-    del Uci, Uv
-    place_long(deferred, rowptr, Cci, Cv, stream)
-    del deferred
-    return _finish(CSR(m, B.n, rowptr, Cci, Cv), flags, info)
+    # (deferred_placement: the two copies below -- compaction of the LDS-bin rows, placement
+    # of the hub rows -- run on the side stream and the product returns at once; R-MAT's
+    # streamed panels: ~12 ms of copies a panel beside the next panel's planning)
+    defer = getattr(_DEFER, "on", False) and dev.type == "cuda"
+    sA = torch.cuda.current_stream(dev) if defer else None
+    sB = _side_stream(dev) if defer else None
+    if defer:
+        sB.wait_stream(sA)
+    with torch.cuda.stream(sB) if defer else _nullctx():
+        stream = _native.stream_ptr(dev)
+        _native.check(_native.hip().spmm_spgemm_compact(P(ub), P(rowptr), m, P(Uci), P(Uv), P(Cci), P(Cv), stream),
+                      "spgemm_compact")
+        place_long(deferred, rowptr, Cci, Cv, stream)
+    C_ = CSR(m, B.n, rowptr, Cci, Cv)
+    if defer:
+        for t in (ub, rowptr, Uci, Uv, Cci, Cv, *[x for d in deferred for x in d]):
+            t.record_stream(sB)
+        ready = torch.cuda.Event()
+        ready.record(sB)
+        if bool(((flags & 1) != 0).any()):   # rows to re-sort (_finish, on this stream): C complete first
+            sA.wait_event(ready)
+        else:
+            C_.ready = ready
+    del Uci, Uv, deferred
+    return _finish(C_, flags, info)
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
 
 
 ORDERED_MAX_LIGHT = 0.05           # ordered mode: at most this share of non-empty rows below the ESC bins
@@ -1020,12 +1046,48 @@ _SIDE = {}
 
 def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
     """One side stream per (device, thread): loopback ranks are threads that
-    share a device, and must not interleave their pipelines on one stream."""
+    share a device, and must not interleave their pipelines on one stream.
+    High priority: HIP maps streams onto its GPU_MAX_HW_QUEUES hardware queues
+    round-robin, and a side stream that lands on the main stream's queue runs
+    strictly after it (an R-MAT kernel trace showed every kernel of both on one
+    queue); a different priority is a different queue."""
     key = (dev.index, threading.get_ident())
     s = _SIDE.get(key)
     if s is None:
-        s = _SIDE[key] = torch.cuda.Stream(dev)
+        s = _SIDE[key] = torch.cuda.Stream(dev, priority=-1)
     return s
+
+
+_DEFER = threading.local()
+
+
+class deferred_placement:
+    """Inside this context the pipelined one-pass returns a product before its
+    side-stream work -- the compaction and the long-row placement of its last
+    chunk -- has finished: the row pointer and nnz are final, the column /
+    value arrays are complete once the CSR's ``ready`` event has passed
+    (:func:`wait_ready`).  Every kernel still runs; the caller's next work on
+    the main stream (the next streamed panel's planning and kernels) overlaps
+    the copy instead of waiting for it (``models.spgemm.streamed_spgemm``,
+    ``overlap=True``)."""
+
+    def __enter__(self):
+        self._prev = getattr(_DEFER, "on", False)
+        _DEFER.on = True
+        return self
+
+    def __exit__(self, *exc):
+        _DEFER.on = self._prev
+        return False
+
+
+def wait_ready(C_: CSR, stream=None) -> CSR:
+    """Make ``stream`` (default: the current one) wait until ``C_``'s arrays are
+    complete (a product formed under :class:`deferred_placement`)."""
+    ev = getattr(C_, "ready", None)
+    if ev is not None:
+        (stream if stream is not None else torch.cuda.current_stream(C_.rowptr.device)).wait_event(ev)
+    return C_
 
 
 def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_ready=None) -> Optional[CSR]:
@@ -1082,6 +1144,8 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
     sB.wait_stream(sA)
     free = [None, None]
     off = hist[0]
+    defer = getattr(_DEFER, "on", False)
+    rp_done, ok = None, False
     try:   # the side stream may still read this call's buffers: drain it even on an error
         for c in range(nch):
             lo, hi = bounds[c], bounds[c + 1]
@@ -1118,6 +1182,9 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
                 sB.wait_event(done)
                 torch.cumsum(out_nnz[lo:hi], 0, dtype=torch.int64, out=rowptr[lo + 1:hi + 1])
                 rowptr[lo + 1:hi + 1] += rowptr[lo]
+                if defer and c == nch - 1:   # the row pointer is final here, before the copies
+                    rp_done = torch.cuda.Event()
+                    rp_done.record(sB)
                 _native.check(lib.spmm_spgemm_compact(P(ub_rel) + 8 * lo, P(rowptr) + 8 * lo, hi - lo, P(sci), P(sv),
                                                       P(Cci), P(Cv), sB.cuda_stream), "spgemm_compact(pipelined)")
                 for d in deferred:   # allocated on sA, last read on sB
@@ -1127,11 +1194,29 @@ def onepass_pipelined(A: CSR, B: CSR, nprod: torch.Tensor, info: SpgemmInfo, B_r
                 del deferred
                 free[c % 2] = torch.cuda.Event()
                 free[c % 2].record(sB)
+        ok = True
     finally:
-        sA.wait_stream(sB)
+        if not (ok and defer):
+            sA.wait_stream(sB)
+    ready = None
+    if ok and defer:
+        # return before the last chunk's compaction / placement has finished: the main stream
+        # waits for the row pointer only, and every buffer the side stream still touches
+        # stays out of the allocator's reach until it has passed
+        sA.wait_event(rp_done)
+        ready = torch.cuda.Event()
+        ready.record(sB)
+        for t in (out_nnz, rowptr, ub_rel, Cci, Cv, *[x for st in stage for x in st]):
+            t.record_stream(sB)
     nnz = int(rowptr[-1])
     info.nnz = nnz
-    return _finish(CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz]), flags, info)
+    C_ = CSR(m, B.n, rowptr, Cci[:nnz], Cv[:nnz])
+    if ready is not None:
+        if bool(((flags & 1) != 0).any()):   # rows to re-sort (_finish, on this stream): C complete first
+            sA.wait_event(ready)
+        else:
+            C_.ready = ready
+    return _finish(C_, flags, info)
 
 
 def _finish(C_: CSR, flags: torch.Tensor, info: SpgemmInfo, counts=None) -> CSR:

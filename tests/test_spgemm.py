@@ -281,6 +281,44 @@ def test_spgemm_gpu_pipelined_onepass_matches_plain(monkeypatch, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["on", "off"])
+def test_streamed_spgemm_gpu_overlap_panels_equal(monkeypatch, pipeline):
+    """Streamed panels with ``overlap=True`` (each panel's last compaction and
+    long-row placement still running on the side stream when it is handed
+    over; the consumer waits on its ``ready`` event) equal the panels of the
+    serialised flow, hub rows included."""
+    from spmm_amd.models import spgemm as MS
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    A = gen_csr.rmat_csr(13, 16, seed=33, device=dev)
+    B = A.transpose()
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", "on")
+    monkeypatch.setattr(CONFIG, "spgemm_pipeline", pipeline)   # (off: the plain one-pass, R-MAT 24's panels)
+    monkeypatch.setattr(SG, "PIPE_MIN_PRODUCTS", 1 << 20)
+    monkeypatch.setattr(SG, "PIPE_CHUNK_PRODUCTS", 1 << 22)
+    budget = max(int(SG.row_nprod(A, B).sum()) // 4, 1 << 21)
+    out = {}
+    for overlap in (False, True):
+        got = []
+
+        def consume(lo, hi, C, got=got):
+            got.append((lo, hi, getattr(C, "ready", None) is not None))
+            SG.wait_ready(C)
+            got.append((C.rowptr.clone(), C.col.clone(), C.val.clone()))
+
+        MS.streamed_spgemm(A, B, consume, budget=budget, overlap=overlap)
+        torch.cuda.synchronize()
+        out[overlap] = got
+    assert len(out[True]) == len(out[False]) >= 4
+    assert any(g[2] for g in out[True][0::2]) and not any(g[2] for g in out[False][0::2])
+    for (p1, c1), (p2, c2) in zip(zip(out[False][0::2], out[False][1::2]), zip(out[True][0::2], out[True][1::2])):
+        assert p1[:2] == p2[:2]
+        assert torch.equal(c1[0], c2[0]) and torch.equal(c1[1], c2[1])
+        assert torch.allclose(c1[2], c2[2], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("onepass", ["on", "off"])
 def test_spgemm_gpu_long_rows_keep_cancelled_and_signed_zero_entries(monkeypatch, onepass):
     """Hub rows (HBM long-row path) whose products cancel exactly or are -0.0

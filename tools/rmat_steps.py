@@ -15,6 +15,10 @@ from spmm_amd.parallel import comm as CM  # noqa: E402
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 comm = CM.init(backend="auto", device="auto")
+if comm.device.type == "cuda":   # the side stream first (see bench.py)
+    from spmm_amd.ops import spgemm as SG  # noqa: E402
+
+    SG._side_stream(comm.device)
 sync = torch.cuda.synchronize if comm.device.type == "cuda" else (lambda: None)
 t = time.time()
 prob = MS.RmatProblem.build(scale, 16, comm, seed=1)
@@ -28,6 +32,6 @@ for s in range(steps):
 
     sync()
     t = time.time()
-    prob.step(comm, None, consume)
+    prob.step(comm, None, consume, overlap=os.environ.get("RMAT_OVERLAP", "1") == "1")
     sync()
     print(f"step {s}: {(time.time() - t) * 1e3:.1f} ms nnz {nnz[0]}", flush=True)
