@@ -329,6 +329,13 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
     nwg_h = np.maximum((na_h + epw - 1) // epw, 1)
     bad = torch.zeros(1, dtype=torch.int64, device=dev)   # rows whose counts disagree (device-side)
     nil = None
+    # Side stream: a batch's accumulation (long_dense / long_rank: LDS-bound) and what follows
+    # it run on the side stream, so the next batch's routing passes (HBM-write-bound) run
+    # beside them on the main one; the main stream waits for the side one before returning
+    sA = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    side = (sA is not None and CONFIG.spgemm_long_side and int(stream or 0) == int(sA.cuda_stream))
+    sB = _side_stream(dev) if side else None
+    bad_b = torch.zeros(1, dtype=torch.int64, device=dev) if side else bad   # (written on the side stream)
     start, done = 0, 0
     while start < nrows:
         # batch = the longest run of rows from start whose products fit cap (at least one row)
@@ -397,31 +404,42 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
         rt_cnt = T.reshape(-1)
         if LONG_STATS is not None:
             _long_stats(rt_cnt + D.reshape(-1) if direct else rt_cnt)
-        rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
-        lists = torch.empty(2 * R * nch + 4, dtype=torch.int32, device=dev)   # the two kernels' item lists + counters
-        _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
-                                                 P(lists), P(D) if direct else nil, P(dl) if direct else nil,
-                                                 P(dl_rp) if direct else nil, P(btab) if direct else nil,
-                                                 P(B.col) if direct else nil, P(B.val) if direct else nil, stream),
-                      "long_dense")
-        del lists
+        if side:   # this batch's routed scratch is complete on the main stream
+            sB.wait_stream(sA)
+            for t in (rb, rt_off, T, scratch, *((D, dl, dl_rp, dl_off, mode) if direct else ())):
+                t.record_stream(sB)
+        with torch.cuda.stream(sB) if side else _nullctx():
+            st = sB.cuda_stream if side else stream
+            rt_nnz = torch.empty(R * nch, dtype=torch.int64, device=dev)
+            lists = torch.empty(2 * R * nch + 4, dtype=torch.int32, device=dev)   # the two kernels' item lists + counters
+            _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
+                                                     P(lists), P(D) if direct else nil, P(dl) if direct else nil,
+                                                     P(dl_rp) if direct else nil, P(btab) if direct else nil,
+                                                     P(B.col) if direct else nil, P(B.val) if direct else nil, st),
+                          "long_dense")
+            del lists
+            nnz_rt = rt_nnz.view(R, nch)
+            nnz_r = nnz_rt.sum(1)
+            if expect_nnz is not None:
+                bad_b += nnz_r.ne(expect_nnz[rb].long()).sum()
+            if out_nnz is not None:
+                out_nnz[rb] = nnz_r.to(out_nnz.dtype)
+            if values and defer is not None:
+                defer.append((rb, rt_off, rt_nnz, scratch))
+            elif values:
+                dst = (Crp[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
+                _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
+                                                         P(Cv), st), "long_place")
+        if side and values and defer is not None:
+            rt_nnz.record_stream(sA)   # (allocated on the side stream, read by the caller's placement)
         if direct:
             del dl, dl_rp, dl_off, mode
-        nnz_rt = rt_nnz.view(R, nch)
-        nnz_r = nnz_rt.sum(1)
-        if expect_nnz is not None:
-            bad += nnz_r.ne(expect_nnz[rb].long()).sum()
-        if out_nnz is not None:
-            out_nnz[rb] = nnz_r.to(out_nnz.dtype)
-        if values and defer is not None:
-            defer.append((rb, rt_off, rt_nnz, scratch))
-        elif values:
-            dst = (Crp[rb][:, None] + torch.cumsum(nnz_rt, 1) - nnz_rt).reshape(-1).contiguous()
-            _native.check(lib.spmm_spgemm_long_place(P(rt_off), P(dst), P(rt_nnz), R * nch, P(scratch), P(Cci),
-                                                     P(Cv), stream), "long_place")
         del scratch
         done = int(csum_h[end - 1])
         start = end
+    if side:
+        sA.wait_stream(sB)
+        bad += bad_b
     nbad = int(bad)
     if nbad:
         raise RuntimeError(f"spgemm long rows: routing histogram or numeric count disagrees with the product / "

@@ -77,6 +77,8 @@ class Config:
     # test suite sets 120 s (tests/conftest.py).  The native a4 separates the
     # two: an MPI arrival handshake first, then a 120 s bound on the RCCL
     # transfer alone (csrc/runtime/comm.cpp RcclComm::arrive)
+    # long-row path: each batch's accumulation on the side stream, beside the next batch's routing
+    spgemm_long_side: int = field(default_factory=lambda: _env("SPMM_SPGEMM_LONG_SIDE", 1, int))
     comm_timeout_s: float = field(default_factory=lambda: _env("SPMM_COMM_TIMEOUT", 600.0, float))
 
     def as_dict(self) -> dict:

@@ -281,6 +281,31 @@ def test_spgemm_gpu_pipelined_onepass_matches_plain(monkeypatch, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("onepass", ["on", "off"])
+def test_spgemm_gpu_long_rows_side_stream_equal(monkeypatch, onepass):
+    """The long-row batches' accumulation on the side stream (beside the next
+    batch's routing; several batches forced by a small scratch budget) gives
+    the same CSR as the serialised flow, one-pass and two-phase."""
+    from spmm_amd.utils.config import CONFIG
+
+    dev = torch.device("cuda")
+    A = gen_csr.rmat_csr(13, 16, seed=35, device=dev)
+    B = A.transpose()
+    monkeypatch.setattr(CONFIG, "spgemm_onepass", onepass)
+    monkeypatch.setattr(CONFIG, "spgemm_bitmap", "off")
+    monkeypatch.setattr(SG, "GLOBAL_WS_BYTES", 1 << 22)   # many small long-row batches
+    out = []
+    for side in (0, 1):
+        monkeypatch.setattr(CONFIG, "spgemm_long_side", side)
+        info = SG.SpgemmInfo()
+        out.append((SG.spgemm(A, B, info), info))
+    (C0, i0), (C1, i1) = out
+    assert i0.rows_per_bin_num.get(SG.NUM_GLOBAL, 0) > 0   # hub rows took the long-row path
+    assert torch.equal(C0.rowptr, C1.rowptr) and torch.equal(C0.col, C1.col)
+    assert torch.allclose(C0.val, C1.val, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pipeline", ["on", "off"])
 def test_streamed_spgemm_gpu_overlap_panels_equal(monkeypatch, pipeline):
     """Streamed panels with ``overlap=True`` (each panel's last compaction and
