@@ -2228,8 +2228,11 @@ SPMM_EXPORT int spmm_spgemm_long_btab(const int64_t* Brp, const int32_t* Bci, co
 SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_cnt, int64_t nrt, int nch,
                                        void* scratch, int64_t* rt_nnz, int32_t* ws, const int64_t* dt_cnt,
                                        const void* dl, const int64_t* dl_rp, const uint32_t* btab, const int32_t* Bci,
-                                       const float* Bv, void* stream) {
+                                       const float* Bv, int grid_pct, void* stream) {
   // ws: 2 * nrt + 4 int32 (the two work lists, their lengths and long_dense's item ticket counter)
+  // grid_pct: share (percent) of the resident capacity the two persistent grids take -- less than
+  // all when another stream's kernels (the next batch's routing) run beside them (R-MAT 24:
+  // 75 % = 11.46-11.48 s, 100 % = 11.94, 50 % = 13.13; PERF_LOG round 6)
   // direct products (optional): dt_cnt per item, dl / dl_rp the batch rows'
   // long entries (long_route), btab, B
   if (nrt <= 0) return 0;
@@ -2250,6 +2253,7 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
     const char* e = getenv("SPMM_LONG_RANK");
     return e && e[0] == '0' ? 0 : 1;
   }();
+  const int64_t gpct = grid_pct < 1 || grid_pct > 100 ? 100 : grid_pct;
   int32_t* nl = ws;
   int32_t* ticket = ws + 2;
   int32_t* rank_list = ws + 4;
@@ -2261,7 +2265,8 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
   SPMM_LAUNCH_CHECK();
   // persistent grids at the resident capacity (list lengths are device-side)
   if (use_rank) {
-    const unsigned rgrid = (unsigned)std::min<int64_t>((nrt + LR_WAVES - 1) / LR_WAVES, (values ? 3 : 8) * (int64_t)ncu);
+    const unsigned rgrid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((nrt + LR_WAVES - 1) / LR_WAVES, (values ? 3 : 8) * (int64_t)ncu * gpct / 100));
     if (values)
       hipLaunchKernelGGL(long_rank<true>, dim3(rgrid), dim3(LR_WAVES * 64), 0, s, rank_list, nl, rt_off, rt_cnt, nch,
                          (unsigned long long*)scratch, rt_nnz);
@@ -2273,7 +2278,7 @@ SPMM_EXPORT int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const 
   auto launch = [&](auto kern) {
     int per = 0;   // resident workgroups per CU (LDS-bound with values: 132 KB at W = 2^15)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, LONG_DNT, 0) != hipSuccess || per <= 0) per = 1;
-    const unsigned grid = (unsigned)std::min<int64_t>(nrt, (int64_t)per * ncu);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nrt, (int64_t)per * ncu * gpct / 100));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(LONG_DNT), 0, s, dense_list, nl + 1, rt_off, rt_cnt, nch,
                        (unsigned long long*)scratch, rt_nnz, dt_cnt, (const uint4*)dl, dl_rp, btab, Bci, Bv, ticket);
   };

@@ -34,7 +34,7 @@ int spmm_spgemm_long_wg_scan(int32_t* wg_hist, const int64_t* wg0, const int64_t
 int spmm_spgemm_long_dense(int values, const int64_t* rt_off, const int64_t* rt_cnt, int64_t nrt, int nch,
                            void* scratch, int64_t* rt_nnz, int32_t* ws, const int64_t* dt_cnt, const void* dl,
                            const int64_t* dl_rp, const uint32_t* btab, const int32_t* Bci, const float* Bv,
-                           void* stream);
+                           int grid_pct, void* stream);
 int spmm_spgemm_long_place(const int64_t* src, const int64_t* dst, const int64_t* cnt, int64_t nrt,
                            const void* scratch, int32_t* Cci, float* Cv, void* stream);
 int spmm_spgemm_long_params(int* lgw, int* epw, int* maxch);
@@ -247,7 +247,7 @@ void long_rows(int values, const DCsr& A, const DCsr& B, const std::vector<int32
     DevBuf<int64_t> rt_nnz((size_t)R * nch, s);
     DevBuf<int32_t> lists((size_t)2 * R * nch + 4, s);
     A4_HIP((hipError_t)spmm_spgemm_long_dense(values, drt_off.get(), T.get(), R * nch, nch, scratch.get(), rt_nnz.get(),
-                                              lists.get(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s));
+                                              lists.get(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 100, s));
     const std::vector<int64_t> nz = down(rt_nnz.get(), (size_t)R * nch, s);
     if (!values) {
       for (int64_t i = 0; i < R; ++i) {

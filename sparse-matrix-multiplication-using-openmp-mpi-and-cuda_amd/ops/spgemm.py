@@ -53,7 +53,7 @@ _native.register_hip("spmm_spgemm_long_route", C_INT, c_vp, c_vp, c_vp, c_vp, c_
 _native.register_hip("spmm_spgemm_long_wg_scan", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_btab", c_vp, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_dense", C_INT, c_vp, c_vp, C_I64, C_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                     c_vp, c_vp, c_vp)
+                     c_vp, c_vp, C_INT, c_vp)
 _native.register_hip("spmm_spgemm_long_place", c_vp, c_vp, c_vp, C_I64, c_vp, c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_long_params", c_vp, c_vp, c_vp)
 _native.register_hip("spmm_spgemm_esc_ordered", c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C_I64, C_INT,
@@ -285,6 +285,12 @@ def _long_btab(B: CSR, nch: int):
     return out
 
 
+# long_dense / long_rank grids on the side stream, beside the next batch's routing: this share
+# (percent) of their resident capacity (R-MAT 24: 75 -> 11.46-11.48 s, 70 -> 11.59, 80 -> 11.89,
+# 100 -> 11.94, 50 -> 13.13; PERF_LOG round 6)
+LONG_SIDE_GRID_PCT = 75
+
+
 def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torch.Tensor, stream,
                out_nnz: Optional[torch.Tensor] = None, Crp=None, Cci=None, Cv=None,
                expect_nnz: Optional[torch.Tensor] = None, defer: Optional[list] = None) -> None:
@@ -415,7 +421,8 @@ def _long_rows(values: int, A: CSR, B: CSR, rows: torch.Tensor, nprod_rows: torc
             _native.check(lib.spmm_spgemm_long_dense(values, P(rt_off), P(rt_cnt), R * nch, nch, P(scratch), P(rt_nnz),
                                                      P(lists), P(D) if direct else nil, P(dl) if direct else nil,
                                                      P(dl_rp) if direct else nil, P(btab) if direct else nil,
-                                                     P(B.col) if direct else nil, P(B.val) if direct else nil, st),
+                                                     P(B.col) if direct else nil, P(B.val) if direct else nil,
+                                                     LONG_SIDE_GRID_PCT if side else 100, st),
                           "long_dense")
             del lists
             nnz_rt = rt_nnz.view(R, nch)
